@@ -1,0 +1,108 @@
+/*
+ * sirconv.h — C ABI of the MI355X (gfx950) SIRConv edge-aggregation kernels.
+ *
+ * This is the drop-in boundary for the hot path of briangodwinlim/SIR-GCN `SIRConv`
+ * (models/conv.py:7-67).  In the reference the path is
+ *     graph.update_all(self.message_func, self._agg_func('m', 'ft'))      conv.py:63
+ * with the edge UDF  m = out_norm[u] * in_norm[v] * sigma(eq[v] + ek[u])   conv.py:43-45
+ * which DGL 2.1.0 runs as index_select gathers + elementwise + GSpMM(copy_e, sum)
+ * over the in-edge CSC (and, under autograd, gsddmm/index_add for the backward).
+ * The three entry points below replace exactly that: the forward aggregation and the
+ * two halves of its backward.  Everything around them (the nn.Linear projections
+ * conv.py:60-61,65, degrees/norms conv.py:51-57) stays with the host (PyTorch on ROCm).
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers; all work is enqueued on `stream` (a hipStream_t,
+ *    NULL = default stream); calls are asynchronous, stateless and reentrant.
+ *  - The caller owns every buffer.  Outputs are fully overwritten (no pre-zeroing).
+ *  - Row-major feature matrices with explicit leading dimensions (elements).
+ *  - Graph structure is a "row CSR": rows are the nodes being reduced INTO, `col` holds the
+ *    node at the other end of each edge, edges of a row are in ascending edge id
+ *    (DGL's stable CSC order).  int32 indices (valid while E < 2^31).
+ *  - Work plan: `items` = int32[n_items][4] {row, e_begin, e_end, slot}; every row appears
+ *    in >= 1 item; a row longer than the plan's chunk is split over several items with
+ *    slot >= 0 (partial-sum slot), unsplit rows have slot = -1.  `splits` =
+ *    int32[n_splits][4] {row, slot_begin, n_slots, degree} for the split rows, combined in
+ *    slot order (deterministic, no atomics).  `partial` = float[n_slots_total * H] scratch.
+ *  - Return 0 on success, otherwise an SIR_E* code; sir_last_error() gives the text
+ *    (thread-local).
+ */
+#ifndef SIRCONV_H
+#define SIRCONV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIR_ABI_VERSION 1
+
+/* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
+enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
+/* sigma: the `activation` callable of conv.py:32,45 (ReLU, LeakyReLU(slope), GELU erf / tanh) */
+enum { SIR_ACT_IDENTITY = 0, SIR_ACT_RELU = 1, SIR_ACT_LEAKY_RELU = 2, SIR_ACT_GELU = 3, SIR_ACT_GELU_TANH = 4 };
+/* storage dtype of the gathered node features */
+enum { SIR_DTYPE_F32 = 0, SIR_DTYPE_BF16 = 1 };
+/* error codes */
+enum { SIR_OK = 0, SIR_EINVAL = 1, SIR_EUNSUPPORTED = 2, SIR_ELAUNCH = 3 };
+
+int sir_abi_version(void);
+const char* sir_last_error(void);
+
+/*
+ * Forward edge aggregation — replaces conv.py:63 (update_all with the sum/mean/sym UDF).
+ *   S[v] = sum_{e in row v} c_e * sigma(Q[v] + K[col[e]]),  c_e = norm_col[u] * norm_row[v]
+ *   (SYM only; SUM/MEAN use c_e = 1 exactly as ones*ones in conv.py:45), MEAN divides by
+ *   max(degree, 1) afterwards (DGL fn.mean).  Rows with no edges get S = 0.
+ *   rowptr/col: row CSR by destination (rows = dst nodes, col = src node ids).
+ *   Q: [n_rows, H] (ldq) indexed by row;  K: [*, H] (ldk) indexed by col.
+ *   norm_row / norm_col: fp32 (SYM only, else may be NULL).
+ */
+int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
+                     const int32_t* items, int64_t n_items,
+                     const int32_t* splits, int64_t n_splits,
+                     int64_t H, int dtype,
+                     const void* Q, int64_t ldq, const void* K, int64_t ldk,
+                     const float* norm_row, const float* norm_col,
+                     int agg, int act, float slope,
+                     float* S, int64_t lds, float* partial, void* stream);
+
+/*
+ * Backward, destination pass — the Q half of autograd through conv.py:45,63.
+ *   g = G[v] (MEAN: G[v] / max(deg v, 1)),  t_e = g * c_e (SYM) or g,
+ *   dQ[v] = sum_{e in row v} sigma'(Q[v] + K[u]) * t_e   (sigma' as torch's backward).
+ *   If MEAN and Gm != NULL, the divided rows g are also written to Gm (for the src pass).
+ */
+int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
+                         const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits,
+                         int64_t H, int dtype,
+                         const void* Q, int64_t ldq, const void* K, int64_t ldk,
+                         const float* G, int64_t ldg,
+                         const float* norm_row, const float* norm_col,
+                         int agg, int act, float slope,
+                         float* dQ, int64_t lddq, float* Gm, int64_t ldgm,
+                         float* partial, void* stream);
+
+/*
+ * Backward, source pass — the K half (replaces the index_add of conv.py:45's src gather).
+ *   Row CSR by SOURCE: rows = src nodes u, col = dst node ids v (ascending edge id).
+ *   dK[u] = sum_{e in row u} sigma'(Q[v] + K[u]) * t_e,  t_e = Gd[v] * c_e (SYM) or Gd[v],
+ *   where Gd is the already-divided gradient (MEAN: the Gm of the dst pass; else G).
+ *   norm_row = out-norm of u, norm_col = in-norm of v (SYM only).
+ */
+int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s,
+                         const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits,
+                         int64_t H, int dtype,
+                         const void* K, int64_t ldk, const void* Q, int64_t ldq,
+                         const float* Gd, int64_t ldg,
+                         const float* norm_row, const float* norm_col,
+                         int agg, int act, float slope,
+                         float* dK, int64_t lddk, float* partial, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIRCONV_H */

@@ -1,0 +1,191 @@
+"""CPU restatement of the reference SIRConv layer (TEST INFRASTRUCTURE ONLY).
+
+Reference: briangodwinlim/SIR-GCN ``models/conv.py:7-67`` (snapshot 2025-08-24), whose sparse
+part runs inside DGL 2.1.0 (absent; its behaviour is restated from its published source, see
+``tests/golden/dgl_shim``).  Each function cites the reference line it follows.
+
+Two flavours live here:
+
+* kernel-level functions (``edge_agg_fwd`` / ``edge_agg_bwd``) that compute exactly what the
+  HIP edge kernels compute, given Q, K, dS -> S, dQ, dK; used by the GPU parity tests;
+* ``reference_cpu_step`` — the reference's CPU dataflow (DGL edge-UDF path: ``index_select``
+  gathers -> add -> sigma -> norm product -> ``index_add`` -> W_R) with torch autograd for the
+  backward; this is the ``cpu_baseline`` timed by ``bench.py`` ("port") and the whole-layer
+  checker (``layer_fwd_bwd``).
+
+Everything is torch-CPU (or numpy for the integer CSR work); no GPU, no product imports.
+"""
+import math
+
+import numpy as np
+import torch
+
+AGGS = ("sum", "mean", "sym")
+ACTS = ("identity", "relu", "leaky", "gelu", "gelu_tanh")
+
+
+# ----------------------------------------------------------------------------- graph
+def csr_by_dst(src, dst, num_nodes):
+    """In-edge CSR (DGL's CSC): rows = dst, ``col`` = src, ``eid`` ascending inside a row.
+
+    [DGL-ext] DGL builds CSC by a stable sort of COO by dst (edge-id order kept), which is
+    the order ``SpMMSumCsr`` accumulates in (``conv.py:63`` -> gspmm).  Bit-exact target.
+    """
+    src = np.asarray(src, dtype=np.int64)
+    dst = np.asarray(dst, dtype=np.int64)
+    eid = np.argsort(dst, kind="stable").astype(np.int64)
+    counts = np.bincount(dst, minlength=num_nodes).astype(np.int64)
+    rowptr = np.zeros(num_nodes + 1, dtype=np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    return rowptr, src[eid], eid
+
+
+def csr_by_src(src, dst, num_nodes):
+    """Out-edge CSR: rows = src, ``col`` = dst, ``eid`` ascending (autograd of the src
+    gather, ``index_add`` in edge order, accumulates dK[u] in exactly this order)."""
+    return csr_by_dst(dst, src, num_nodes)
+
+
+def degree_norms(in_deg, out_deg, agg):
+    """``conv.py:51-57``: clamp(min=1) float degrees; ``sym`` -> deg^-0.5 else ones; fp32."""
+    in_degs = torch.as_tensor(in_deg).float().clamp(min=1)
+    out_degs = torch.as_tensor(out_deg).float().clamp(min=1)
+    n = in_degs.numel()
+    in_norm = torch.pow(in_degs, -0.5) if agg == "sym" else torch.ones(n)
+    out_norm = torch.pow(out_degs, -0.5) if agg == "sym" else torch.ones(n)
+    return in_norm, out_norm
+
+
+# ----------------------------------------------------------------------------- sigma
+def act_fwd(z, act, slope=0.01):
+    if act == "identity":
+        return z
+    if act == "relu":
+        return torch.relu(z)
+    if act == "leaky":
+        return torch.nn.functional.leaky_relu(z, slope)
+    if act == "gelu":
+        return torch.nn.functional.gelu(z)
+    if act == "gelu_tanh":
+        return torch.nn.functional.gelu(z, approximate="tanh")
+    raise ValueError(act)
+
+
+def act_bwd(z, grad, act, slope=0.01):
+    """d sigma(z) * grad, as torch's backward formulas compute it."""
+    if act == "identity":
+        return grad
+    if act == "relu":
+        return torch.where(z > 0, grad, torch.zeros_like(grad))
+    if act == "leaky":
+        return torch.where(z > 0, grad, grad * slope)
+    if act in ("gelu", "gelu_tanh"):
+        zz = z.detach().clone().requires_grad_(True)
+        with torch.enable_grad():
+            y = act_fwd(zz, act)
+            (g,) = torch.autograd.grad(y, zz, grad)
+        return g
+    raise ValueError(act)
+
+
+# ----------------------------------------------------------------------------- kernels
+def _edge_coef(out_norm, in_norm, src, dst, agg):
+    """``conv.py:45``: ``edges.src['out_norm'] * edges.dst['in_norm']`` (fp32 product first)."""
+    if agg == "sym":
+        return (out_norm[src] * in_norm[dst]).unsqueeze(-1)
+    return None
+
+
+def edge_agg_fwd(src, dst, num_nodes, Q, K, agg, act, slope=0.01):
+    """S[v] = sum_{e:u->v} (n_out[u] n_in[v]) * sigma(Q[v] + K[u]); mean divides by deg.
+
+    ``conv.py:43-45`` (message) + ``conv.py:63`` (update_all, fn.sum / fn.mean) restated.
+    Accumulation is ``index_add`` in edge-id order == DGL CPU SpMM order per row.
+    """
+    src = torch.as_tensor(src, dtype=torch.int64)
+    dst = torch.as_tensor(dst, dtype=torch.int64)
+    in_deg = torch.bincount(dst, minlength=num_nodes)
+    out_deg = torch.bincount(src, minlength=num_nodes)
+    in_norm, out_norm = degree_norms(in_deg, out_deg, agg)
+    z = Q.index_select(0, dst) + K.index_select(0, src)
+    m = act_fwd(z, act, slope)
+    c = _edge_coef(out_norm, in_norm, src, dst, agg)
+    if c is not None:
+        m = c * m
+    S = torch.zeros((num_nodes, Q.shape[1]), dtype=m.dtype).index_add_(0, dst, m)
+    if agg == "mean":
+        S = S / in_deg.clamp(1, max(int(src.numel()), 1)).to(S.dtype).unsqueeze(-1)
+    return S
+
+
+def edge_agg_bwd(src, dst, num_nodes, Q, K, dS, agg, act, slope=0.01):
+    """Analytic backward of ``edge_agg_fwd`` (autograd through ``conv.py:45,63``):
+    t_e = (c_e) * g[v] with g = dS (mean: dS / deg), dz_e = sigma'(z_e) t_e,
+    dQ[v] = sum over in-edges (edge order), dK[u] = sum over out-edges (edge order)."""
+    src = torch.as_tensor(src, dtype=torch.int64)
+    dst = torch.as_tensor(dst, dtype=torch.int64)
+    in_deg = torch.bincount(dst, minlength=num_nodes)
+    out_deg = torch.bincount(src, minlength=num_nodes)
+    in_norm, out_norm = degree_norms(in_deg, out_deg, agg)
+    g = dS
+    if agg == "mean":
+        g = dS / in_deg.clamp(1, max(int(src.numel()), 1)).to(dS.dtype).unsqueeze(-1)
+    z = Q.index_select(0, dst) + K.index_select(0, src)
+    t = g.index_select(0, dst)
+    c = _edge_coef(out_norm, in_norm, src, dst, agg)
+    if c is not None:
+        t = t * c
+    dz = act_bwd(z, t, act, slope)
+    H = Q.shape[1]
+    dQ = torch.zeros((num_nodes, H), dtype=dz.dtype).index_add_(0, dst, dz)
+    dK = torch.zeros((num_nodes, H), dtype=dz.dtype).index_add_(0, src, dz)
+    return dQ, dK
+
+
+# ----------------------------------------------------------------------------- layer
+def reference_cpu_step(src, dst, num_nodes, X, W_Q, b_Q, W_K, W_R, b_R, dY, agg, act,
+                       slope=0.01, need_grads=True):
+    """The reference's CPU dataflow for one SIRConv layer, fwd (+ autograd bwd).
+
+    ``conv.py:49-67``: norms (51-57), K = X W_K^T, Q = X W_Q^T + b_Q (59-61),
+    update_all(message_func, agg) (63) as DGL's edge-UDF path runs it (gathers, elementwise,
+    index_add), Y = S W_R^T + b_R (65).  Returns Y and (if ``need_grads``) the gradients.
+    """
+    src = torch.as_tensor(src, dtype=torch.int64)
+    dst = torch.as_tensor(dst, dtype=torch.int64)
+    params = [t.detach().clone().requires_grad_(need_grads) for t in (X, W_Q, b_Q, W_K, W_R, b_R)]
+    X_, W_Q_, b_Q_, W_K_, W_R_, b_R_ = params
+    with torch.set_grad_enabled(need_grads):
+        K = torch.nn.functional.linear(X_, W_K_)
+        Q = torch.nn.functional.linear(X_, W_Q_, b_Q_)
+        S = edge_agg_fwd(src, dst, num_nodes, Q, K, agg, act, slope)
+        Y = torch.nn.functional.linear(S, W_R_, b_R_)
+    out = {"Y": Y.detach()}
+    if need_grads:
+        Y.backward(dY)
+        for name, p in zip(("dX", "dW_Q", "db_Q", "dW_K", "dW_R", "db_R"), params):
+            out[name] = p.grad
+    return out
+
+
+def layer_fwd_bwd(src, dst, num_nodes, X, W_Q, b_Q, W_K, W_R, b_R, dY, agg, act, slope=0.01):
+    """Whole-layer oracle with the analytic backward written out (no autograd), so each
+    gradient formula is explicit."""
+    src = torch.as_tensor(src, dtype=torch.int64)
+    dst = torch.as_tensor(dst, dtype=torch.int64)
+    Q = X @ W_Q.t() + b_Q
+    K = X @ W_K.t()
+    S = edge_agg_fwd(src, dst, num_nodes, Q, K, agg, act, slope)
+    Y = S @ W_R.t() + b_R
+    G = dY @ W_R                                     # dS (mean division inside edge_agg_bwd)
+    dQ, dK = edge_agg_bwd(src, dst, num_nodes, Q, K, G, agg, act, slope)
+    return {
+        "Y": Y, "S": S, "Q": Q, "K": K, "dS": G, "dQ": dQ, "dK": dK,
+        "dX": dQ @ W_Q + dK @ W_K, "dW_Q": dQ.t() @ X, "db_Q": dQ.sum(0),
+        "dW_K": dK.t() @ X, "dW_R": dY.t() @ S, "db_R": dY.sum(0),
+    }
+
+
+def gelu_erf_scalar(x):
+    """Scalar GELU(erf) used by small pure-Python checks."""
+    return 0.5 * x * (1.0 + math.erf(x / math.sqrt(2.0)))

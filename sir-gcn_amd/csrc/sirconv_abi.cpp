@@ -1,0 +1,144 @@
+// sirconv_abi.cpp — the extern "C" boundary declared in include/sirconv.h.
+//
+// Synchronous argument checks, then one (or two, with split rows) asynchronous launches on
+// the caller's stream.  No allocation, no device sync, no hipSetDevice: the caller (the
+// Python host layer) selects the device and owns every buffer.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <string>
+
+#include "sirconv.h"
+#include "sirconv_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fn, const char* msg) {
+    g_last_error = std::string(fn) + ": " + msg;
+    return code;
+}
+
+int check_common(const char* fn, const int32_t* rowptr, const int32_t* col, const int32_t* items,
+                 int64_t n_items, const int32_t* splits, int64_t n_splits, int64_t H, int dtype,
+                 int agg, int act, const float* norm_row, const float* norm_col, const void* out,
+                 const float* partial) {
+    if (dtype != SIR_DTYPE_F32) return fail(SIR_EUNSUPPORTED, fn, "only SIR_DTYPE_F32 storage is implemented");
+    if (agg < SIR_AGG_SUM || agg > SIR_AGG_SYM) return fail(SIR_EINVAL, fn, "agg must be SUM, MEAN or SYM");
+    if (act < SIR_ACT_IDENTITY || act > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown activation");
+    if (H <= 0 || H > 1024) return fail(SIR_EINVAL, fn, "H must be in [1, 1024]");
+    if (n_items < 0 || n_splits < 0) return fail(SIR_EINVAL, fn, "negative item/split count");
+    if (n_items > 0 && (rowptr == nullptr || items == nullptr || out == nullptr))
+        return fail(SIR_EINVAL, fn, "rowptr/items/output must be non-NULL");
+    if (col == nullptr && n_items > 0) return fail(SIR_EINVAL, fn, "col must be non-NULL");
+    if (n_splits > 0 && (splits == nullptr || partial == nullptr))
+        return fail(SIR_EINVAL, fn, "split rows need `splits` and a `partial` workspace");
+    if (agg == SIR_AGG_SYM && n_items > 0 && (norm_row == nullptr || norm_col == nullptr))
+        return fail(SIR_EINVAL, fn, "SYM needs norm_row and norm_col");
+    return SIR_OK;
+}
+
+int finish(const char* fn, hipError_t err, const char* why) {
+    if (err == hipSuccess) return SIR_OK;
+    if (err == hipErrorInvalidValue && why) return fail(SIR_EUNSUPPORTED, fn, why);
+    return fail(SIR_ELAUNCH, fn, hipGetErrorString(err));
+}
+
+}  // namespace
+
+extern "C" {
+
+int sir_abi_version(void) { return SIR_ABI_VERSION; }
+
+const char* sir_last_error(void) { return g_last_error.c_str(); }
+
+int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
+                     const int32_t* items, int64_t n_items,
+                     const int32_t* splits, int64_t n_splits,
+                     int64_t H, int dtype,
+                     const void* Q, int64_t ldq, const void* K, int64_t ldk,
+                     const float* norm_row, const float* norm_col,
+                     int agg, int act, float slope,
+                     float* S, int64_t lds, float* partial, void* stream) {
+    const char* fn = "sir_edge_agg_fwd";
+    int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
+                          norm_row, norm_col, S, partial);
+    if (rc) return rc;
+    if (ldq < H || ldk < H || lds < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+    if (n_items > 0 && (Q == nullptr || K == nullptr)) return fail(SIR_EINVAL, fn, "Q/K must be non-NULL");
+    sir::EdgeArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items;
+    a.R = static_cast<const float*>(Q); a.ldr = ldq;
+    a.C = static_cast<const float*>(K); a.ldc = ldk;
+    a.G = nullptr; a.ldg = H;
+    a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
+    a.out = S; a.ldo = lds; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
+    const char* why = nullptr;
+    hipError_t err = sir::run_edge(sir::MODE_FWD, a, agg, act, splits, n_splits, S, lds,
+                                   agg == SIR_AGG_MEAN, static_cast<hipStream_t>(stream), &why);
+    return finish(fn, err, why);
+}
+
+int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
+                         const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits,
+                         int64_t H, int dtype,
+                         const void* Q, int64_t ldq, const void* K, int64_t ldk,
+                         const float* G, int64_t ldg,
+                         const float* norm_row, const float* norm_col,
+                         int agg, int act, float slope,
+                         float* dQ, int64_t lddq, float* Gm, int64_t ldgm,
+                         float* partial, void* stream) {
+    const char* fn = "sir_edge_agg_bwd_dst";
+    int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
+                          norm_row, norm_col, dQ, partial);
+    if (rc) return rc;
+    if (ldq < H || ldk < H || ldg < H || lddq < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+    if (Gm != nullptr && ldgm < H) return fail(SIR_EINVAL, fn, "ldgm must be >= H");
+    if (n_items > 0 && (Q == nullptr || K == nullptr || G == nullptr))
+        return fail(SIR_EINVAL, fn, "Q/K/G must be non-NULL");
+    sir::EdgeArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items;
+    a.R = static_cast<const float*>(Q); a.ldr = ldq;
+    a.C = static_cast<const float*>(K); a.ldc = ldk;
+    a.G = G; a.ldg = ldg;
+    a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
+    a.out = dQ; a.ldo = lddq; a.partial = partial;
+    a.Gm = (agg == SIR_AGG_MEAN) ? Gm : nullptr; a.ldgm = Gm ? ldgm : H;
+    const char* why = nullptr;
+    hipError_t err = sir::run_edge(sir::MODE_BWD_DST, a, agg, act, splits, n_splits, dQ, lddq, false,
+                                   static_cast<hipStream_t>(stream), &why);
+    return finish(fn, err, why);
+}
+
+int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s,
+                         const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits,
+                         int64_t H, int dtype,
+                         const void* K, int64_t ldk, const void* Q, int64_t ldq,
+                         const float* Gd, int64_t ldg,
+                         const float* norm_row, const float* norm_col,
+                         int agg, int act, float slope,
+                         float* dK, int64_t lddk, float* partial, void* stream) {
+    const char* fn = "sir_edge_agg_bwd_src";
+    int rc = check_common(fn, rowptr_s, col_s, items, n_items, splits, n_splits, H, dtype, agg, act,
+                          norm_row, norm_col, dK, partial);
+    if (rc) return rc;
+    if (ldq < H || ldk < H || ldg < H || lddk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+    if (n_items > 0 && (Q == nullptr || K == nullptr || Gd == nullptr))
+        return fail(SIR_EINVAL, fn, "K/Q/Gd must be non-NULL");
+    sir::EdgeArgs a{};
+    a.rowptr = rowptr_s; a.col = col_s; a.items = items; a.n_items = n_items;
+    a.R = static_cast<const float*>(K); a.ldr = ldk;
+    a.C = static_cast<const float*>(Q); a.ldc = ldq;
+    a.G = Gd; a.ldg = ldg;
+    a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
+    a.out = dK; a.ldo = lddk; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
+    const char* why = nullptr;
+    hipError_t err = sir::run_edge(sir::MODE_BWD_SRC, a, agg, act, splits, n_splits, dK, lddk, false,
+                                   static_cast<hipStream_t>(stream), &why);
+    return finish(fn, err, why);
+}
+
+}  // extern "C"

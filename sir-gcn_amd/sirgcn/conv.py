@@ -1,0 +1,149 @@
+"""Drop-in ``SIRConv`` running its message passing on hand-written gfx950 kernels.
+
+Mirrors briangodwinlim/SIR-GCN ``models/conv.py:7-67``:
+
+* same constructor ``SIRConv(input_dim, hidden_dim, output_dim, activation, dropout=0,
+  inner_bias=True, outer_bias=True, agg_type='sum')`` (``conv.py:32``) and attributes
+  (``activation``, ``dropout``, ``linear_query``, ``linear_key`` (no bias, ``conv.py:37``),
+  ``linear_relation``, ``_agg_type``) -> identical ``state_dict`` keys;
+* same ``forward(graph, feat) -> Tensor[V, output_dim]`` (``conv.py:49``);
+* same numerics: fp32 degree norms (``conv.py:51-57``), message
+  ``(out_norm[u] * in_norm[v]) * sigma(eq[v] + ek[u])`` (``conv.py:45``), sum / mean (= sum /
+  clamp(deg, 1)) / sym aggregation (``conv.py:41,63``), ``Y = W_R S + b_R`` (``conv.py:65``) so
+  isolated destinations output ``b_R``.
+
+What runs where: the two node projections are ONE GEMM against the concatenated [W_Q; W_K]
+(rocBLAS/hipBLASLt through torch), the edge aggregation and its backward are the HIP kernels
+of ``libsirconv.so`` (C ABI, ``include/sirconv.h``), W_R is a torch GEMM.  There is no CPU
+path: a CPU tensor, a missing library or an unsupported sigma/agg raises.
+"""
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from . import _native
+from .graph import DEFAULT_CHUNK, get_plan
+
+
+def activation_code(act):
+    """Map the reference's ``activation`` callable (``conv.py:32,45``) to a kernel code."""
+    if isinstance(act, nn.LeakyReLU):
+        return _native.ACT_LEAKY, float(act.negative_slope)
+    if isinstance(act, nn.ReLU) or act in (torch.relu, F.relu):
+        return _native.ACT_RELU, 0.0
+    if isinstance(act, nn.GELU):
+        return (_native.ACT_GELU_TANH if act.approximate == "tanh" else _native.ACT_GELU), 0.0
+    if act is F.gelu:
+        return _native.ACT_GELU, 0.0
+    if isinstance(act, nn.Identity) or act is None:
+        return _native.ACT_IDENTITY, 0.0
+    if act is F.leaky_relu:
+        return _native.ACT_LEAKY, 0.01
+    raise NotImplementedError(
+        f"SIRConv: activation {act!r} has no native kernel (supported: ReLU, LeakyReLU, GELU, Identity)")
+
+
+class EdgeAggregate(torch.autograd.Function):
+    """S = update_all(message_func, agg) of ``conv.py:63`` on packed ``QK = [Q | K]`` ([V, 2H]).
+
+    Backward returns dQK written by the dst pass (dQ half) and the src pass (dK half)."""
+
+    @staticmethod
+    def forward(ctx, QK, plan, H, agg, act, slope):
+        if QK.device.type != "cuda":
+            raise RuntimeError("SIRConv native path needs a ROCm GPU tensor (no CPU fallback)")
+        ctx.in_dtype = QK.dtype
+        QK = QK.contiguous()
+        if QK.dtype != torch.float32:
+            QK = QK.float()          # fp32 storage kernels (bf16 storage: DESIGN.md next steps)
+        V = QK.shape[0]
+        Q, K = QK[:, :H], QK[:, H:]
+        in_norm, out_norm = plan.norms(agg)
+        S = torch.empty((V, H), device=QK.device, dtype=torch.float32)
+        partial = _partial(plan, H, QK.device)
+        _native.edge_agg_fwd(plan.dst, Q, K, in_norm, out_norm, agg, act, slope, S, partial)
+        ctx.save_for_backward(QK)
+        ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope = plan, H, agg, act, slope
+        return S
+
+    @staticmethod
+    def backward(ctx, dS):
+        (QK,) = ctx.saved_tensors
+        plan, H, agg, act, slope = ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope
+        G = dS.contiguous().float()
+        V = QK.shape[0]
+        dQK = torch.empty_like(QK)
+        in_norm, out_norm = plan.norms(agg)
+        partial = _partial(plan, H, QK.device)
+        Gm = torch.empty((V, H), device=QK.device, dtype=torch.float32) if agg == "mean" else None
+        Q, K = QK[:, :H], QK[:, H:]
+        _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope,
+                                 dQK[:, :H], Gm, partial)
+        _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
+                                 agg, act, slope, dQK[:, H:], partial)
+        return dQK.to(ctx.in_dtype), None, None, None, None, None
+
+
+def _partial(plan, H, device):
+    n = max(plan.dst.n_slots, plan.src.n_slots)
+    return torch.empty((max(n, 1) * H,), device=device, dtype=torch.float32) if n else None
+
+
+class SIRConv(nn.Module):
+    r"""Soft-Isomorphic Relational Graph Convolution (SIR-GCN), MI355X-native.
+
+    .. math::  h_u^* = \sum_{v \in \mathcal{N}(u)} W_R \, \sigma(W_Q h_u + W_K h_v)
+
+    Same parameters as the reference (``conv.py:13-31``).  ``agg_type`` in
+    {``sum``, ``mean``, ``sym``} runs natively; ``max`` is accepted by the constructor for
+    state-dict compatibility but raises at ``forward`` until its kernel lands.
+    """
+
+    def __init__(self, input_dim, hidden_dim, output_dim, activation, dropout=0, inner_bias=True,
+                 outer_bias=True, agg_type='sum'):
+        super().__init__()
+        if agg_type not in ("sum", "mean", "sym", "max"):
+            raise AttributeError(f"module 'dgl.function' has no attribute '{agg_type}'")
+        self.activation = activation
+        self.dropout = nn.Dropout(dropout)
+        self.linear_query = nn.Linear(input_dim, hidden_dim, bias=inner_bias)
+        self.linear_key = nn.Linear(input_dim, hidden_dim, bias=False)
+        self.linear_relation = nn.Linear(hidden_dim, output_dim, bias=outer_bias)
+        self._agg_type = agg_type
+        self.chunk = DEFAULT_CHUNK
+
+    def _project(self, feat_key, feat_query):
+        """K = drop(X W_K^T), Q = drop(X W_Q^T + b_Q) (``conv.py:60-61``) as ONE GEMM -> [V, 2H]."""
+        H = self.linear_query.out_features
+        if feat_key is feat_query:
+            W = torch.cat([self.linear_query.weight, self.linear_key.weight], 0)
+            b = None
+            if self.linear_query.bias is not None:
+                b = torch.cat([self.linear_query.bias, self.linear_query.bias.new_zeros(H)])
+            QK = F.linear(feat_query, W, b)
+        else:
+            QK = torch.cat([self.linear_query(feat_query), self.linear_key(feat_key)], 1)
+        if self.training and self.dropout.p > 0:
+            QK = self.dropout(QK)   # independent masks for Q and K, as two nn.Dropout calls
+        return QK
+
+    def forward(self, graph, feat):
+        if self._agg_type == "max":
+            raise NotImplementedError("SIRConv(agg_type='max'): native kernel not built yet (SURVEY §8f #1)")
+        if isinstance(feat, tuple):          # expand_as_pair: (src feats, dst feats)
+            feat_key, feat_query = feat
+        else:
+            feat_key = feat_query = feat
+        if feat_query.dim() != 2:
+            raise ValueError("SIRConv expects 2-D node features [V, input_dim]")
+        act, slope = activation_code(self.activation)
+        plan = get_plan(graph, feat_query.device, self.chunk)
+        if plan.num_nodes != feat_query.shape[0]:
+            raise ValueError(f"feat has {feat_query.shape[0]} rows, graph has {plan.num_nodes} nodes")
+        H = self.linear_query.out_features
+        QK = self._project(feat_key, feat_query)
+        S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope)
+        return self.linear_relation(S)
+
+    def extra_repr(self):
+        return f"agg_type={self._agg_type!r}"

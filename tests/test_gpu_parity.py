@@ -1,0 +1,209 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the golden vectors produced by the
+reference's own conv.py, against the CPU oracle on random shapes, and against a chunked torch
+fp32 GPU reference at BASELINE size.  Run on the MI355X box:  pytest tests -m gpu
+Tolerances: indexing bit-exact; fp32 ||d||/||ref|| <= 1e-5 and
+allclose(rtol=1e-5, atol=1e-6*max|ref|); unsplit ReLU/LeakyReLU rows bit-exact."""
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+import oracle
+from conftest import assert_close, golden_manifest, load_case, rel_err
+
+import sirgcn
+from sirgcn import _native
+from sirgcn.conv import EdgeAggregate, SIRConv, activation_code
+from sirgcn.graph import Graph, GraphPlan
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CASES = [c for c in golden_manifest() if c["agg"] in ("sum", "mean", "sym") and c["act"] != "seq"]
+ACTS = {"relu": nn.ReLU(), "leaky": nn.LeakyReLU(0.2), "gelu": nn.GELU()}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X box"
+    _native.load()
+
+
+def _t(x, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV, dtype)
+
+
+def _kernel_run(z, case, chunk):
+    V, H = case["V"], case["H"]
+    plan = GraphPlan(torch.from_numpy(z["src"]), torch.from_numpy(z["dst"]), V, DEV, chunk=chunk)
+    QK = torch.cat([_t(z["Q"]), _t(z["K"])], 1).requires_grad_(True)
+    act, slope = activation_code(ACTS[case["act"]])
+    S = EdgeAggregate.apply(QK, plan, H, case["agg"], act, slope)
+    S.backward(_t(z["dS"]))
+    torch.cuda.synchronize()
+    return plan, S.cpu(), QK.grad[:, :H].cpu(), QK.grad[:, H:].cpu()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_edge_kernels_vs_reference_golden(case):
+    z = load_case(case["name"])
+    plan, S, dQ, dK = _kernel_run(z, case, chunk=256)
+    exact = (case["dtype"] == "float32" and case["act"] in ("relu", "leaky")
+             and plan.dst.n_splits == 0 and plan.src.n_splits == 0)
+    f32 = lambda k: torch.from_numpy(z[k]).float()
+    if exact:
+        # unsplit rows accumulate in the reference's (DGL CSC / index_add) order -> identical bits
+        assert torch.equal(S, f32("S")), f"S max diff {(S - f32('S')).abs().max()}"
+        assert torch.equal(dQ, f32("dQ")), f"dQ max diff {(dQ - f32('dQ')).abs().max()}"
+        assert torch.equal(dK, f32("dK")), f"dK max diff {(dK - f32('dK')).abs().max()}"
+    else:
+        assert_close(S, z["S"], 1e-5, "S")
+        assert_close(dQ, z["dQ"], 1e-5, "dQ")
+        assert_close(dK, z["dK"], 1e-5, "dK")
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["name"].startswith("small") and c["dtype"] == "float32"],
+                         ids=lambda c: c["name"])
+def test_split_rows_match_reference(case):
+    """chunk=4 forces most rows through the partial/combine path."""
+    z = load_case(case["name"])
+    plan, S, dQ, dK = _kernel_run(z, case, chunk=4)
+    assert plan.dst.n_splits > 0 and plan.src.n_splits > 0
+    assert_close(S, z["S"], 1e-5, "S")
+    assert_close(dQ, z["dQ"], 1e-5, "dQ")
+    assert_close(dK, z["dK"], 1e-5, "dK")
+
+
+def _load_reference_weights(m, z):
+    with torch.no_grad():
+        m.linear_query.weight.copy_(_t(z["W_Q"])); m.linear_query.bias.copy_(_t(z["b_Q"]))
+        m.linear_key.weight.copy_(_t(z["W_K"]))
+        m.linear_relation.weight.copy_(_t(z["W_R"])); m.linear_relation.bias.copy_(_t(z["b_R"]))
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_sirconv_layer_vs_reference_golden(case):
+    z = load_case(case["name"])
+    m = SIRConv(case["d"], case["H"], case["O"], ACTS[case["act"]], 0, agg_type=case["agg"]).to(DEV)
+    _load_reference_weights(m, z)
+    g = Graph(torch.from_numpy(z["src"]), torch.from_numpy(z["dst"]), case["V"])
+    X = _t(z["X"]).requires_grad_(True)
+    Y = m(g, X)
+    Y.backward(_t(z["dY"]))
+    torch.cuda.synchronize()
+    tol = 1e-5
+    got = {"Y": Y, "dX": X.grad, "dW_Q": m.linear_query.weight.grad, "db_Q": m.linear_query.bias.grad,
+           "dW_K": m.linear_key.weight.grad, "dW_R": m.linear_relation.weight.grad,
+           "db_R": m.linear_relation.bias.grad}
+    for k, v in got.items():
+        assert_close(v.detach().cpu(), z[k], tol if case["dtype"] == "float32" else 2e-5, f"{case['name']} {k}")
+
+
+def test_state_dict_keys_match_reference_layout():
+    m = SIRConv(16, 32, 8, nn.LeakyReLU(0.2), 0, agg_type="sym")
+    assert sorted(m.state_dict().keys()) == sorted(
+        ["linear_query.weight", "linear_query.bias", "linear_key.weight",
+         "linear_relation.weight", "linear_relation.bias"])
+    # current-code parameter count 3H^2+2H at d=H=O (SURVEY §6 known-answer note)
+    m2 = SIRConv(256, 256, 256, nn.ReLU())
+    assert sum(p.numel() for p in m2.parameters()) == 3 * 256 * 256 + 2 * 256
+
+
+@pytest.mark.parametrize("H", [1, 3, 7, 16, 60, 64, 100, 128, 256, 260, 300, 512, 1000, 1024])
+@pytest.mark.parametrize("agg", ["sum", "mean", "sym"])
+def test_hidden_sizes_vs_oracle(H, agg):
+    gen = torch.Generator().manual_seed(H * 7 + len(agg))
+    V, E = 300, 2500
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V - 20, (E,), generator=gen)
+    dst[:400] = 5                                            # a split row at chunk 256
+    Q = torch.randn(V, H, generator=gen); K = torch.randn(V, H, generator=gen)
+    dS = torch.randn(V, H, generator=gen)
+    S_ref = oracle.edge_agg_fwd(src, dst, V, Q, K, agg, "leaky", 0.2)
+    dQ_ref, dK_ref = oracle.edge_agg_bwd(src, dst, V, Q, K, dS, agg, "leaky", 0.2)
+    plan = GraphPlan(src, dst, V, DEV)
+    QK = torch.cat([Q, K], 1).to(DEV).requires_grad_(True)
+    S = EdgeAggregate.apply(QK, plan, H, agg, _native.ACT_LEAKY, 0.2)
+    S.backward(dS.to(DEV))
+    assert_close(S.detach().cpu(), S_ref, 1e-5, "S")
+    assert_close(QK.grad[:, :H].cpu(), dQ_ref, 1e-5, "dQ")
+    assert_close(QK.grad[:, H:].cpu(), dK_ref, 1e-5, "dK")
+
+
+def test_unaligned_leading_dimension_takes_scalar_path():
+    gen = torch.Generator().manual_seed(3)
+    V, E, H = 200, 1500, 64
+    src = torch.randint(0, V, (E,), generator=gen); dst = torch.randint(0, V, (E,), generator=gen)
+    Q = torch.randn(V, H, generator=gen); K = torch.randn(V, H, generator=gen)
+    buf = torch.zeros(V, 2 * H + 1, device=DEV)
+    buf[:, :H] = Q.to(DEV); buf[:, H + 1:] = K.to(DEV)
+    plan = GraphPlan(src, dst, V, DEV)
+    S = torch.empty(V, H, device=DEV)
+    _native.edge_agg_fwd(plan.dst, buf[:, :H], buf[:, H + 1:], None, None, "sum", _native.ACT_RELU, 0.0, S, None)
+    assert_close(S.cpu(), oracle.edge_agg_fwd(src, dst, V, Q, K, "sum", "relu"), 1e-5, "S")
+
+
+def test_errors_are_loud():
+    m = SIRConv(8, 16, 4, nn.Tanh())
+    g = Graph([0, 1], [1, 0], 2)
+    with pytest.raises(NotImplementedError):
+        m.to(DEV)(g, torch.randn(2, 8, device=DEV))
+    m = SIRConv(8, 16, 4, nn.ReLU())
+    with pytest.raises(RuntimeError):
+        m(g, torch.randn(2, 8))              # CPU tensor: no CPU fallback
+    with pytest.raises(NotImplementedError):
+        SIRConv(8, 16, 4, nn.ReLU(), agg_type="max").to(DEV)(g, torch.randn(2, 8, device=DEV))
+    plan = GraphPlan(torch.tensor([0, 1]), torch.tensor([1, 0]), 2, DEV)
+    QK = torch.randn(2, 2 * 257, device=DEV)
+    with pytest.raises(RuntimeError, match="unsupported hidden size"):
+        _native.edge_agg_fwd(plan.dst, QK[:, :257], QK[:, 257:], None, None, "sum", 1, 0.0,
+                             torch.empty(2, 257, device=DEV), None)
+
+
+def _chunked_torch_reference(src, dst, V, Q, K, dS, agg, slope):
+    """fp32 torch GPU reference of the same math, edge-chunked (never the product path)."""
+    H = Q.shape[1]
+    in_deg = torch.bincount(dst, minlength=V); out_deg = torch.bincount(src, minlength=V)
+    in_norm = torch.pow(in_deg.float().clamp(min=1), -0.5); out_norm = torch.pow(out_deg.float().clamp(min=1), -0.5)
+    degf = in_deg.clamp(min=1).float().unsqueeze(1)
+    G = dS / degf if agg == "mean" else dS
+    S = torch.zeros(V, H, device=Q.device); dQ = torch.zeros_like(S); dK = torch.zeros_like(S)
+    step = 1 << 20
+    for s in range(0, src.numel(), step):
+        u, v = src[s:s + step], dst[s:s + step]
+        z = Q[v] + K[u]
+        m = torch.nn.functional.leaky_relu(z, slope)
+        t = G[v]
+        if agg == "sym":
+            c = (out_norm[u] * in_norm[v]).unsqueeze(1)
+            m = c * m; t = t * c
+        dz = torch.where(z > 0, t, t * slope)
+        S.index_add_(0, v, m); dQ.index_add_(0, v, dz); dK.index_add_(0, u, dz)
+    if agg == "mean":
+        S = S / degf
+    return S, dQ, dK
+
+
+@pytest.mark.parametrize("agg", ["sum", "sym", "mean"])
+def test_full_size_S1_vs_torch_reference_and_deterministic(agg):
+    from sirgcn.synth import powerlaw_graph
+    g = powerlaw_graph(500_000, 10_000_000, 0.8, seed=0)
+    V, H = g.num_nodes(), 256
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    QK = torch.randn(V, 2 * H, device=DEV, generator=gen)
+    dS = torch.randn(V, H, device=DEV, generator=gen)
+    plan = GraphPlan(g._src, g._dst, V, DEV)
+    assert plan.dst.n_splits > 0                            # hubs are split
+    outs = []
+    for _ in range(2):
+        x = QK.clone().requires_grad_(True)
+        S = EdgeAggregate.apply(x, plan, H, agg, _native.ACT_LEAKY, 0.2)
+        S.backward(dS)
+        outs.append((S.detach(), x.grad))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), "not deterministic"
+    src, dst = g._src.to(DEV), g._dst.to(DEV)
+    S_ref, dQ_ref, dK_ref = _chunked_torch_reference(src, dst, V, QK[:, :H], QK[:, H:], dS, agg, 0.2)
+    S, dQK = outs[0]
+    assert rel_err(S, S_ref) < 1e-5
+    assert rel_err(dQK[:, :H], dQ_ref) < 1e-5
+    assert rel_err(dQK[:, H:], dK_ref) < 1e-5
