@@ -51,6 +51,23 @@ int sir_abi_version(void);
 const char* sir_last_error(void);
 
 /*
+ * Per-edge sign-mask size (64-bit words) for hidden size H and activation `act`, or 0 when
+ * the sign-mask backward is not available (needs act in {RELU, LEAKY_RELU}, H % 4 == 0,
+ * 128 < H <= 1024, 16-B aligned rows).  Layout, edge e in destination-CSR order:
+ *   word mask[e*NW + 4*j + w], bit l  =  (Q[v] + K[u])[4*(l + 64*j) + w] > 0.
+ */
+int64_t sir_mask_words(int64_t H, int act);
+
+/*
+ * conv.py:51-57 degree normalisers: norm[i] = 1 / sqrt((float)max(deg_i, 1)) with
+ * deg_i = rowptr[i+1] - rowptr[i] (IEEE sqrt and division: the bits CPU torch.pow(d, -0.5)
+ * returns).  Computes in_norm from the destination CSR and (if non-NULL) out_norm from the
+ * source CSR, n = number of nodes.
+ */
+int sir_degree_norms(const int32_t* rowptr_dst, float* in_norm,
+                     const int32_t* rowptr_src, float* out_norm, int64_t n, void* stream);
+
+/*
  * Forward edge aggregation — replaces conv.py:63 (update_all with the sum/mean/sym UDF).
  *   S[v] = sum_{e in row v} c_e * sigma(Q[v] + K[col[e]]),  c_e = norm_col[u] * norm_row[v]
  *   (SYM only; SUM/MEAN use c_e = 1 exactly as ones*ones in conv.py:45), MEAN divides by
@@ -58,6 +75,8 @@ const char* sir_last_error(void);
  *   rowptr/col: row CSR by destination (rows = dst nodes, col = src node ids).
  *   Q: [n_rows, H] (ldq) indexed by row;  K: [*, H] (ldk) indexed by col.
  *   norm_row / norm_col: fp32 (SYM only, else may be NULL).
+ *   mask_out: NULL, or E * sir_mask_words(H, act) words receiving the sign of every z
+ *   (input of the sign-mask backward).
  */
 int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      const int32_t* items, int64_t n_items,
@@ -66,19 +85,22 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      const void* Q, int64_t ldq, const void* K, int64_t ldk,
                      const float* norm_row, const float* norm_col,
                      int agg, int act, float slope,
-                     float* S, int64_t lds, float* partial, void* stream);
+                     float* S, int64_t lds, uint64_t* mask_out, float* partial, void* stream);
 
 /*
  * Backward, destination pass — the Q half of autograd through conv.py:45,63.
  *   g = G[v] (MEAN: G[v] / max(deg v, 1)),  t_e = g * c_e (SYM) or g,
  *   dQ[v] = sum_{e in row v} sigma'(Q[v] + K[u]) * t_e   (sigma' as torch's backward).
  *   If MEAN and Gm != NULL, the divided rows g are also written to Gm (for the src pass).
+ *   mask != NULL selects the sign-mask mode: sigma'(z) is read from the forward's mask and
+ *   Q, K are not touched (may be NULL); results are bit-identical to the recompute mode.
  */
 int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
                          const int32_t* items, int64_t n_items,
                          const int32_t* splits, int64_t n_splits,
                          int64_t H, int dtype,
                          const void* Q, int64_t ldq, const void* K, int64_t ldk,
+                         const uint64_t* mask,
                          const float* G, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
@@ -91,12 +113,15 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
  *   dK[u] = sum_{e in row u} sigma'(Q[v] + K[u]) * t_e,  t_e = Gd[v] * c_e (SYM) or Gd[v],
  *   where Gd is the already-divided gradient (MEAN: the Gm of the dst pass; else G).
  *   norm_row = out-norm of u, norm_col = in-norm of v (SYM only).
+ *   mask != NULL: sign-mask mode (K, Q unused); perm_s[j] = destination-CSR position of the
+ *   edge at source-CSR position j (indexes the mask).
  */
-int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s,
+int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
                          const int32_t* items, int64_t n_items,
                          const int32_t* splits, int64_t n_splits,
                          int64_t H, int dtype,
                          const void* K, int64_t ldk, const void* Q, int64_t ldq,
+                         const uint64_t* mask,
                          const float* Gd, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,

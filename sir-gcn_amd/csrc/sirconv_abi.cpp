@@ -1,11 +1,11 @@
 // sirconv_abi.cpp — the extern "C" boundary declared in include/sirconv.h.
 //
-// Synchronous argument checks, then one (or two, with split rows) asynchronous launches on
-// the caller's stream.  No allocation, no device sync, no hipSetDevice: the caller (the
-// Python host layer) selects the device and owns every buffer.
+// Synchronous argument checks, then asynchronous launches on the caller's stream (the edge
+// kernel, plus the split-row combine when the plan has split rows).  No allocation, no device
+// sync, no hipSetDevice: the caller (the Python host layer) selects the device and owns every
+// buffer.
 #include <hip/hip_runtime.h>
 
-#include <cstdio>
 #include <string>
 
 #include "sirconv.h"
@@ -39,9 +39,17 @@ int check_common(const char* fn, const int32_t* rowptr, const int32_t* col, cons
     return SIR_OK;
 }
 
+int check_mask(const char* fn, int64_t H, int act) {
+    if (sir_mask_words(H, act) == 0)
+        return fail(SIR_EUNSUPPORTED, fn, "sign mask needs act RELU/LEAKY_RELU, H % 4 == 0 and 128 < H <= 1024");
+    return SIR_OK;
+}
+
 int finish(const char* fn, hipError_t err, const char* why) {
     if (err == hipSuccess) return SIR_OK;
     if (err == hipErrorInvalidValue && why) return fail(SIR_EUNSUPPORTED, fn, why);
+    if (err == hipErrorInvalidValue)
+        return fail(SIR_EUNSUPPORTED, fn, "sign-mask mode needs 16-B aligned full-wave rows");
     return fail(SIR_ELAUNCH, fn, hipGetErrorString(err));
 }
 
@@ -53,6 +61,23 @@ int sir_abi_version(void) { return SIR_ABI_VERSION; }
 
 const char* sir_last_error(void) { return g_last_error.c_str(); }
 
+int64_t sir_mask_words(int64_t H, int act) {
+    if (act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU) return 0;
+    if (H % 4 != 0 || H <= 128 || H > 1024) return 0;
+    return 4 * ((H + 255) / 256);
+}
+
+int sir_degree_norms(const int32_t* rowptr_dst, float* in_norm,
+                     const int32_t* rowptr_src, float* out_norm, int64_t n, void* stream) {
+    const char* fn = "sir_degree_norms";
+    if (n < 0) return fail(SIR_EINVAL, fn, "negative node count");
+    if (n > 0 && (rowptr_dst == nullptr || in_norm == nullptr)) return fail(SIR_EINVAL, fn, "NULL rowptr/norm");
+    if ((rowptr_src == nullptr) != (out_norm == nullptr)) return fail(SIR_EINVAL, fn, "rowptr_src/out_norm pairing");
+    hipError_t err = sir::run_degree_norms(rowptr_dst, in_norm, rowptr_src, out_norm, n,
+                                           static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
 int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      const int32_t* items, int64_t n_items,
                      const int32_t* splits, int64_t n_splits,
@@ -60,13 +85,14 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      const void* Q, int64_t ldq, const void* K, int64_t ldk,
                      const float* norm_row, const float* norm_col,
                      int agg, int act, float slope,
-                     float* S, int64_t lds, float* partial, void* stream) {
+                     float* S, int64_t lds, uint64_t* mask_out, float* partial, void* stream) {
     const char* fn = "sir_edge_agg_fwd";
     int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, S, partial);
     if (rc) return rc;
     if (ldq < H || ldk < H || lds < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
     if (n_items > 0 && (Q == nullptr || K == nullptr)) return fail(SIR_EINVAL, fn, "Q/K must be non-NULL");
+    if (mask_out != nullptr && (rc = check_mask(fn, H, act))) return rc;
     sir::EdgeArgs a{};
     a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items;
     a.R = static_cast<const float*>(Q); a.ldr = ldq;
@@ -74,6 +100,7 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
     a.G = nullptr; a.ldg = H;
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = S; a.ldo = lds; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
+    a.mask_out = mask_out;
     const char* why = nullptr;
     hipError_t err = sir::run_edge(sir::MODE_FWD, a, agg, act, splits, n_splits, S, lds,
                                    agg == SIR_AGG_MEAN, static_cast<hipStream_t>(stream), &why);
@@ -85,6 +112,7 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
                          const int32_t* splits, int64_t n_splits,
                          int64_t H, int dtype,
                          const void* Q, int64_t ldq, const void* K, int64_t ldk,
+                         const uint64_t* mask,
                          const float* G, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
@@ -94,29 +122,36 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
     int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, dQ, partial);
     if (rc) return rc;
-    if (ldq < H || ldk < H || ldg < H || lddq < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+    if (ldg < H || lddq < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
     if (Gm != nullptr && ldgm < H) return fail(SIR_EINVAL, fn, "ldgm must be >= H");
-    if (n_items > 0 && (Q == nullptr || K == nullptr || G == nullptr))
-        return fail(SIR_EINVAL, fn, "Q/K/G must be non-NULL");
+    if (n_items > 0 && G == nullptr) return fail(SIR_EINVAL, fn, "G must be non-NULL");
+    if (mask != nullptr) {
+        if ((rc = check_mask(fn, H, act))) return rc;
+    } else {
+        if (ldq < H || ldk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+        if (n_items > 0 && (Q == nullptr || K == nullptr)) return fail(SIR_EINVAL, fn, "Q/K must be non-NULL");
+    }
     sir::EdgeArgs a{};
     a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items;
-    a.R = static_cast<const float*>(Q); a.ldr = ldq;
-    a.C = static_cast<const float*>(K); a.ldc = ldk;
+    a.R = static_cast<const float*>(Q); a.ldr = mask ? H : ldq;
+    a.C = static_cast<const float*>(K); a.ldc = mask ? H : ldk;
     a.G = G; a.ldg = ldg;
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = dQ; a.ldo = lddq; a.partial = partial;
     a.Gm = (agg == SIR_AGG_MEAN) ? Gm : nullptr; a.ldgm = Gm ? ldgm : H;
+    a.mask_in = mask;
     const char* why = nullptr;
     hipError_t err = sir::run_edge(sir::MODE_BWD_DST, a, agg, act, splits, n_splits, dQ, lddq, false,
                                    static_cast<hipStream_t>(stream), &why);
     return finish(fn, err, why);
 }
 
-int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s,
+int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
                          const int32_t* items, int64_t n_items,
                          const int32_t* splits, int64_t n_splits,
                          int64_t H, int dtype,
                          const void* K, int64_t ldk, const void* Q, int64_t ldq,
+                         const uint64_t* mask,
                          const float* Gd, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
@@ -125,16 +160,23 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s,
     int rc = check_common(fn, rowptr_s, col_s, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, dK, partial);
     if (rc) return rc;
-    if (ldq < H || ldk < H || ldg < H || lddk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
-    if (n_items > 0 && (Q == nullptr || K == nullptr || Gd == nullptr))
-        return fail(SIR_EINVAL, fn, "K/Q/Gd must be non-NULL");
+    if (ldg < H || lddk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+    if (n_items > 0 && Gd == nullptr) return fail(SIR_EINVAL, fn, "Gd must be non-NULL");
+    if (mask != nullptr) {
+        if ((rc = check_mask(fn, H, act))) return rc;
+        if (n_items > 0 && perm_s == nullptr) return fail(SIR_EINVAL, fn, "sign-mask mode needs perm_s");
+    } else {
+        if (ldq < H || ldk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+        if (n_items > 0 && (Q == nullptr || K == nullptr)) return fail(SIR_EINVAL, fn, "K/Q must be non-NULL");
+    }
     sir::EdgeArgs a{};
     a.rowptr = rowptr_s; a.col = col_s; a.items = items; a.n_items = n_items;
-    a.R = static_cast<const float*>(K); a.ldr = ldk;
-    a.C = static_cast<const float*>(Q); a.ldc = ldq;
+    a.R = static_cast<const float*>(K); a.ldr = mask ? H : ldk;
+    a.C = static_cast<const float*>(Q); a.ldc = mask ? H : ldq;
     a.G = Gd; a.ldg = ldg;
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = dK; a.ldo = lddk; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
+    a.mask_in = mask; a.perm = perm_s;
     const char* why = nullptr;
     hipError_t err = sir::run_edge(sir::MODE_BWD_SRC, a, agg, act, splits, n_splits, dK, lddk, false,
                                    static_cast<hipStream_t>(stream), &why);

@@ -1,11 +1,11 @@
-// sirconv_kernels.hip — gfx950 (MI355X, CDNA4) edge-aggregation kernels for SIRConv.
+// sirconv_edge_impl.h — gfx950 (MI355X, CDNA4) edge-aggregation kernels for SIRConv.
 //
 // Reference path: briangodwinlim/SIR-GCN models/conv.py:43-45 (message UDF) + conv.py:63
 // (graph.update_all -> DGL 2.1.0 gather + GSpMM copy_e/sum; autograd -> gsddmm + index_add).
 //
 // Design:
 //  * Row-CSR, atomics-free.  A "row" is the node reduced INTO: dst for the forward and the dQ
-//    pass, src for the dK pass.  One wave (or a 16/32-lane sub-wave when H is small) owns one
+//    pass, src for the dK pass.  One wave (or a 4..32-lane sub-wave when H is small) owns one
 //    work item {row, e_begin, e_end, slot}; the row-side vector (Q[v] or K[u], and G[v]) stays in
 //    registers, each edge gathers ONE (fwd, dQ) or TWO (dK) contiguous H-float rows with 16-B
 //    per-lane loads (1 KiB per wave-instruction at H=256), UNROLL edges in flight per wave.
@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#pragma once
 #include "sirconv_internal.h"
 
 namespace sir {
@@ -100,14 +101,14 @@ __device__ __forceinline__ void vstore(float* __restrict__ p, const float (&s)[V
 
 // ------------------------------------------------------------------------------ edge batch
 // Processes UU consecutive edges [e, e+UU) of one row: all gathers issued before any use.
-template <int MODE, int ACT, int AGG, int LPR, int NV, int VW, int UU>
+template <int MODE, int ACT, int AGG, int LPR, int NV, int VW, int UU, bool MASKW>
 __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                                            const float* __restrict__ C, int64_t ldc,
                                            const float* __restrict__ G, int64_t ldg,
                                            const float* __restrict__ norm_col, float nr, float slope,
                                            int li, int HC,
                                            const float (&rv)[NV][VW], const float (&gv)[NV][VW],
-                                           float (&acc)[NV][VW]) {
+                                           float (&acc)[NV][VW], uint64_t* __restrict__ mask, int lane) {
     int u[UU];
 #pragma unroll
     for (int i = 0; i < UU; ++i) u[i] = col[e + i];
@@ -124,23 +125,39 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (NV == 1 || c < HC) vload<VW>(cv[i][j], cp + c * VW);
+            if (c < HC) vload<VW>(cv[i][j], cp + c * VW);
         }
         if constexpr (MODE == MODE_BWD_SRC) {
             const float* gp = G + (int64_t)u[i] * ldg;
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const int c = li + LPR * j;
-                if (NV == 1 || c < HC) vload<VW>(gc[i][j], gp + c * VW);
+                if (c < HC) vload<VW>(gc[i][j], gp + c * VW);
             }
         }
     }
 #pragma unroll
     for (int i = 0; i < UU; ++i) {
+        if constexpr (MASKW) {
+            // sign mask of z for the sign-mask backward: word (j*4+w), bit lane = z[(lane+64j)*4+w] > 0
+            static_assert(LPR == 64 && VW == 4, "mask layout needs full-wave rows of float4");
+            constexpr int NW = NV * VW;
+            uint64_t wd[NW];
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                const bool ok = (li + LPR * j) < HC;
+#pragma unroll
+                for (int w = 0; w < VW; ++w) wd[j * VW + w] = __ballot(ok && (rv[j][w] + cv[i][j][w]) > 0.f);
+            }
+            uint64_t mine = 0;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) mine = (lane == k) ? wd[k] : mine;
+            if (lane < NW) mask[(int64_t)(e + i) * NW + lane] = mine;
+        }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (NV == 1 || c < HC) {
+            if (c < HC) {
 #pragma unroll
                 for (int w = 0; w < VW; ++w) {
                     if constexpr (MODE == MODE_FWD) {
@@ -169,7 +186,7 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 // MODE_FWD:     R = Q (rows = dst), C = K (gathered by src), out = S
 // MODE_BWD_DST: R = Q, C = K, G = dS rows (row-side), out = dQ, optional Gm = G/deg (MEAN)
 // MODE_BWD_SRC: R = K (rows = src), C = Q (gathered by dst), G = Gd (gathered), out = dK
-template <int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U>
+template <int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U, bool MASKW>
 __global__ void __launch_bounds__(256)
 k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
        const int4* __restrict__ items, int64_t n_items,
@@ -179,7 +196,7 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
        const float* __restrict__ norm_row, const float* __restrict__ norm_col,
        float slope, int H,
        float* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-       float* __restrict__ Gm, int64_t ldgm) {
+       float* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LPR;
@@ -207,7 +224,7 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
         const int c = li + LPR * j;
 #pragma unroll
         for (int w = 0; w < VW; ++w) { acc[j][w] = 0.f; rv[j][w] = 0.f; gv[j][w] = 0.f; }
-        if (NV == 1 || c < HC) vload<VW>(rv[j], rp + c * VW);
+        if (c < HC) vload<VW>(rv[j], rp + c * VW);
     }
     if constexpr (MODE == MODE_BWD_DST) {
         const float* gp = G + (int64_t)row * ldg;
@@ -222,7 +239,7 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (NV == 1 || c < HC) {
+            if (c < HC) {
                 vload<VW>(gv[j], gp + c * VW);
                 if constexpr (AGG == AGG_MEAN) {
 #pragma unroll
@@ -237,21 +254,21 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 
     int e = e0;
     for (; e + U <= e1; e += U)
-        edge_batch<MODE, ACT, AGG, LPR, NV, VW, U>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc);
+        edge_batch<MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
     if constexpr (U > 4) {
         if (e + 4 <= e1) {
-            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 4>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc);
+            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 4, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
             e += 4;
         }
     }
     if constexpr (U > 2) {
         if (e + 2 <= e1) {
-            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 2>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc);
+            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 2, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
             e += 2;
         }
     }
     if (e < e1)
-        edge_batch<MODE, ACT, AGG, LPR, NV, VW, 1>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc);
+        edge_batch<MODE, ACT, AGG, LPR, NV, VW, 1, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
 
     if (slot < 0) {
         if constexpr (MODE == MODE_FWD && AGG == AGG_MEAN) {
@@ -266,70 +283,228 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (NV == 1 || c < HC) vstore<VW>(op + c * VW, acc[j]);
+            if (c < HC) vstore<VW>(op + c * VW, acc[j]);
         }
     } else {
         float* pp = partial + (int64_t)slot * H;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (NV == 1 || c < HC) vstore<VW>(pp + c * VW, acc[j]);
+            if (c < HC) vstore<VW>(pp + c * VW, acc[j]);
         }
     }
 }
 
-// Combine the partial rows of split rows in slot order; MEAN_DIV divides by the degree.
-template <bool MEAN_DIV, int LPR, int NV, int VW>
+// ------------------------------------------------------------------------------ sign-mask backward
+// For sigma in {ReLU, LeakyReLU} sigma'(z) depends only on sign(z), which the forward stored as
+// one bit per (edge, element) (k_edge<MODE_FWD, ..., MASKW>).  The backward then never
+// re-gathers Q or K:
+//   MODE_BWD_DST: dQ[v] = sum_e sel(bit, t_e), t_e = g[v] (* c_e)      -> reads only the mask
+//   MODE_BWD_SRC: dK[u] = sum_e sel(bit, t_e), t_e = Gd[v] (* c_e)     -> one gathered row + mask
+// with sel(bit, t) = bit ? t : t*slope (LeakyReLU) / 0 (ReLU): exactly dsig<ACT>(z, t), so the
+// result is bit-identical to the recompute path.  Full-wave rows of float4 only (LPR = 64).
+template <int ACT>
+__device__ __forceinline__ float sel(bool pos, float t, float slope) {
+    if constexpr (ACT == ACT_RELU) return pos ? t : 0.f;
+    else return pos ? t : t * slope;
+}
+
+template <int MODE, int ACT, int AGG, int NV, int UU>
+__device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, const int* __restrict__ perm,
+                                           const float* __restrict__ G, int64_t ldg,
+                                           const uint64_t* __restrict__ mask,
+                                           const float* __restrict__ norm_col, float nr, float slope,
+                                           int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4]) {
+    constexpr int NW = NV * 4;
+    int p[UU];
+    int v[UU];
+#pragma unroll
+    for (int i = 0; i < UU; ++i) {
+        if constexpr (MODE == MODE_BWD_SRC) {
+            v[i] = col[e + i];
+            p[i] = perm[e + i];
+        } else {
+            p[i] = e + i;
+            if constexpr (AGG == AGG_SYM) v[i] = col[e + i];
+        }
+    }
+    uint64_t wd[UU][NW];
+#pragma unroll
+    for (int i = 0; i < UU; ++i)
+#pragma unroll
+        for (int k = 0; k < NW; ++k) wd[i][k] = mask[(int64_t)p[i] * NW + k];
+    float cf[UU];
+    if constexpr (AGG == AGG_SYM) {
+#pragma unroll
+        for (int i = 0; i < UU; ++i) cf[i] = norm_col[v[i]] * nr;
+    }
+    float gc[(MODE == MODE_BWD_SRC) ? UU : 1][NV][4];
+    if constexpr (MODE == MODE_BWD_SRC) {
+#pragma unroll
+        for (int i = 0; i < UU; ++i) {
+            const float* gp = G + (int64_t)v[i] * ldg;
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                const int c = lane + 64 * j;
+                if (c < HC) vload<4>(gc[i][j], gp + c * 4);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < UU; ++i) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int c = lane + 64 * j;
+            if (c < HC) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    float t;
+                    if constexpr (MODE == MODE_BWD_SRC) t = gc[i][j][w];
+                    else t = gv[j][w];
+                    if constexpr (AGG == AGG_SYM) t = t * cf[i];
+                    const bool pos = (wd[i][j * 4 + w] >> lane) & 1ull;
+                    acc[j][w] += sel<ACT>(pos, t, slope);
+                }
+            }
+        }
+    }
+}
+
+template <int MODE, int ACT, int AGG, int NV, int U>
 __global__ void __launch_bounds__(256)
-k_combine(const int4* __restrict__ splits, int64_t n_splits, const float* __restrict__ partial,
-          int H, float* __restrict__ out, int64_t ldo) {
-    constexpr int RPW = 64 / LPR;
+k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
+            const int4* __restrict__ items, int64_t n_items,
+            const float* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
+            const float* __restrict__ norm_row, const float* __restrict__ norm_col,
+            float slope, int H, float* __restrict__ out, int64_t ldo, float* __restrict__ partial,
+            float* __restrict__ Gm, int64_t ldgm) {
     const int lane = threadIdx.x & 63;
-    const int sub = lane / LPR;
-    const int li = lane - sub * LPR;
-    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t idx = wave * RPW + sub;
-    if (idx >= n_splits) return;
-    const int4 sp = splits[idx];
-    const int HC = H / VW;
-    float acc[NV][VW];
+    const int64_t wave = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    if (wave >= n_items) return;
+    int4 it = items[wave];
+    it.x = __builtin_amdgcn_readfirstlane(it.x);
+    it.y = __builtin_amdgcn_readfirstlane(it.y);
+    it.z = __builtin_amdgcn_readfirstlane(it.z);
+    it.w = __builtin_amdgcn_readfirstlane(it.w);
+    const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
+    const int HC = H / 4;
+    float gv[NV][4];
+    float acc[NV][4];
 #pragma unroll
     for (int j = 0; j < NV; ++j)
 #pragma unroll
-        for (int w = 0; w < VW; ++w) acc[j][w] = 0.f;
-    for (int s = 0; s < sp.z; ++s) {
-        const float* pp = partial + (int64_t)(sp.y + s) * H;
+        for (int w = 0; w < 4; ++w) { acc[j][w] = 0.f; gv[j][w] = 0.f; }
+    if constexpr (MODE == MODE_BWD_DST) {
+        const float* gp = G + (int64_t)row * ldg;
+        float degf = 1.f;
+        bool first = true;
+        if constexpr (AGG == AGG_MEAN) {
+            const int rs = rowptr[row];
+            const int d = rowptr[row + 1] - rs;
+            degf = (float)(d > 1 ? d : 1);
+            first = (e0 == rs);
+        }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            const int c = li + LPR * j;
-            if (NV == 1 || c < HC) {
-                float v[VW];
-                vload<VW>(v, pp + c * VW);
+            const int c = lane + 64 * j;
+            if (c < HC) {
+                vload<4>(gv[j], gp + c * 4);
+                if constexpr (AGG == AGG_MEAN) {
 #pragma unroll
-                for (int w = 0; w < VW; ++w) acc[j][w] += v[w];
+                    for (int w = 0; w < 4; ++w) gv[j][w] = gv[j][w] / degf;
+                    if (Gm != nullptr && first) vstore<4>(Gm + (int64_t)row * ldgm + c * 4, gv[j]);
+                }
             }
         }
     }
-    const float degf = (float)(sp.w > 1 ? sp.w : 1);
-    float* op = out + (int64_t)sp.x * ldo;
+    float nr = 1.f;
+    if constexpr (AGG == AGG_SYM) nr = norm_row[row];
+    int e = e0;
+    for (; e + U <= e1; e += U)
+        mask_batch<MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    if constexpr (U > 4) {
+        if (e + 4 <= e1) {
+            mask_batch<MODE, ACT, AGG, NV, 4>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            e += 4;
+        }
+    }
+    if constexpr (U > 2) {
+        if (e + 2 <= e1) {
+            mask_batch<MODE, ACT, AGG, NV, 2>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            e += 2;
+        }
+    }
+    if (e < e1)
+        mask_batch<MODE, ACT, AGG, NV, 1>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    float* op = (slot < 0) ? out + (int64_t)row * ldo : partial + (int64_t)slot * H;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const int c = li + LPR * j;
-        if (NV == 1 || c < HC) {
-            if constexpr (MEAN_DIV) {
-#pragma unroll
-                for (int w = 0; w < VW; ++w) acc[j][w] = acc[j][w] / degf;
-            }
-            vstore<VW>(op + c * VW, acc[j]);
-        }
+        const int c = lane + 64 * j;
+        if (c < HC) vstore<4>(op + c * 4, acc[j]);
     }
 }
 
-// ------------------------------------------------------------------------------ dispatch
-struct Shape {
-    int lpr, nv, vw;
-};
+// Combine the partial rows of split rows (deterministic, no atomics).  One 1024-thread block
+// per split row: threads cover the row's columns (VW floats each); the remaining thread
+// dimension takes slices of the partial slots (slot s -> slice s % nslice, 4 loads in
+// flight); the slices are added in slice order through LDS.  MEAN_DIV divides by the degree.
+template <bool MEAN_DIV, int VW>
+__global__ void __launch_bounds__(1024)
+k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
+          int H, float* __restrict__ out, int64_t ldo) {
+    __shared__ float red[1024 * VW];
+    const int4 sp = splits[blockIdx.x];
+    const int HC = H / VW;
+    const int cols = HC < 1024 ? HC : 1024;
+    const int nslice = 1024 / cols;
+    const int t = threadIdx.x;
+    const int slice = t / cols;
+    const float degf = (float)(sp.w > 1 ? sp.w : 1);
+    for (int c0 = 0; c0 < HC; c0 += cols) {
+        const int c = c0 + (t % cols);
+        float acc[VW];
+#pragma unroll
+        for (int w = 0; w < VW; ++w) acc[w] = 0.f;
+        if (slice < nslice && c < HC) {
+            const float* base = partial + (int64_t)sp.y * H + c * VW;
+            int s = slice;
+            for (; s + 3 * nslice < sp.z; s += 4 * nslice) {
+                float v[4][VW];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) vload<VW>(v[i], base + (int64_t)(s + i * nslice) * H);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int w = 0; w < VW; ++w) acc[w] += v[i][w];
+            }
+            for (; s < sp.z; s += nslice) {
+                float v[VW];
+                vload<VW>(v, base + (int64_t)s * H);
+#pragma unroll
+                for (int w = 0; w < VW; ++w) acc[w] += v[w];
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < VW; ++w) red[t * VW + w] = acc[w];
+        __syncthreads();
+        if (t < cols && c < HC) {
+            float r[VW];
+#pragma unroll
+            for (int w = 0; w < VW; ++w) r[w] = red[t * VW + w];
+            for (int k = 1; k < nslice; ++k)
+#pragma unroll
+                for (int w = 0; w < VW; ++w) r[w] += red[(k * cols + t) * VW + w];
+            if constexpr (MEAN_DIV) {
+#pragma unroll
+                for (int w = 0; w < VW; ++w) r[w] = r[w] / degf;
+            }
+            vstore<VW>(out + (int64_t)sp.x * ldo + c * VW, r);
+        }
+        __syncthreads();
+    }
+}
 
+// ------------------------------------------------------------------------------ per-mode launch
 template <int MODE, int ACT, int AGG, int LPR, int NV, int VW>
 static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     constexpr int U = (NV == 1) ? 8 : 4;
@@ -337,16 +512,61 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     const int64_t waves = (a.n_items + RPW - 1) / RPW;
     const int64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_edge<MODE, ACT, AGG, LPR, NV, VW, U>), dim3((unsigned)blocks), dim3(256), 0, st,
+    constexpr bool kMaskable = (MODE == MODE_FWD) && (LPR == 64) && (VW == 4) &&
+                               (ACT == ACT_RELU || ACT == ACT_LEAKY);
+    if constexpr (kMaskable) {
+        if (a.mask_out != nullptr) {
+            hipLaunchKernelGGL((k_edge<MODE, ACT, AGG, LPR, NV, VW, U, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+                               a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
+                               a.R, a.ldr, a.C, a.ldc, a.G, a.ldg, a.norm_row, a.norm_col, a.slope, a.H,
+                               a.out, a.ldo, a.partial, a.Gm, a.ldgm, a.mask_out);
+            return hipGetLastError();
+        }
+    } else {
+        if (a.mask_out != nullptr) return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL((k_edge<MODE, ACT, AGG, LPR, NV, VW, U, false>), dim3((unsigned)blocks), dim3(256), 0, st,
                        a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
                        a.R, a.ldr, a.C, a.ldc, a.G, a.ldg, a.norm_row, a.norm_col, a.slope, a.H,
+                       a.out, a.ldo, a.partial, a.Gm, a.ldgm, nullptr);
+    return hipGetLastError();
+}
+
+template <int MODE, int ACT, int AGG, int NV>
+static hipError_t launch_mask_t(const EdgeArgs& a, hipStream_t st) {
+    constexpr int U = (NV == 1) ? 8 : (NV == 2 ? 4 : 2);
+    const int64_t blocks = (a.n_items + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_edge_mask<MODE, ACT, AGG, NV, U>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       a.rowptr, a.col, a.perm, reinterpret_cast<const int4*>(a.items), a.n_items,
+                       a.G, a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H,
                        a.out, a.ldo, a.partial, a.Gm, a.ldgm);
     return hipGetLastError();
 }
 
 template <int MODE, int ACT, int AGG>
+static hipError_t launch_mask_shape(const EdgeArgs& a, Shape s, hipStream_t st) {
+    switch (s.nv) {
+        case 1: return launch_mask_t<MODE, ACT, AGG, 1>(a, st);
+        case 2: return launch_mask_t<MODE, ACT, AGG, 2>(a, st);
+        case 3: return launch_mask_t<MODE, ACT, AGG, 3>(a, st);
+        default: return launch_mask_t<MODE, ACT, AGG, 4>(a, st);
+    }
+}
+
+template <int MODE, int ACT, int AGG>
 static hipError_t launch_edge_shape(const EdgeArgs& a, Shape s, hipStream_t st) {
+    if constexpr (MODE != MODE_FWD && (ACT == ACT_RELU || ACT == ACT_LEAKY)) {
+        if (a.mask_in != nullptr) {
+            if (s.vw != 4 || s.lpr != 64) return hipErrorInvalidValue;
+            return launch_mask_shape<MODE, ACT, AGG>(a, s, st);
+        }
+    } else if constexpr (MODE != MODE_FWD) {
+        if (a.mask_in != nullptr) return hipErrorInvalidValue;
+    }
     if (s.vw == 4) {
+        if (s.lpr == 4) return launch_edge_t<MODE, ACT, AGG, 4, 1, 4>(a, st);
+        if (s.lpr == 8) return launch_edge_t<MODE, ACT, AGG, 8, 1, 4>(a, st);
         if (s.lpr == 16) return launch_edge_t<MODE, ACT, AGG, 16, 1, 4>(a, st);
         if (s.lpr == 32) return launch_edge_t<MODE, ACT, AGG, 32, 1, 4>(a, st);
         switch (s.nv) {
@@ -381,85 +601,6 @@ static hipError_t launch_edge_mode(const EdgeArgs& a, int agg, int act, Shape s,
         case ACT_GELU: return launch_edge_agg<MODE, ACT_GELU>(a, agg, s, st);
         default: return launch_edge_agg<MODE, ACT_GELU_TANH>(a, agg, s, st);
     }
-}
-
-template <bool MEAN_DIV, int LPR, int NV, int VW>
-static hipError_t launch_combine_t(const int32_t* splits, int64_t n, const float* partial, int H,
-                                   float* out, int64_t ldo, hipStream_t st) {
-    constexpr int RPW = 64 / LPR;
-    const int64_t waves = (n + RPW - 1) / RPW;
-    const int64_t blocks = (waves + 3) / 4;
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_combine<MEAN_DIV, LPR, NV, VW>), dim3((unsigned)blocks), dim3(256), 0, st,
-                       reinterpret_cast<const int4*>(splits), n, partial, H, out, ldo);
-    return hipGetLastError();
-}
-
-template <bool MEAN_DIV>
-static hipError_t launch_combine_shape(const int32_t* splits, int64_t n, const float* partial, int H,
-                                       float* out, int64_t ldo, Shape s, hipStream_t st) {
-    if (s.vw == 4) {
-        if (s.lpr == 16) return launch_combine_t<MEAN_DIV, 16, 1, 4>(splits, n, partial, H, out, ldo, st);
-        if (s.lpr == 32) return launch_combine_t<MEAN_DIV, 32, 1, 4>(splits, n, partial, H, out, ldo, st);
-        switch (s.nv) {
-            case 1: return launch_combine_t<MEAN_DIV, 64, 1, 4>(splits, n, partial, H, out, ldo, st);
-            case 2: return launch_combine_t<MEAN_DIV, 64, 2, 4>(splits, n, partial, H, out, ldo, st);
-            case 3: return launch_combine_t<MEAN_DIV, 64, 3, 4>(splits, n, partial, H, out, ldo, st);
-            default: return launch_combine_t<MEAN_DIV, 64, 4, 4>(splits, n, partial, H, out, ldo, st);
-        }
-    }
-    switch (s.nv) {
-        case 1: return launch_combine_t<MEAN_DIV, 64, 1, 1>(splits, n, partial, H, out, ldo, st);
-        case 2: return launch_combine_t<MEAN_DIV, 64, 2, 1>(splits, n, partial, H, out, ldo, st);
-        default: return launch_combine_t<MEAN_DIV, 64, 4, 1>(splits, n, partial, H, out, ldo, st);
-    }
-}
-
-static bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-// Vector width 4 needs every row start 16-B aligned.
-bool pick_shape(int H, bool vec4_ok, Shape* s) {
-    if (H <= 0) return false;
-    if (vec4_ok && (H % 4) == 0) {
-        const int hc = H / 4;
-        s->vw = 4;
-        if (hc <= 16) { s->lpr = 16; s->nv = 1; return true; }
-        if (hc <= 32) { s->lpr = 32; s->nv = 1; return true; }
-        s->lpr = 64;
-        s->nv = (hc + 63) / 64;
-        return s->nv <= 4;
-    }
-    s->vw = 1;
-    s->lpr = 64;
-    s->nv = (H + 63) / 64;
-    if (s->nv == 3) s->nv = 4;
-    return s->nv <= 4;
-}
-
-hipError_t run_edge(int mode, const EdgeArgs& a, int agg, int act,
-                    const int32_t* splits, int64_t n_splits, float* out_final, int64_t ld_final,
-                    bool mean_div, hipStream_t st, const char** why) {
-    const bool v4 = aligned16(a.R) && aligned16(a.C) && aligned16(a.G) && aligned16(a.out) &&
-                    aligned16(a.partial) && aligned16(a.Gm) &&
-                    (a.ldr % 4 == 0) && (a.ldc % 4 == 0) && (a.ldg % 4 == 0) && (a.ldo % 4 == 0) &&
-                    (a.ldgm % 4 == 0);
-    Shape s;
-    if (!pick_shape(a.H, v4, &s)) {
-        *why = "unsupported hidden size (H must be <= 1024 with H%4==0 and 16-B aligned rows, else <= 256)";
-        return hipErrorInvalidValue;
-    }
-    hipError_t err;
-    switch (mode) {
-        case MODE_FWD: err = launch_edge_mode<MODE_FWD>(a, agg, act, s, st); break;
-        case MODE_BWD_DST: err = launch_edge_mode<MODE_BWD_DST>(a, agg, act, s, st); break;
-        default: err = launch_edge_mode<MODE_BWD_SRC>(a, agg, act, s, st); break;
-    }
-    if (err != hipSuccess) return err;
-    if (n_splits > 0) {
-        err = mean_div ? launch_combine_shape<true>(splits, n_splits, a.partial, a.H, out_final, ld_final, s, st)
-                       : launch_combine_shape<false>(splits, n_splits, a.partial, a.H, out_final, ld_final, s, st);
-    }
-    return err;
 }
 
 }  // namespace sir

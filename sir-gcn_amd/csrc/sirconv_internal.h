@@ -24,7 +24,21 @@ struct EdgeArgs {
     float* out;  int64_t ldo;
     float* partial;
     float* Gm;  int64_t ldgm;
+    uint64_t* mask_out;          // forward: write the sign mask (ReLU family, full-wave rows)
+    const uint64_t* mask_in;     // backward: sign-mask mode (Q/K not read)
+    const int* perm;             // BWD_SRC mask mode: src-CSR position -> dst-CSR position
 };
+
+struct Shape {
+    int lpr, nv, vw;   // lanes per row, float-vectors per lane, floats per vector
+};
+
+hipError_t launch_mode_fwd(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
+hipError_t launch_mode_bwd_dst(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
+hipError_t launch_mode_bwd_src(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
+
+hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
+                            int64_t n, hipStream_t st);
 
 hipError_t run_edge(int mode, const EdgeArgs& a, int agg, int act,
                     const int32_t* splits, int64_t n_splits, float* out_final, int64_t ld_final,

@@ -22,11 +22,13 @@ _P, _I64, _I, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
     "sir_abi_version": (ctypes.c_int, []),
     "sir_last_error": (ctypes.c_char_p, []),
+    "sir_mask_words": (ctypes.c_int64, [_I64, _I]),
+    "sir_degree_norms": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
-                                        _P, _P, _I, _I, _F, _P, _I64, _P, _P]),
-    "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
+                                        _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
+    "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
                                             _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P]),
-    "sir_edge_agg_bwd_src": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
+    "sir_edge_agg_bwd_src": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
                                             _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _P]),
 }
 
@@ -102,36 +104,54 @@ def _ld(t, H):
     return t.stride(0)
 
 
-def edge_agg_fwd(csr, Q, K, norm_row, norm_col, agg, act, slope, S, partial):
+def mask_words(H, act):
+    """64-bit words of sign mask per edge, or 0 if the sign-mask backward is unavailable."""
+    return int(load().sir_mask_words(H, act))
+
+
+def degree_norms(rowptr_dst, rowptr_src, in_norm, out_norm):
+    lib = load()
+    n = in_norm.numel()
+    rc = lib.sir_degree_norms(_ptr(rowptr_dst), _ptr(in_norm), _ptr(rowptr_src), _ptr(out_norm), n,
+                              _stream(in_norm.device))
+    _check(rc, lib)
+
+
+def _ldx(t, H):
+    return H if t is None else _ld(t, H)
+
+
+def edge_agg_fwd(csr, Q, K, norm_row, norm_col, agg, act, slope, S, partial, mask_out=None):
     lib = load()
     H = S.shape[1]
     with _Timed("sir_edge_agg_fwd", S.device):
         rc = lib.sir_edge_agg_fwd(
-        _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
-        H, DTYPE_F32, _ptr(Q), _ld(Q, H), _ptr(K), _ld(K, H), _ptr(norm_row), _ptr(norm_col),
-        AGG[agg], act, float(slope), _ptr(S), _ld(S, H), _ptr(partial), _stream(S.device))
+            _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
+            H, DTYPE_F32, _ptr(Q), _ld(Q, H), _ptr(K), _ld(K, H), _ptr(norm_row), _ptr(norm_col),
+            AGG[agg], act, float(slope), _ptr(S), _ld(S, H), _ptr(mask_out), _ptr(partial), _stream(S.device))
     _check(rc, lib)
 
 
-def edge_agg_bwd_dst(csr, Q, K, G, norm_row, norm_col, agg, act, slope, dQ, Gm, partial):
+def edge_agg_bwd_dst(csr, Q, K, G, norm_row, norm_col, agg, act, slope, dQ, Gm, partial, mask=None):
     lib = load()
     H = dQ.shape[1]
     with _Timed("sir_edge_agg_bwd_dst", dQ.device):
         rc = lib.sir_edge_agg_bwd_dst(
-        _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
-        H, DTYPE_F32, _ptr(Q), _ld(Q, H), _ptr(K), _ld(K, H), _ptr(G), _ld(G, H),
-        _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
-        _ptr(dQ), _ld(dQ, H), _ptr(Gm), (_ld(Gm, H) if Gm is not None else H), _ptr(partial), _stream(dQ.device))
+            _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
+            H, DTYPE_F32, _ptr(Q), _ldx(Q, H), _ptr(K), _ldx(K, H), _ptr(mask), _ptr(G), _ld(G, H),
+            _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
+            _ptr(dQ), _ld(dQ, H), _ptr(Gm), _ldx(Gm, H), _ptr(partial), _stream(dQ.device))
     _check(rc, lib)
 
 
-def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, partial):
+def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, partial, mask=None):
     lib = load()
     H = dK.shape[1]
     with _Timed("sir_edge_agg_bwd_src", dK.device):
         rc = lib.sir_edge_agg_bwd_src(
-        _ptr(csr_s.rowptr), _ptr(csr_s.col), _ptr(csr_s.items), csr_s.n_items, _ptr(csr_s.splits),
-        csr_s.n_splits, H, DTYPE_F32, _ptr(K), _ld(K, H), _ptr(Q), _ld(Q, H), _ptr(Gd), _ld(Gd, H),
-        _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
-        _ptr(dK), _ld(dK, H), _ptr(partial), _stream(dK.device))
+            _ptr(csr_s.rowptr), _ptr(csr_s.col), _ptr(csr_s.perm if mask is not None else None),
+            _ptr(csr_s.items), csr_s.n_items, _ptr(csr_s.splits), csr_s.n_splits, H, DTYPE_F32,
+            _ptr(K), _ldx(K, H), _ptr(Q), _ldx(Q, H), _ptr(mask), _ptr(Gd), _ld(Gd, H),
+            _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
+            _ptr(dK), _ld(dK, H), _ptr(partial), _stream(dK.device))
     _check(rc, lib)

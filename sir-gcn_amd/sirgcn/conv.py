@@ -46,7 +46,12 @@ def activation_code(act):
 class EdgeAggregate(torch.autograd.Function):
     """S = update_all(message_func, agg) of ``conv.py:63`` on packed ``QK = [Q | K]`` ([V, 2H]).
 
-    Backward returns dQK written by the dst pass (dQ half) and the src pass (dK half)."""
+    Backward returns dQK written by the dst pass (dQ half) and the src pass (dK half).
+    For sigma in {ReLU, LeakyReLU} (and 128 < H <= 1024) the forward also stores the sign of
+    every z = Q[v] + K[u] (H bits per edge) and the backward runs in sign-mask mode: no Q/K
+    re-gather, QK not kept alive; results are bit-identical to the recompute mode."""
+
+    use_mask = True
 
     @staticmethod
     def forward(ctx, QK, plan, H, agg, act, slope):
@@ -61,26 +66,38 @@ class EdgeAggregate(torch.autograd.Function):
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=QK.device, dtype=torch.float32)
         partial = _partial(plan, H, QK.device)
-        _native.edge_agg_fwd(plan.dst, Q, K, in_norm, out_norm, agg, act, slope, S, partial)
-        ctx.save_for_backward(QK)
-        ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope = plan, H, agg, act, slope
+        nw = _native.mask_words(H, act) if EdgeAggregate.use_mask else 0
+        mask = None
+        if nw and QK.requires_grad:
+            mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=QK.device, dtype=torch.int64)
+        _native.edge_agg_fwd(plan.dst, Q, K, in_norm, out_norm, agg, act, slope, S, partial, mask)
+        if mask is not None:
+            ctx.save_for_backward(mask)
+        else:
+            ctx.save_for_backward(QK)
+        ctx.masked = mask is not None
+        ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.V = plan, H, agg, act, slope, V
         return S
 
     @staticmethod
     def backward(ctx, dS):
-        (QK,) = ctx.saved_tensors
-        plan, H, agg, act, slope = ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope
+        (saved,) = ctx.saved_tensors
+        plan, H, agg, act, slope, V = ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.V
         G = dS.contiguous().float()
-        V = QK.shape[0]
-        dQK = torch.empty_like(QK)
+        dQK = torch.empty((V, 2 * H), device=G.device, dtype=torch.float32)
         in_norm, out_norm = plan.norms(agg)
-        partial = _partial(plan, H, QK.device)
-        Gm = torch.empty((V, H), device=QK.device, dtype=torch.float32) if agg == "mean" else None
-        Q, K = QK[:, :H], QK[:, H:]
+        partial = _partial(plan, H, G.device)
+        Gm = torch.empty((V, H), device=G.device, dtype=torch.float32) if agg == "mean" else None
+        if ctx.masked:
+            Q = K = None
+            mask = saved
+        else:
+            Q, K = saved[:, :H], saved[:, H:]
+            mask = None
         _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope,
-                                 dQK[:, :H], Gm, partial)
+                                 dQK[:, :H], Gm, partial, mask)
         _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
-                                 agg, act, slope, dQK[:, H:], partial)
+                                 agg, act, slope, dQK[:, H:], partial, mask)
         return dQK.to(ctx.in_dtype), None, None, None, None, None
 
 

@@ -93,6 +93,7 @@ class RowCSR:
     n_splits: int
     n_slots: int
     max_degree: int
+    perm: Optional[torch.Tensor] = None   # int32 [E]: this CSR's position -> dst-CSR position
 
 
 def build_row_csr(rows, cols, n_rows, chunk=DEFAULT_CHUNK):
@@ -164,6 +165,11 @@ class GraphPlan:
         else:
             self.dst = build_row_csr(dst, src, self.num_nodes, chunk)
         self.src = build_row_csr(src, dst, self.num_nodes, chunk)
+        # sign-mask backward: the mask is written in dst-CSR order; the src pass finds an
+        # edge's mask through its dst-CSR position
+        pos_in_dst = torch.empty(self.num_edges, dtype=torch.int64, device=self.device)
+        pos_in_dst[self.dst.eid] = torch.arange(self.num_edges, device=self.device)
+        self.src.perm = pos_in_dst[self.src.eid].to(torch.int32).contiguous()
         self.in_deg = (self.dst.rowptr[1:] - self.dst.rowptr[:-1]).to(torch.int64)
         self.out_deg = (self.src.rowptr[1:] - self.src.rowptr[:-1]).to(torch.int64)
         self._norms = {}
@@ -173,8 +179,14 @@ class GraphPlan:
         if agg != "sym":
             return None, None
         if "sym" not in self._norms:
-            in_norm = torch.pow(self.in_deg.float().clamp(min=1), -0.5).contiguous()
-            out_norm = torch.pow(self.out_deg.float().clamp(min=1), -0.5).contiguous()
+            if self.device.type == "cuda":     # native: IEEE 1/sqrt == CPU torch.pow(d, -0.5) bits
+                from . import _native
+                in_norm = torch.empty(self.num_nodes, dtype=torch.float32, device=self.device)
+                out_norm = torch.empty_like(in_norm)
+                _native.degree_norms(self.dst.rowptr, self.src.rowptr, in_norm, out_norm)
+            else:                              # host-side plans (tests) use the reference formula
+                in_norm = torch.pow(self.in_deg.float().clamp(min=1), -0.5).contiguous()
+                out_norm = torch.pow(self.out_deg.float().clamp(min=1), -0.5).contiguous()
             self._norms["sym"] = (in_norm, out_norm)
         return self._norms["sym"]
 

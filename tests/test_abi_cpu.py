@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "sirconv.h")
 def declared_symbols():
     with open(HEADER) as f:
         text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(sir_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int64_t|int|const char\*)\s+(sir_\w+)\s*\(", text, re.M)))
 
 
 def test_header_and_binding_agree():
@@ -35,42 +35,59 @@ def _null():
     return ctypes.c_void_p(None)
 
 
+def _fwd(lib, rowptr, col, items, n_items, H, dtype, Q, ldq, K, ldk, nr, nc, agg, act, S, lds, mask=None):
+    return lib.sir_edge_agg_fwd(rowptr, col, items, n_items, _null(), 0, H, dtype, Q, ldq, K, ldk, nr, nc,
+                                agg, act, 0.2, S, lds, mask if mask is not None else _null(), _null(), _null())
+
+
 def test_argument_checks_are_synchronous_and_reported():
     lib = _native.load()
+    n = _null()
     # unsupported dtype
-    rc = lib.sir_edge_agg_fwd(_null(), _null(), _null(), 0, _null(), 0, 256, 7, _null(), 256, _null(), 256,
-                              _null(), _null(), 0, 2, 0.2, _null(), 256, _null(), _null())
-    assert rc == 2 and b"F32" in lib.sir_last_error()
+    assert _fwd(lib, n, n, n, 0, 256, 7, n, 256, n, 256, n, n, 0, 2, n, 256) == 2
+    assert b"F32" in lib.sir_last_error()
     # bad agg
-    rc = lib.sir_edge_agg_fwd(_null(), _null(), _null(), 0, _null(), 0, 256, 0, _null(), 256, _null(), 256,
-                              _null(), _null(), 9, 2, 0.2, _null(), 256, _null(), _null())
-    assert rc == 1 and b"agg" in lib.sir_last_error()
+    assert _fwd(lib, n, n, n, 0, 256, 0, n, 256, n, 256, n, n, 9, 2, n, 256) == 1
+    assert b"agg" in lib.sir_last_error()
     # H out of range
-    rc = lib.sir_edge_agg_bwd_dst(_null(), _null(), _null(), 0, _null(), 0, 4096, 0, _null(), 4096, _null(), 4096,
-                                  _null(), 4096, _null(), _null(), 0, 2, 0.2, _null(), 4096, _null(), 4096,
-                                  _null(), _null())
+    rc = lib.sir_edge_agg_bwd_dst(n, n, n, 0, n, 0, 4096, 0, n, 4096, n, 4096, n, n, 4096, n, n, 0, 2, 0.2,
+                                  n, 4096, n, 4096, n, n)
     assert rc == 1 and b"H must be" in lib.sir_last_error()
     # non-NULL requirements when there is work
-    rc = lib.sir_edge_agg_bwd_src(_null(), _null(), _null(), 5, _null(), 0, 64, 0, _null(), 64, _null(), 64,
-                                  _null(), 64, _null(), _null(), 0, 2, 0.2, _null(), 64, _null(), _null())
+    rc = lib.sir_edge_agg_bwd_src(n, n, n, n, 5, n, 0, 64, 0, n, 64, n, 64, n, n, 64, n, n, 0, 2, 0.2,
+                                  n, 64, n, n)
     assert rc == 1
-    # SYM requires norms
     buf = ctypes.create_string_buffer(64)
     p = ctypes.cast(buf, ctypes.c_void_p)
-    rc = lib.sir_edge_agg_fwd(p, p, p, 1, _null(), 0, 16, 0, p, 16, p, 16, _null(), _null(), 2, 2, 0.2,
-                              p, 16, _null(), _null())
-    assert rc == 1 and b"SYM" in lib.sir_last_error()
+    # SYM requires norms
+    assert _fwd(lib, p, p, p, 1, 16, 0, p, 16, p, 16, n, n, 2, 2, p, 16) == 1
+    assert b"SYM" in lib.sir_last_error()
     # leading dimension smaller than H
-    rc = lib.sir_edge_agg_fwd(p, p, p, 1, _null(), 0, 16, 0, p, 8, p, 16, _null(), _null(), 0, 2, 0.2,
-                              p, 16, _null(), _null())
-    assert rc == 1 and b"leading" in lib.sir_last_error()
+    assert _fwd(lib, p, p, p, 1, 16, 0, p, 8, p, 16, n, n, 0, 2, p, 16) == 1
+    assert b"leading" in lib.sir_last_error()
+    # sign mask is only defined for the ReLU family and 128 < H <= 1024
+    assert _fwd(lib, p, p, p, 1, 64, 0, p, 64, p, 64, n, n, 0, 2, p, 64, mask=p) == 2
+    assert _fwd(lib, p, p, p, 1, 256, 0, p, 256, p, 256, n, n, 0, 3, p, 256, mask=p) == 2
+    assert b"sign mask" in lib.sir_last_error()
+    # mask-mode src pass needs the permutation
+    rc = lib.sir_edge_agg_bwd_src(p, p, n, p, 1, n, 0, 256, 0, n, 256, n, 256, p, p, 256, n, n, 0, 2, 0.2,
+                                  p, 256, n, n)
+    assert rc == 1 and b"perm" in lib.sir_last_error()
+
+
+def test_mask_words_contract():
+    lib = _native.load()
+    assert lib.sir_mask_words(256, 2) == 4 and lib.sir_mask_words(256, 1) == 4
+    assert lib.sir_mask_words(300, 2) == 8 and lib.sir_mask_words(1024, 2) == 16
+    assert lib.sir_mask_words(128, 2) == 0 and lib.sir_mask_words(256, 3) == 0
+    assert lib.sir_mask_words(258, 2) == 0 and lib.sir_mask_words(2048, 2) == 0
 
 
 def test_empty_work_is_a_no_op():
     lib = _native.load()
-    rc = lib.sir_edge_agg_fwd(_null(), _null(), _null(), 0, _null(), 0, 256, 0, _null(), 256, _null(), 256,
-                              _null(), _null(), 0, 2, 0.2, _null(), 256, _null(), _null())
-    assert rc == 0
+    n = _null()
+    assert _fwd(lib, n, n, n, 0, 256, 0, n, 256, n, 256, n, n, 0, 2, n, 256) == 0
+    assert lib.sir_degree_norms(n, n, n, n, 0, n) == 0
 
 
 def test_package_surface():

