@@ -52,15 +52,27 @@ def parse():
     return ap.parse_args()
 
 
-def edge_pass_bytes(name, V_rows, E, H, agg, s=4, si=4):
-    """Algorithmic HBM bytes of one launch of each edge pass."""
-    extra = (E * 4 + V_rows * 4) if agg == "sym" else 0          # norm_col per edge, norm_row per row
-    if name == "sir_edge_agg_fwd":       # col idx + K[u] row per edge; Q[v] read + S[v] write + rowptr
-        return E * (si + H * s) + V_rows * (2 * H * s + si) + extra
-    if name == "sir_edge_agg_bwd_dst":   # col idx + K[u] per edge; Q, G read + dQ write per row
-        return E * (si + H * s) + V_rows * (3 * H * s + si) + extra + (V_rows * H * s if agg == "mean" else 0)
-    if name == "sir_edge_agg_bwd_src":   # col idx + Q[v] + G[v] per edge; K read + dK write per row
-        return E * (si + 2 * H * s) + V_rows * (2 * H * s + si) + extra
+def edge_pass_bytes(name, V_rows, E, H, agg, masked, s=4, si=4):
+    """Algorithmic HBM bytes of one launch of each edge pass.
+
+    Recompute mode (any sigma): fwd gathers K[u]; dQ pass re-gathers K[u]; dK pass gathers Q[v]
+    and G[v].  Sign-mask mode (ReLU family): fwd also writes H bits/edge; dQ pass reads only the
+    mask; dK pass gathers G[v] + the edge's mask words (+ its permutation index).
+    """
+    mb = 8 * 4 * ((H + 255) // 256) if masked else 0           # mask bytes per edge
+    sym_e = E * (si + 4) if agg == "sym" else 0                 # col + norm_col per edge when c_e needed
+    sym_r = V_rows * 4 if agg == "sym" else 0
+    if name == "sir_edge_agg_fwd":       # col + K[u] (+ mask write) per edge; Q read + S write + rowptr
+        return E * (si + H * s + mb) + V_rows * (2 * H * s + si) + (E * 4 if agg == "sym" else 0) + sym_r
+    if name == "sir_edge_agg_bwd_dst":
+        mean = V_rows * H * s if agg == "mean" else 0           # Gm side output
+        if masked:                       # mask per edge; G read + dQ write per row
+            return E * mb + sym_e + V_rows * (2 * H * s + si) + sym_r + mean
+        return E * (si + H * s) + V_rows * (3 * H * s + si) + (E * 4 if agg == "sym" else 0) + sym_r + mean
+    if name == "sir_edge_agg_bwd_src":
+        if masked:                       # col + perm + G[v] + mask per edge; dK write per row
+            return E * (2 * si + H * s + mb) + V_rows * (H * s + si) + (E * 4 if agg == "sym" else 0) + sym_r
+        return E * (si + 2 * H * s) + V_rows * (2 * H * s + si) + (E * 4 if agg == "sym" else 0) + sym_r
     raise KeyError(name)
 
 
@@ -173,10 +185,13 @@ def main():
     el = el_t.item()
     ms = 1e3 * el / args.steps
 
+    from sirgcn.conv import EdgeAggregate
+    masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY))
     kernels = {}
     for name, evs in timing.items():
         t = sum(a.elapsed_time(b) for a, b in evs) / len(evs)    # ms per launch
-        bytes_ = edge_pass_bytes(name, rows_local if name != "sir_edge_agg_bwd_src" else V, edges_local, H, args.agg)
+        bytes_ = edge_pass_bytes(name, rows_local if name != "sir_edge_agg_bwd_src" else V, edges_local, H,
+                                 args.agg, masked)
         kernels[name] = {"ms": round(t, 4), "launches": len(evs), "bytes": bytes_,
                          "GBps": round(bytes_ / (t * 1e-3) / 1e9, 1)}
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
@@ -190,7 +205,7 @@ def main():
     except (OSError, ValueError):
         pass
     d = kernels[dom]
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    roofline = {"bound": "hbm", "kernel": dom, "backward_mode": "sign-mask" if masked else "recompute", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(d["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes": d["bytes"], "ms_per_launch": d["ms"], "all_kernels": kernels}
 

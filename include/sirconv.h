@@ -24,6 +24,7 @@
  *    slot >= 0 (partial-sum slot), unsplit rows have slot = -1.  `splits` =
  *    int32[n_splits][4] {row, slot_begin, n_slots, degree} for the split rows, combined in
  *    slot order (deterministic, no atomics).  `partial` = float[n_slots_total * H] scratch.
+ *  - `col` (and `perm_s`) may be NULL when the graph has no edges.
  *  - Return 0 on success, otherwise an SIR_E* code; sir_last_error() gives the text
  *    (thread-local).
  */

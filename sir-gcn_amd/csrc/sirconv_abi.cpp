@@ -31,7 +31,7 @@ int check_common(const char* fn, const int32_t* rowptr, const int32_t* col, cons
     if (n_items < 0 || n_splits < 0) return fail(SIR_EINVAL, fn, "negative item/split count");
     if (n_items > 0 && (rowptr == nullptr || items == nullptr || out == nullptr))
         return fail(SIR_EINVAL, fn, "rowptr/items/output must be non-NULL");
-    if (col == nullptr && n_items > 0) return fail(SIR_EINVAL, fn, "col must be non-NULL");
+    (void)col;  // may be NULL exactly when the graph has no edges (every item is empty)
     if (n_splits > 0 && (splits == nullptr || partial == nullptr))
         return fail(SIR_EINVAL, fn, "split rows need `splits` and a `partial` workspace");
     if (agg == SIR_AGG_SYM && n_items > 0 && (norm_row == nullptr || norm_col == nullptr))
