@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the edge-cut (sirgcn.dist) code path even at world size 1")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -141,7 +143,8 @@ def main():
     X_full = torch.randn(V, H, generator=gen)
     dY_full = torch.randn(V, H, generator=torch.Generator().manual_seed(5))
 
-    if world == 1:
+    dconv = None
+    if world == 1 and not args.force_dist:
         from sirgcn import Graph
         g = Graph(src, dst, V)
         X = X_full.to(dev).requires_grad_(True)
@@ -164,6 +167,8 @@ def main():
         X.grad = None
         Y = layer()
         Y.backward(dY)
+        if dconv is not None:
+            dconv.allreduce_grads()
 
     for _ in range(args.warmup):
         step()

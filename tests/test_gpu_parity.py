@@ -263,3 +263,30 @@ def test_sign_mask_backward_bit_identical_to_recompute(case):
             EdgeAggregate.use_mask = True
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("agg", ["sum", "sym", "mean"])
+def test_edge_cut_path_single_rank_equals_single_gpu(agg):
+    """sirgcn.dist with world=1 (padded remap, all-gather/reduce-scatter degenerate) must give
+    the same bits as the single-GPU layer (collectives themselves: tests/test_dist_gloo.py)."""
+    from sirgcn.dist import DistGraph, DistSIRConv
+    from sirgcn.synth import powerlaw_edges
+    V, E, H = 3000, 60000, 256
+    src, dst = powerlaw_edges(V, E, 0.8, seed=5)
+    X = torch.randn(V, H, generator=torch.Generator().manual_seed(1)).to(DEV)
+    dY = torch.randn(V, H, generator=torch.Generator().manual_seed(2)).to(DEV)
+    torch.manual_seed(3)
+    conv = SIRConv(H, H, H, nn.LeakyReLU(0.2), 0, agg_type=agg).to(DEV)
+    x1 = X.clone().requires_grad_(True)
+    Y1 = conv(Graph(src, dst, V), x1); Y1.backward(dY)
+    g1 = {n: p.grad.clone() for n, p in conv.named_parameters()}
+    conv.zero_grad(set_to_none=True)
+    dg = DistGraph.from_global(src, dst, V, 0, 1, DEV)
+    x2 = X.clone().requires_grad_(True)
+    Y2 = DistSIRConv(conv)(dg, x2); Y2.backward(dY)
+    torch.cuda.synchronize()
+    # Q/K come from one packed GEMM on one path and two GEMMs on the other -> rounding-level diffs
+    assert_close(Y2.detach().cpu(), Y1.detach().cpu(), 1e-6, "Y")
+    assert_close(x2.grad.cpu(), x1.grad.cpu(), 1e-6, "dX")
+    for n, p in conv.named_parameters():
+        assert_close(p.grad.cpu(), g1[n].cpu(), 1e-6, n)
