@@ -106,6 +106,90 @@ def _partial(plan, H, device):
     return torch.empty((max(n, 1) * H,), device=device, dtype=torch.float32) if n else None
 
 
+def _tn(A, B):
+    """A^T B for tall A [V, m], B [V, n] (the weight-gradient GEMMs, K = V).
+
+    hipBLASLt runs these long-K shapes at ~60-75 TF/s fp32; splitting K into k row blocks as one
+    batched GEMM and summing the k partial products runs at 130-150 TF/s on MI355X
+    (tools/gemm_probe.py).  Deterministic (fixed split)."""
+    V = A.shape[0]
+    k = 32
+    while k > 1 and V // k < 4096:
+        k //= 2
+    if k == 1:
+        return A.t() @ B
+    n = (V // k) * k
+    out = torch.bmm(A[:n].view(k, n // k, A.shape[1]).transpose(1, 2), B[:n].view(k, n // k, B.shape[1])).sum(0)
+    if n < V:
+        out += A[n:].t() @ B[n:]
+    return out
+
+
+class SIRConvFunction(torch.autograd.Function):
+    """The whole layer (``conv.py:49-67``) with a hand-scheduled backward:
+
+    forward : QK = X [W_Q; W_K]^T + [b_Q; 0]  (one GEMM)  ->  S = edge kernels  ->  Y = S W_R^T + b_R
+    backward: G = dY W_R, dW_R = dY^T S (split-K), db_R = sum dY, dQ/dK = edge passes,
+              dX = [dQ dK] [W_Q; W_K], [dW_Q; dW_K] = [dQ dK]^T X (split-K), db_Q = sum dQ.
+    Used when dropout is inactive and inputs are fp32 (the modular path covers the rest)."""
+
+    @staticmethod
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope):
+        H = W_Q.shape[0]
+        X = X.contiguous()
+        W_cat = torch.cat([W_Q, W_K], 0)
+        if b_Q is not None:
+            QK = torch.addmm(torch.cat([b_Q, b_Q.new_zeros(H)]), X, W_cat.t())
+        else:
+            QK = torch.mm(X, W_cat.t())
+        V = QK.shape[0]
+        in_norm, out_norm = plan.norms(agg)
+        S = torch.empty((V, H), device=X.device, dtype=torch.float32)
+        partial = _partial(plan, H, X.device)
+        training = any(ctx.needs_input_grad[:6])
+        nw = _native.mask_words(H, act) if (EdgeAggregate.use_mask and training) else 0
+        mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=X.device, dtype=torch.int64) if nw else None
+        _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, act, slope, S, partial, mask)
+        Y = torch.addmm(b_R, S, W_R.t()) if b_R is not None else torch.mm(S, W_R.t())
+        ctx.save_for_backward(X, W_cat, W_R, S, mask if mask is not None else QK)
+        ctx.masked = mask is not None
+        ctx.plan, ctx.agg, ctx.act, ctx.slope = plan, agg, act, slope
+        ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        X, W_cat, W_R, S, saved = ctx.saved_tensors
+        plan, agg, act, slope = ctx.plan, ctx.agg, ctx.act, ctx.slope
+        H = W_R.shape[1]
+        V = X.shape[0]
+        dY = dY.contiguous()
+        G = torch.mm(dY, W_R)
+        dW_R = _tn(dY, S) if ctx.needs_input_grad[4] else None
+        db_R = dY.sum(0) if ctx.has_br and ctx.needs_input_grad[5] else None
+        in_norm, out_norm = plan.norms(agg)
+        partial = _partial(plan, H, X.device)
+        Gm = torch.empty((V, H), device=X.device, dtype=torch.float32) if agg == "mean" else None
+        if ctx.masked:
+            Q = K = None
+            mask = saved
+        else:
+            Q, K = saved[:, :H], saved[:, H:]
+            mask = None
+        dQK = torch.empty((V, 2 * H), device=X.device, dtype=torch.float32)
+        _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope,
+                                 dQK[:, :H], Gm, partial, mask)
+        _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
+                                 agg, act, slope, dQK[:, H:], partial, mask)
+        dX = torch.mm(dQK, W_cat) if ctx.needs_input_grad[0] else None
+        dW_Q = dW_K = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
+            dW = _tn(dQK, X)
+            dW_Q, dW_K = dW[:H], dW[H:]
+        db_Q = dQK[:, :H].sum(0) if ctx.has_bq and ctx.needs_input_grad[2] else None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None
+
+
 class SIRConv(nn.Module):
     r"""Soft-Isomorphic Relational Graph Convolution (SIR-GCN), MI355X-native.
 
@@ -115,6 +199,8 @@ class SIRConv(nn.Module):
     {``sum``, ``mean``, ``sym``} runs natively; ``max`` is accepted by the constructor for
     state-dict compatibility but raises at ``forward`` until its kernel lands.
     """
+
+    use_fused = True      # whole-layer Function when dropout is off and inputs are fp32
 
     def __init__(self, input_dim, hidden_dim, output_dim, activation, dropout=0, inner_bias=True,
                  outer_bias=True, agg_type='sum'):
@@ -158,6 +244,13 @@ class SIRConv(nn.Module):
         if plan.num_nodes != feat_query.shape[0]:
             raise ValueError(f"feat has {feat_query.shape[0]} rows, graph has {plan.num_nodes} nodes")
         H = self.linear_query.out_features
+        fused = (self.use_fused and feat_key is feat_query and feat_query.dtype == torch.float32 and feat_query.is_cuda
+                 and not torch.is_autocast_enabled() and not (self.training and self.dropout.p > 0)
+                 and self.linear_query.weight.dtype == torch.float32)
+        if fused:
+            return SIRConvFunction.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
+                                         self.linear_key.weight, self.linear_relation.weight,
+                                         self.linear_relation.bias, plan, self._agg_type, act, slope)
         QK = self._project(feat_key, feat_query)
         S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope)
         return self.linear_relation(S)
