@@ -136,24 +136,30 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
             }
         }
     }
+    if constexpr (MASKW) {
+        // sign mask of z for the sign-mask backward: word (j*4+w), bit lane = z[(lane+64j)*4+w] > 0.
+        // The UU edges' words are contiguous; lane k takes word k (uniform -> per-lane select)
+        // and ONE store writes the batch's UU*NW*8 bytes.
+        static_assert(LPR == 64 && VW == 4, "mask layout needs full-wave rows of float4");
+        constexpr int NW = NV * VW;
+        static_assert(UU * NW <= 64, "one mask store per batch");
+        uint64_t mine = 0;
 #pragma unroll
-    for (int i = 0; i < UU; ++i) {
-        if constexpr (MASKW) {
-            // sign mask of z for the sign-mask backward: word (j*4+w), bit lane = z[(lane+64j)*4+w] > 0
-            static_assert(LPR == 64 && VW == 4, "mask layout needs full-wave rows of float4");
-            constexpr int NW = NV * VW;
-            uint64_t wd[NW];
+        for (int i = 0; i < UU; ++i) {
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const bool ok = (li + LPR * j) < HC;
 #pragma unroll
-                for (int w = 0; w < VW; ++w) wd[j * VW + w] = __ballot(ok && (rv[j][w] + cv[i][j][w]) > 0.f);
+                for (int w = 0; w < VW; ++w) {
+                    const uint64_t b = __ballot(ok && (rv[j][w] + cv[i][j][w]) > 0.f);
+                    mine = (lane == i * NW + j * VW + w) ? b : mine;
+                }
             }
-            uint64_t mine = 0;
-#pragma unroll
-            for (int k = 0; k < NW; ++k) mine = (lane == k) ? wd[k] : mine;
-            if (lane < NW) mask[(int64_t)(e + i) * NW + lane] = mine;
         }
+        if (lane < UU * NW) mask[(int64_t)e * NW + lane] = mine;
+    }
+#pragma unroll
+    for (int i = 0; i < UU; ++i) {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
