@@ -69,6 +69,16 @@ int sir_degree_norms(const int32_t* rowptr_dst, float* in_norm,
                      const int32_t* rowptr_src, float* out_norm, int64_t n, void* stream);
 
 /*
+ * Column sums out[c] = sum_r X[r*ld + c] of a tall fp32 matrix — the bias gradients of the
+ * layer's linears (db_R = sum_v dY[v], db_Q = sum_v dQ[v]; autograd of conv.py:61,65).
+ * Deterministic (fixed two-level order).  n_cols % 4 == 0, ld % 4 == 0, X 16-B aligned;
+ * workspace: SIR_COLSUM_BLOCKS * n_cols floats.
+ */
+#define SIR_COLSUM_BLOCKS 1024
+int sir_col_sum(const float* X, int64_t ld, int64_t n_rows, int64_t n_cols, float* out,
+                float* workspace, void* stream);
+
+/*
  * Forward edge aggregation — replaces conv.py:63 (update_all with the sum/mean/sym UDF).
  *   S[v] = sum_{e in row v} c_e * sigma(Q[v] + K[col[e]]),  c_e = norm_col[u] * norm_row[v]
  *   (SYM only; SUM/MEAN use c_e = 1 exactly as ones*ones in conv.py:45), MEAN divides by

@@ -78,6 +78,19 @@ int sir_degree_norms(const int32_t* rowptr_dst, float* in_norm,
     return finish(fn, err, nullptr);
 }
 
+int sir_col_sum(const float* X, int64_t ld, int64_t n_rows, int64_t n_cols, float* out,
+                float* workspace, void* stream) {
+    const char* fn = "sir_col_sum";
+    if (n_rows < 0 || n_cols < 0 || n_cols > (1 << 20)) return fail(SIR_EINVAL, fn, "bad shape");
+    if (n_cols % 4 != 0 || ld % 4 != 0 || ld < n_cols) return fail(SIR_EINVAL, fn, "n_cols and ld must be multiples of 4, ld >= n_cols");
+    if (n_cols > 0 && (out == nullptr || workspace == nullptr || (n_rows > 0 && X == nullptr)))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if ((reinterpret_cast<uintptr_t>(X) & 15u) != 0) return fail(SIR_EINVAL, fn, "X must be 16-B aligned");
+    hipError_t err = sir::run_colsum(X, ld, n_rows, (int)n_cols, out, workspace, SIR_COLSUM_BLOCKS,
+                                     static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
 int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      const int32_t* items, int64_t n_items,
                      const int32_t* splits, int64_t n_splits,

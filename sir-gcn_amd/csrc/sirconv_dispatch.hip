@@ -18,6 +18,71 @@ k_degree_norms(const int* __restrict__ rowptr_a, float* __restrict__ norm_a,
     }
 }
 
+// Column sums of a tall row-major matrix (the bias gradients db_R = sum_v dY[v], db_Q = sum_v dQ[v]).
+// Deterministic two-pass: pass 1 gives each of `nb` blocks a contiguous range of rows and writes
+// one partial row per block; pass 2 adds the nb partials in block order.  float4 columns.
+__global__ void __launch_bounds__(256)
+k_colsum_partial(const float* __restrict__ X, int64_t ld, int64_t n_rows, int n_cols,
+                 int64_t rows_per_block, float* __restrict__ part) {
+    const int c4 = n_cols / 4;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = (r0 + rows_per_block < n_rows) ? r0 + rows_per_block : n_rows;
+    for (int cb = 0; cb < c4; cb += 64) {
+        const int c = cb + (threadIdx.x & 63);
+        const int slice = threadIdx.x >> 6;          // 4 waves take rows r0+slice, +4, ...
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c < c4) {
+            int64_t r = r0 + slice;
+            for (; r + 12 < r1; r += 16) {
+                float4 v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(X + (r + 4 * i) * ld + 4 * c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w; }
+            }
+            for (; r < r1; r += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(X + r * ld + 4 * c);
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            }
+        }
+        __shared__ float4 red[256];
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        if (threadIdx.x < 64 && c < c4) {
+            float4 t = red[threadIdx.x];
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+                const float4 u = red[threadIdx.x + 64 * k];
+                t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+            }
+            *reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * n_cols + 4 * c) = t;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_colsum_final(const float* __restrict__ part, int nb, int n_cols, float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_cols) return;
+    float acc = 0.f;
+    for (int b = 0; b < nb; ++b) acc += part[(int64_t)b * n_cols + c];
+    out[c] = acc;
+}
+
+hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, float* out,
+                      float* workspace, int nb, hipStream_t st) {
+    if (n_cols <= 0) return hipSuccess;
+    const int64_t rpb = (n_rows + nb - 1) / nb;
+    if (n_rows > 0)
+        hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)nb), dim3(256), 0, st, X, ld, n_rows, n_cols, rpb, workspace);
+    else
+        return hipMemsetAsync(out, 0, sizeof(float) * n_cols, st);
+    hipLaunchKernelGGL(k_colsum_final, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, st,
+                       workspace, nb, n_cols, out);
+    return hipGetLastError();
+}
+
 template <bool MEAN_DIV>
 static hipError_t launch_combine(const int32_t* splits, int64_t n, const float* partial, int H,
                                  float* out, int64_t ldo, int vw, hipStream_t st) {

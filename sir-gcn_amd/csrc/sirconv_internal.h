@@ -40,6 +40,9 @@ hipError_t launch_mode_bwd_src(const EdgeArgs& a, int agg, int act, Shape s, hip
 hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
                             int64_t n, hipStream_t st);
 
+hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, float* out,
+                      float* workspace, int nb, hipStream_t st);
+
 hipError_t run_edge(int mode, const EdgeArgs& a, int agg, int act,
                     const int32_t* splits, int64_t n_splits, float* out_final, int64_t ld_final,
                     bool mean_div, hipStream_t st, const char** why);

@@ -24,6 +24,7 @@ SIGNATURES = {
     "sir_last_error": (ctypes.c_char_p, []),
     "sir_mask_words": (ctypes.c_int64, [_I64, _I]),
     "sir_degree_norms": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P]),
+    "sir_col_sum": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _P, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
@@ -115,6 +116,20 @@ def degree_norms(rowptr_dst, rowptr_src, in_norm, out_norm):
     rc = lib.sir_degree_norms(_ptr(rowptr_dst), _ptr(in_norm), _ptr(rowptr_src), _ptr(out_norm), n,
                               _stream(in_norm.device))
     _check(rc, lib)
+
+
+COLSUM_BLOCKS = 1024
+
+
+def col_sum(X):
+    """Deterministic column sums of a tall fp32 [n, m] view (bias gradients)."""
+    lib = load()
+    n, m = X.shape
+    out = torch.empty(m, device=X.device, dtype=torch.float32)
+    ws = torch.empty(COLSUM_BLOCKS * m, device=X.device, dtype=torch.float32)
+    rc = lib.sir_col_sum(_ptr(X), X.stride(0), n, m, _ptr(out), _ptr(ws), _stream(X.device))
+    _check(rc, lib)
+    return out
 
 
 def _ldx(t, H):

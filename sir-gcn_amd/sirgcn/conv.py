@@ -125,6 +125,13 @@ def _tn(A, B):
     return out
 
 
+def _bias_grad(G):
+    """sum over rows (native deterministic column sum when the layout allows)."""
+    if G.shape[1] % 4 == 0 and G.stride(1) == 1 and G.stride(0) % 4 == 0 and G.data_ptr() % 16 == 0:
+        return _native.col_sum(G)
+    return G.sum(0)
+
+
 class SIRConvFunction(torch.autograd.Function):
     """The whole layer (``conv.py:49-67``) with a hand-scheduled backward:
 
@@ -166,7 +173,7 @@ class SIRConvFunction(torch.autograd.Function):
         dY = dY.contiguous()
         G = torch.mm(dY, W_R)
         dW_R = _tn(dY, S) if ctx.needs_input_grad[4] else None
-        db_R = dY.sum(0) if ctx.has_br and ctx.needs_input_grad[5] else None
+        db_R = _bias_grad(dY) if ctx.has_br and ctx.needs_input_grad[5] else None
         in_norm, out_norm = plan.norms(agg)
         partial = _partial(plan, H, X.device)
         Gm = torch.empty((V, H), device=X.device, dtype=torch.float32) if agg == "mean" else None
@@ -186,7 +193,7 @@ class SIRConvFunction(torch.autograd.Function):
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
             dW = _tn(dQK, X)
             dW_Q, dW_K = dW[:H], dW[H:]
-        db_Q = dQK[:, :H].sum(0) if ctx.has_bq and ctx.needs_input_grad[2] else None
+        db_Q = _bias_grad(dQK[:, :H]) if ctx.has_bq and ctx.needs_input_grad[2] else None
         return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None
 
 

@@ -298,3 +298,15 @@ def test_edge_cut_path_single_rank_equals_single_gpu(agg):
              "linear_relation.weight": "dW_R", "linear_relation.bias": "db_R"}
     for n, p in conv.named_parameters():
         assert_parity(p.grad.cpu(), g1[n].cpu(), truth[names[n]], 1e-5, n)
+
+
+@pytest.mark.parametrize("n,m", [(0, 8), (1, 4), (1000, 256), (2_000_003, 256), (5000, 512), (777, 1028)])
+def test_col_sum_bias_gradient(n, m):
+    X = torch.randn(n, m, device=DEV, generator=torch.Generator(device=DEV).manual_seed(n + m))
+    got = _native.col_sum(X)
+    ref32 = X.sum(0)
+    truth = X.double().sum(0)
+    assert_parity(got.cpu(), ref32.cpu(), truth.cpu(), 1e-5, "colsum")
+    assert torch.equal(got, _native.col_sum(X))          # deterministic
+    view = torch.randn(300, 2 * m, device=DEV)[:, :m]    # strided view (the dQ half of dQK)
+    assert_parity(_native.col_sum(view).cpu(), view.sum(0).cpu(), view.double().sum(0).cpu(), 1e-5, "colsum view")
