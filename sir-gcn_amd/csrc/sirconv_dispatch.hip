@@ -61,13 +61,32 @@ k_colsum_partial(const float* __restrict__ X, int64_t ld, int64_t n_rows, int n_
     }
 }
 
-__global__ void __launch_bounds__(256)
+// 64 columns x 16 slices per block; slice k adds partials k, k+16, ... (8 loads in flight),
+// then the 16 slice sums are added in slice order.
+__global__ void __launch_bounds__(1024)
 k_colsum_final(const float* __restrict__ part, int nb, int n_cols, float* __restrict__ out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_cols) return;
+    __shared__ float red[1024];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int slice = threadIdx.x >> 6;
     float acc = 0.f;
-    for (int b = 0; b < nb; ++b) acc += part[(int64_t)b * n_cols + c];
-    out[c] = acc;
+    if (c < n_cols) {
+        int b = slice;
+        for (; b + 7 * 16 < nb; b += 8 * 16) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = part[(int64_t)(b + 16 * i) * n_cols + c];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc += v[i];
+        }
+        for (; b < nb; b += 16) acc += part[(int64_t)b * n_cols + c];
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < 64 && c < n_cols) {
+        float t = red[threadIdx.x];
+        for (int k = 1; k < 16; ++k) t += red[threadIdx.x + 64 * k];
+        out[c] = t;
+    }
 }
 
 hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, float* out,
@@ -78,7 +97,7 @@ hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, fl
         hipLaunchKernelGGL(k_colsum_partial, dim3((unsigned)nb), dim3(256), 0, st, X, ld, n_rows, n_cols, rpb, workspace);
     else
         return hipMemsetAsync(out, 0, sizeof(float) * n_cols, st);
-    hipLaunchKernelGGL(k_colsum_final, dim3((unsigned)((n_cols + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_colsum_final, dim3((unsigned)((n_cols + 63) / 64)), dim3(1024), 0, st,
                        workspace, nb, n_cols, out);
     return hipGetLastError();
 }

@@ -309,10 +309,25 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 //   MODE_BWD_SRC: dK[u] = sum_e sel(bit, t_e), t_e = Gd[v] (* c_e)     -> one gathered row + mask
 // with sel(bit, t) = bit ? t : t*slope (LeakyReLU) / 0 (ReLU): exactly dsig<ACT>(z, t), so the
 // result is bit-identical to the recompute path.  Full-wave rows of float4 only (LPR = 64).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Per-lane select by a wave-uniform 64-bit lane mask: lane l gets (m >> l) & 1 ? if1 : if0.
+// A ballot word is exactly an EXEC-style lane mask, so it is v_cndmask's condition operand
+// (one VALU op instead of shift/and/compare/select).  Pure asm: no memory, freely schedulable.
+__device__ __forceinline__ float lane_select(uint64_t m, float if0, float if1) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(m));
+    return r;
+}
+
 template <int ACT>
-__device__ __forceinline__ float sel(bool pos, float t, float slope) {
-    if constexpr (ACT == ACT_RELU) return pos ? t : 0.f;
-    else return pos ? t : t * slope;
+__device__ __forceinline__ float sel_mask(uint64_t m, float t, float slope) {
+    if constexpr (ACT == ACT_RELU) return lane_select(m, 0.f, t);
+    else return lane_select(m, t * slope, t);
 }
 
 template <int MODE, int ACT, int AGG, int NV, int UU>
@@ -327,18 +342,18 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
 #pragma unroll
     for (int i = 0; i < UU; ++i) {
         if constexpr (MODE == MODE_BWD_SRC) {
-            v[i] = col[e + i];
-            p[i] = perm[e + i];
+            v[i] = __builtin_amdgcn_readfirstlane(col[e + i]);
+            p[i] = __builtin_amdgcn_readfirstlane(perm[e + i]);
         } else {
             p[i] = e + i;
-            if constexpr (AGG == AGG_SYM) v[i] = col[e + i];
+            if constexpr (AGG == AGG_SYM) v[i] = __builtin_amdgcn_readfirstlane(col[e + i]);
         }
     }
     uint64_t wd[UU][NW];
 #pragma unroll
     for (int i = 0; i < UU; ++i)
 #pragma unroll
-        for (int k = 0; k < NW; ++k) wd[i][k] = mask[(int64_t)p[i] * NW + k];
+        for (int k = 0; k < NW; ++k) wd[i][k] = uniform64(mask[(int64_t)p[i] * NW + k]);
     float cf[UU];
     if constexpr (AGG == AGG_SYM) {
 #pragma unroll
@@ -368,8 +383,7 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
                     if constexpr (MODE == MODE_BWD_SRC) t = gc[i][j][w];
                     else t = gv[j][w];
                     if constexpr (AGG == AGG_SYM) t = t * cf[i];
-                    const bool pos = (wd[i][j * 4 + w] >> lane) & 1ull;
-                    acc[j][w] += sel<ACT>(pos, t, slope);
+                    acc[j][w] += sel_mask<ACT>(wd[i][j * 4 + w], t, slope);
                 }
             }
         }

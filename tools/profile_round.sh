@@ -1,0 +1,13 @@
+#!/bin/bash
+# Profiling recipe used for profiles/ (run on the MI355X box from the repo root):
+#   kernel trace + stats, then one PMC pass per counter (FETCH_SIZE and WRITE_SIZE cannot share
+#   a pass on gfx950), then per-launch HBM bytes -> profiles/pmc_traffic.json.
+set -e
+OUT=${1:-gpurun_out}
+ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
+export TMPDIR=/tmp
+mkdir -p "$OUT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/prof.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/pmc_fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/pmc_write.log" 2>&1
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --out "$OUT/pmc_traffic.json" > /dev/null
