@@ -78,6 +78,57 @@ __device__ __forceinline__ float dsig(float z, float t, float slope) {
 }
 
 // ------------------------------------------------------------------------------ vectors
+// Cache-policy experiment knobs (tools/edge_ab.py builds them as separate libraries):
+//   SIR_NT_STREAM = 1: non-temporal loads/stores for the once-touched row-side streams
+//                      (Q/G rows read, S/dQ/dK/partial rows and the sign mask written);
+//   SIR_NT_GATHER = 1: non-temporal loads for the gathered rows too.
+#ifndef SIR_NT_STREAM
+#define SIR_NT_STREAM 0
+#endif
+#ifndef SIR_NT_GATHER
+#define SIR_NT_GATHER 0
+#endif
+typedef float sir_f4 __attribute__((ext_vector_type(4)));
+
+template <int VW, bool NT>
+__device__ __forceinline__ void vload_p(float (&d)[VW], const float* __restrict__ p) {
+    if constexpr (VW == 4 && NT) {
+        const sir_f4 t = __builtin_nontemporal_load(reinterpret_cast<const sir_f4*>(p));
+        d[0] = t.x; d[1] = t.y; d[2] = t.z; d[3] = t.w;
+    } else if constexpr (VW == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        d[0] = t.x; d[1] = t.y; d[2] = t.z; d[3] = t.w;
+    } else {
+#pragma unroll
+        for (int w = 0; w < VW; ++w) d[w] = NT ? __builtin_nontemporal_load(p + w) : p[w];
+    }
+}
+
+template <int VW, bool NT>
+__device__ __forceinline__ void vstore_p(float* __restrict__ p, const float (&s)[VW]) {
+    if constexpr (VW == 4 && NT) {
+        sir_f4 t;
+        t.x = s[0]; t.y = s[1]; t.z = s[2]; t.w = s[3];
+        __builtin_nontemporal_store(t, reinterpret_cast<sir_f4*>(p));
+    } else if constexpr (VW == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(s[0], s[1], s[2], s[3]);
+    } else {
+#pragma unroll
+        for (int w = 0; w < VW; ++w) {
+            if constexpr (NT) __builtin_nontemporal_store(s[w], p + w);
+            else p[w] = s[w];
+        }
+    }
+}
+
+// row-side streams (read or written once) and gathered rows
+template <int VW>
+__device__ __forceinline__ void vload_row(float (&d)[VW], const float* __restrict__ p) { vload_p<VW, SIR_NT_STREAM>(d, p); }
+template <int VW>
+__device__ __forceinline__ void vstore_row(float* __restrict__ p, const float (&s)[VW]) { vstore_p<VW, SIR_NT_STREAM>(p, s); }
+template <int VW>
+__device__ __forceinline__ void vload_gather(float (&d)[VW], const float* __restrict__ p) { vload_p<VW, SIR_NT_GATHER>(d, p); }
+
 template <int VW>
 __device__ __forceinline__ void vload(float (&d)[VW], const float* __restrict__ p) {
     if constexpr (VW == 4) {
@@ -125,14 +176,14 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (c < HC) vload<VW>(cv[i][j], cp + c * VW);
+            if (c < HC) vload_gather<VW>(cv[i][j], cp + c * VW);
         }
         if constexpr (MODE == MODE_BWD_SRC) {
             const float* gp = G + (int64_t)u[i] * ldg;
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const int c = li + LPR * j;
-                if (c < HC) vload<VW>(gc[i][j], gp + c * VW);
+                if (c < HC) vload_gather<VW>(gc[i][j], gp + c * VW);
             }
         }
     }
@@ -156,7 +207,10 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                 }
             }
         }
-        if (lane < UU * NW) mask[(int64_t)e * NW + lane] = mine;
+        if (lane < UU * NW) {
+            if constexpr (SIR_NT_STREAM) __builtin_nontemporal_store(mine, mask + (int64_t)e * NW + lane);
+            else mask[(int64_t)e * NW + lane] = mine;
+        }
     }
 #pragma unroll
     for (int i = 0; i < UU; ++i) {
@@ -230,7 +284,7 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
         const int c = li + LPR * j;
 #pragma unroll
         for (int w = 0; w < VW; ++w) { acc[j][w] = 0.f; rv[j][w] = 0.f; gv[j][w] = 0.f; }
-        if (c < HC) vload<VW>(rv[j], rp + c * VW);
+        if (c < HC) vload_row<VW>(rv[j], rp + c * VW);
     }
     if constexpr (MODE == MODE_BWD_DST) {
         const float* gp = G + (int64_t)row * ldg;
@@ -246,11 +300,11 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
             if (c < HC) {
-                vload<VW>(gv[j], gp + c * VW);
+                vload_row<VW>(gv[j], gp + c * VW);
                 if constexpr (AGG == AGG_MEAN) {
 #pragma unroll
                     for (int w = 0; w < VW; ++w) gv[j][w] = gv[j][w] / degf;   // DivBackward: grad / deg
-                    if (Gm != nullptr && first) vstore<VW>(Gm + (int64_t)row * ldgm + c * VW, gv[j]);
+                    if (Gm != nullptr && first) vstore_row<VW>(Gm + (int64_t)row * ldgm + c * VW, gv[j]);
                 }
             }
         }
@@ -261,6 +315,12 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
     int e = e0;
     for (; e + U <= e1; e += U)
         edge_batch<MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+    if constexpr (U > 8) {
+        if (e + 8 <= e1) {
+            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 8, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+            e += 8;
+        }
+    }
     if constexpr (U > 4) {
         if (e + 4 <= e1) {
             edge_batch<MODE, ACT, AGG, LPR, NV, VW, 4, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
@@ -289,14 +349,14 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (c < HC) vstore<VW>(op + c * VW, acc[j]);
+            if (c < HC) vstore_row<VW>(op + c * VW, acc[j]);
         }
     } else {
         float* pp = partial + (int64_t)slot * H;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (c < HC) vstore<VW>(pp + c * VW, acc[j]);
+            if (c < HC) vstore_row<VW>(pp + c * VW, acc[j]);
         }
     }
 }
@@ -367,7 +427,7 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const int c = lane + 64 * j;
-                if (c < HC) vload<4>(gc[i][j], gp + c * 4);
+                if (c < HC) vload_gather<4>(gc[i][j], gp + c * 4);
             }
         }
     }
@@ -428,11 +488,11 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
         for (int j = 0; j < NV; ++j) {
             const int c = lane + 64 * j;
             if (c < HC) {
-                vload<4>(gv[j], gp + c * 4);
+                vload_row<4>(gv[j], gp + c * 4);
                 if constexpr (AGG == AGG_MEAN) {
 #pragma unroll
                     for (int w = 0; w < 4; ++w) gv[j][w] = gv[j][w] / degf;
-                    if (Gm != nullptr && first) vstore<4>(Gm + (int64_t)row * ldgm + c * 4, gv[j]);
+                    if (Gm != nullptr && first) vstore_row<4>(Gm + (int64_t)row * ldgm + c * 4, gv[j]);
                 }
             }
         }
@@ -442,6 +502,12 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     int e = e0;
     for (; e + U <= e1; e += U)
         mask_batch<MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    if constexpr (U > 8) {
+        if (e + 8 <= e1) {
+            mask_batch<MODE, ACT, AGG, NV, 8>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            e += 8;
+        }
+    }
     if constexpr (U > 4) {
         if (e + 4 <= e1) {
             mask_batch<MODE, ACT, AGG, NV, 4>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
@@ -460,7 +526,7 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int c = lane + 64 * j;
-        if (c < HC) vstore<4>(op + c * 4, acc[j]);
+        if (c < HC) vstore_row<4>(op + c * 4, acc[j]);
     }
 }
 
@@ -525,9 +591,16 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 }
 
 // ------------------------------------------------------------------------------ per-mode launch
+#ifndef SIR_UNROLL
+#define SIR_UNROLL 8      // gathered rows in flight per wave (NV == 1 shapes); 2..16
+#endif
+#if SIR_UNROLL > 16 || SIR_UNROLL < 2
+#error "SIR_UNROLL must be in [2, 16] (tail handles < 16 edges)"
+#endif
+
 template <int MODE, int ACT, int AGG, int LPR, int NV, int VW>
 static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
-    constexpr int U = (NV == 1) ? 8 : 4;
+    constexpr int U = (NV == 1) ? SIR_UNROLL : 4;
     constexpr int RPW = 64 / LPR;
     const int64_t waves = (a.n_items + RPW - 1) / RPW;
     const int64_t blocks = (waves + 3) / 4;
@@ -554,7 +627,7 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
 
 template <int MODE, int ACT, int AGG, int NV>
 static hipError_t launch_mask_t(const EdgeArgs& a, hipStream_t st) {
-    constexpr int U = (NV == 1) ? 8 : (NV == 2 ? 4 : 2);
+    constexpr int U = (NV == 1) ? SIR_UNROLL : (NV == 2 ? 4 : 2);
     const int64_t blocks = (a.n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL((k_edge_mask<MODE, ACT, AGG, NV, U>), dim3((unsigned)blocks), dim3(256), 0, st,
