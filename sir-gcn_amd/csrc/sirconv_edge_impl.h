@@ -591,16 +591,28 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 }
 
 // ------------------------------------------------------------------------------ per-mode launch
-#ifndef SIR_UNROLL
-#define SIR_UNROLL 8      // gathered rows in flight per wave (NV == 1 shapes); 2..16
+// Gathered rows in flight per wave for NV == 1 shapes, per pass (A/B-tuned on MI355X with
+// tools/edge_ab.py: more rows in flight per wave than this only adds cache pressure).
+#ifndef SIR_UNROLL_FWD
+#define SIR_UNROLL_FWD 4
 #endif
-#if SIR_UNROLL > 16 || SIR_UNROLL < 2
-#error "SIR_UNROLL must be in [2, 16] (tail handles < 16 edges)"
+#ifndef SIR_UNROLL_DST
+#define SIR_UNROLL_DST 8
 #endif
+#ifndef SIR_UNROLL_SRC
+#define SIR_UNROLL_SRC 8
+#endif
+#if SIR_UNROLL_FWD > 16 || SIR_UNROLL_DST > 16 || SIR_UNROLL_SRC > 16
+#error "unroll must be <= 16 (the tail covers < 16 edges)"
+#endif
+template <int MODE>
+constexpr int unroll_of() {
+    return MODE == MODE_FWD ? SIR_UNROLL_FWD : (MODE == MODE_BWD_DST ? SIR_UNROLL_DST : SIR_UNROLL_SRC);
+}
 
 template <int MODE, int ACT, int AGG, int LPR, int NV, int VW>
 static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
-    constexpr int U = (NV == 1) ? SIR_UNROLL : 4;
+    constexpr int U = (NV == 1) ? unroll_of<MODE>() : 4;
     constexpr int RPW = 64 / LPR;
     const int64_t waves = (a.n_items + RPW - 1) / RPW;
     const int64_t blocks = (waves + 3) / 4;
@@ -627,7 +639,7 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
 
 template <int MODE, int ACT, int AGG, int NV>
 static hipError_t launch_mask_t(const EdgeArgs& a, hipStream_t st) {
-    constexpr int U = (NV == 1) ? SIR_UNROLL : (NV == 2 ? 4 : 2);
+    constexpr int U = (NV == 1) ? unroll_of<MODE>() : (NV == 2 ? 4 : 2);
     const int64_t blocks = (a.n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL((k_edge_mask<MODE, ACT, AGG, NV, U>), dim3((unsigned)blocks), dim3(256), 0, st,

@@ -35,12 +35,13 @@ def main():
     ap.add_argument("--H", type=int, default=256)
     ap.add_argument("--agg", default="sum")
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--libs", nargs="+", required=True)
     a = ap.parse_args()
     V, E, alpha = NAMED[a.graph]
     src, dst = powerlaw_edges(V, E, alpha, seed=0)
     dev = "cuda"
-    plan = GraphPlan(src, dst, V, dev)
+    plan = GraphPlan(src, dst, V, dev, chunk=a.chunk)
     H = a.H
     g = torch.Generator(device=dev).manual_seed(0)
     QK = torch.randn(V, 2 * H, device=dev, generator=g)
