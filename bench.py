@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--force-dist", action="store_true",
                     help="run the edge-cut (sirgcn.dist) code path even at world size 1")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-file", default=None,
+                    help="PMC traffic summary (tools/pmc_traffic.py); default profiles/pmc_traffic_<graph>.json")
     return ap.parse_args()
 
 
@@ -201,12 +202,13 @@ def main():
                          "GBps": round(bytes_ / (t * 1e-3) / 1e9, 1)}
     dom = max(kernels, key=lambda k: kernels[k]["ms"])
     traffic = None
+    pmc_file = args.pmc_file or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.graph}.json")
     try:
-        with open(args.pmc_file) as f:
+        with open(pmc_file) as f:
             pmc = json.load(f)
         rec = pmc.get("kernels", {}).get(dom)
         if rec and pmc.get("graph") == args.graph and pmc.get("agg") == args.agg and pmc.get("H") == H:
-            traffic = rec["hbm_bytes_per_launch"]
+            traffic = rec["hbm_bytes_per_launch"]      # L2<->fabric bytes (Infinity-Cache hits included)
     except (OSError, ValueError):
         pass
     d = kernels[dom]
