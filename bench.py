@@ -124,8 +124,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))     # one rank per GPU (wraps only in rehearsals)
+    torch.cuda.set_device(dev)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
