@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) for real runs; gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the edge-cut (sirgcn.dist) code path even at world size 1")
     ap.add_argument("--pmc-file", default=None,
@@ -128,7 +130,10 @@ def main():
     dev = torch.device("cuda", local % max(ndev, 1))     # one rank per GPU (wraps only in rehearsals)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from sirgcn import SIRConv, _native
     from sirgcn.graph import DEFAULT_CHUNK
@@ -186,7 +191,7 @@ def main():
     if world > 1:
         dist.barrier()
     _native.enable_timing(False)
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = el_t.item()

@@ -28,6 +28,39 @@ from . import _native
 from .graph import DEFAULT_CHUNK, build_row_csr
 
 
+def _host_staged(group, t):
+    """gloo cannot run these collectives on device tensors: stage through host memory
+    (rehearsals / CPU tests only; RCCL runs them in place)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_gather_into(out, inp, group=None):
+    if _host_staged(group, inp):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def reduce_scatter_into(out, inp, group=None):
+    if _host_staged(group, inp):
+        o = out.cpu()
+        dist.reduce_scatter_tensor(o, inp.cpu(), op=dist.ReduceOp.SUM, group=group)
+        out.copy_(o)
+    else:
+        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
+
+
+def all_reduce_sum(t, group=None):
+    if _host_staged(group, t):
+        c = t.cpu()
+        dist.all_reduce(c, group=group)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, group=group)
+
+
 def partition_rows(in_deg, world):
     """Row boundaries [0, r_1, ..., V] with ≈E/world in-edges per range (edge-balanced)."""
     V = in_deg.numel()
@@ -77,7 +110,7 @@ class DistGraph:
         # global out-degree in padded layout: local histograms summed over ranks
         out_local = (self.src.rowptr[1:] - self.src.rowptr[:-1]).to(torch.int64)
         if world > 1:
-            dist.all_reduce(out_local, group=group)
+            all_reduce_sum(out_local, group=group)
         self.out_deg = out_local
         self._norms = {}
 
@@ -115,7 +148,7 @@ class DistEdgeAggregate(torch.autograd.Function):
         K_send[:plan.n_rows] = K_local
         K_all = torch.empty((plan.padded_rows, H), device=dev, dtype=torch.float32)
         if plan.world > 1:
-            dist.all_gather_into_tensor(K_all, K_send, group=plan.group)
+            all_gather_into(K_all, K_send, group=plan.group)
         else:
             K_all.copy_(K_send)
         in_norm, out_norm = plan.norms(agg)
@@ -158,7 +191,7 @@ class DistEdgeAggregate(torch.autograd.Function):
                                  agg, act, slope, dK_all, partial, mask)
         dK_mine = torch.empty((plan.max_rows, H), device=dev, dtype=torch.float32)
         if plan.world > 1:
-            dist.reduce_scatter_tensor(dK_mine, dK_all, op=dist.ReduceOp.SUM, group=plan.group)
+            reduce_scatter_into(dK_mine, dK_all, group=plan.group)
         else:
             dK_mine.copy_(dK_all)
         return dQ, dK_mine[:plan.n_rows], None, None, None, None, None, None, None
@@ -195,7 +228,7 @@ class DistSIRConv(torch.nn.Module):
         if not params or not dist.is_initialized() or dist.get_world_size(group) == 1:
             return
         flat = torch.cat([p.grad.reshape(-1) for p in params])
-        dist.all_reduce(flat, group=group)
+        all_reduce_sum(flat, group=group)
         off = 0
         for p in params:
             n = p.grad.numel()
