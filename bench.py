@@ -213,7 +213,8 @@ def main():
         with open(pmc_file) as f:
             pmc = json.load(f)
         rec = pmc.get("kernels", {}).get(dom)
-        if rec and pmc.get("graph") == args.graph and pmc.get("agg") == args.agg and pmc.get("H") == H:
+        if (rec and world == 1 and pmc.get("graph") == args.graph and pmc.get("agg") == args.agg
+                and pmc.get("H") == H):
             traffic = rec["hbm_bytes_per_launch"]      # L2<->fabric bytes (Infinity-Cache hits included)
     except (OSError, ValueError):
         pass
