@@ -138,6 +138,46 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          int agg, int act, float slope,
                          float* dK, int64_t lddk, float* partial, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Edge-materialised path: agg_type='max' (conv.py:46-47 + DGL max reduce) and sigma callables the
+ * fused kernels do not cover (e.g. Sequential(ReLU, Linear, ReLU), dictionary-lookup/model.py:17).
+ * Edge rows are in destination-CSR order (position e of the dst CSR).  F = feature width
+ * (<= 1024).  Same work plan (items / splits) as above.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Z[e] = Q[row(e)] + K[col[e]]  (the `edges.dst['eq'] + edges.src['ek']` of conv.py:45) */
+int sir_edge_gather_add(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                        int64_t F, const float* Q, int64_t ldq, const float* K, int64_t ldk,
+                        float* Z, int64_t ldz, void* stream);
+
+/* out[row] = sum_{e in row} c_e * X[idx(e)],  idx(e) = perm ? perm[e] : e,
+ * c_e = norm_col[col[e]] * norm_row[row] when norm_row != NULL (the sym norm product, conv.py:45),
+ * mean != 0 divides by max(deg, 1) (fn.mean).  Rows without edges get 0.  Sequential in edge order
+ * within a row (split rows: partial rows combined in slot order; partial = n_slots * F floats).
+ * With the destination CSR this is update_all(copy_e, sum|mean); with the source CSR and perm it
+ * is the index_add of the src gather's backward (dK). */
+int sir_segment_sum(const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+                    const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
+                    int64_t F, const float* X, int64_t ldx, const float* norm_row, const float* norm_col,
+                    int mean, float* out, int64_t ldo, float* partial, void* stream);
+
+/* Backward of sir_segment_sum over the destination CSR: dM[e] = c_e * g[row],
+ * g = dS (mean: dS / max(deg, 1)). */
+int sir_edge_broadcast(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                       int64_t F, const float* dS, int64_t lds, const float* norm_row, const float* norm_col,
+                       int mean, float* dM, int64_t ldm, void* stream);
+
+/* DGL max reduce: Y[row] = max_{e in row} M[e] elementwise, arg = the FIRST arg-max edge position
+ * (ties keep the earlier edge), rows without edges: Y = 0, arg = -1.
+ * pval/parg: n_slots * F workspace for split rows. */
+int sir_segment_max(const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
+                    int64_t F, const float* M, int64_t ldm, float* Y, int64_t ldy, int32_t* arg, int64_t lda,
+                    float* pval, int32_t* parg, void* stream);
+
+/* Backward of sir_segment_max: dM[e] = (arg[row] == e) ? dY[row] : 0 for every edge (dM fully written). */
+int sir_segment_max_bwd(const int32_t* items, int64_t n_items, int64_t F, const int32_t* arg, int64_t lda,
+                        const float* dY, int64_t ldy, float* dM, int64_t ldm, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,5 +10,5 @@ vectors in ``tests/golden/*.npz``, which were produced by executing the referenc
 """
 from .sirconv_oracle import (  # noqa: F401
     ACTS, AGGS, act_fwd, act_bwd, csr_by_dst, csr_by_src, degree_norms,
-    edge_agg_fwd, edge_agg_bwd, layer_fwd_bwd, reference_cpu_step,
+    edge_agg_fwd, edge_agg_bwd, layer_fwd_bwd, max_first_wins, reference_cpu_step,
 )

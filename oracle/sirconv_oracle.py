@@ -142,6 +142,45 @@ def edge_agg_bwd(src, dst, num_nodes, Q, K, dS, agg, act, slope=0.01):
     return dQ, dK
 
 
+# ----------------------------------------------------------------------------- max
+def max_first_wins(dst, num_nodes, M):
+    """DGL ``fn.max`` over in-edges (``conv.py:41,63`` with agg_type='max'): elementwise max, the
+    arg is the FIRST maximal edge in CSC order (= smallest edge id; DGL SpMMCmpCsr updates on
+    strict >), rows without in-edges give 0 / arg -1.  Returns (Y, arg) with arg = edge ids."""
+    dst = torch.as_tensor(dst, dtype=torch.int64)
+    E, F = M.shape
+    Y = torch.zeros((num_nodes, F), dtype=M.dtype)
+    arg = torch.full((num_nodes, F), -1, dtype=torch.int64)
+    if E == 0:
+        return Y, arg
+    idx = dst.unsqueeze(1).expand(E, F)
+    Y = Y.scatter_reduce(0, idx, M, reduce="amax", include_self=False)
+    eid = torch.arange(E).unsqueeze(1).expand(E, F)
+    cand = torch.where(M == Y[dst], eid, torch.full_like(eid, E))
+    arg = torch.full((num_nodes, F), E, dtype=torch.int64).scatter_reduce(0, idx, cand, reduce="amin")
+    arg[arg == E] = -1
+    return Y, arg
+
+
+class _MaxFirstWins(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, M, dst, num_nodes):
+        Y, arg = max_first_wins(dst, num_nodes, M)
+        ctx.save_for_backward(arg, torch.as_tensor(dst, dtype=torch.int64))
+        ctx.E = M.shape[0]
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        arg, dst = ctx.saved_tensors
+        E, F = ctx.E, dY.shape[1]
+        dM = torch.zeros((E, F), dtype=dY.dtype)
+        hit = arg >= 0
+        rows, cols = torch.nonzero(hit, as_tuple=True)
+        dM[arg[rows, cols], cols] = dY[rows, cols]
+        return dM, None, None
+
+
 # ----------------------------------------------------------------------------- layer
 def reference_cpu_step(src, dst, num_nodes, X, W_Q, b_Q, W_K, W_R, b_R, dY, agg, act,
                        slope=0.01, need_grads=True):
@@ -158,8 +197,25 @@ def reference_cpu_step(src, dst, num_nodes, X, W_Q, b_Q, W_K, W_R, b_R, dY, agg,
     with torch.set_grad_enabled(need_grads):
         K = torch.nn.functional.linear(X_, W_K_)
         Q = torch.nn.functional.linear(X_, W_Q_, b_Q_)
-        S = edge_agg_fwd(src, dst, num_nodes, Q, K, agg, act, slope)
-        Y = torch.nn.functional.linear(S, W_R_, b_R_)
+        if callable(act) or agg == "max":
+            # the general UDF dataflow (conv.py:43-47): sigma is any callable, max -> per-edge W_R
+            fn = act if callable(act) else (lambda z: act_fwd(z, act, slope))
+            a = fn(Q.index_select(0, dst) + K.index_select(0, src))
+            if agg == "max":
+                Y = _MaxFirstWins.apply(torch.nn.functional.linear(a, W_R_, b_R_), dst, num_nodes)
+            else:
+                in_deg = torch.bincount(dst, minlength=num_nodes)
+                out_deg = torch.bincount(src, minlength=num_nodes)
+                in_norm, out_norm = degree_norms(in_deg, out_deg, agg)
+                c = _edge_coef(out_norm, in_norm, src, dst, agg)
+                m = c * a if c is not None else a
+                S = torch.zeros((num_nodes, a.shape[1]), dtype=m.dtype).index_add(0, dst, m)
+                if agg == "mean":
+                    S = S / in_deg.clamp(1, max(int(src.numel()), 1)).to(S.dtype).unsqueeze(-1)
+                Y = torch.nn.functional.linear(S, W_R_, b_R_)
+        else:
+            S = edge_agg_fwd(src, dst, num_nodes, Q, K, agg, act, slope)
+            Y = torch.nn.functional.linear(S, W_R_, b_R_)
     out = {"Y": Y.detach()}
     if need_grads:
         Y.backward(dY)

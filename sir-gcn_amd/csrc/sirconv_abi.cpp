@@ -196,4 +196,86 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
     return finish(fn, err, why);
 }
 
+// ------------------------------------------------------------------------------ generic path
+static int check_generic(const char* fn, int64_t n_items, int64_t F, const int32_t* items) {
+    if (F <= 0 || F > 1024) return fail(SIR_EINVAL, fn, "F must be in [1, 1024]");
+    if (n_items < 0) return fail(SIR_EINVAL, fn, "negative item count");
+    if (n_items > 0 && items == nullptr) return fail(SIR_EINVAL, fn, "NULL items");
+    return SIR_OK;
+}
+
+int sir_edge_gather_add(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                        int64_t F, const float* Q, int64_t ldq, const float* K, int64_t ldk,
+                        float* Z, int64_t ldz, void* stream) {
+    const char* fn = "sir_edge_gather_add";
+    int rc = check_generic(fn, n_items, F, items);
+    if (rc) return rc;
+    if (ldq < F || ldk < F || ldz < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if (n_items > 0 && (Q == nullptr || K == nullptr)) return fail(SIR_EINVAL, fn, "NULL Q/K");
+    sir::GenericArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.F = (int)F;
+    a.X = Q; a.ldx = ldq; a.X2 = K; a.ldx2 = ldk; a.out = Z; a.ldo = ldz;
+    return finish(fn, sir::run_gather_add(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
+}
+
+int sir_segment_sum(const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+                    const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
+                    int64_t F, const float* X, int64_t ldx, const float* norm_row, const float* norm_col,
+                    int mean, float* out, int64_t ldo, float* partial, void* stream) {
+    const char* fn = "sir_segment_sum";
+    int rc = check_generic(fn, n_items, F, items);
+    if (rc) return rc;
+    if (ldx < F || ldo < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if ((norm_row == nullptr) != (norm_col == nullptr)) return fail(SIR_EINVAL, fn, "norm_row/norm_col pairing");
+    if (n_splits > 0 && (splits == nullptr || partial == nullptr)) return fail(SIR_EINVAL, fn, "split rows need splits + partial");
+    if (n_items > 0 && out == nullptr) return fail(SIR_EINVAL, fn, "NULL out");
+    sir::GenericArgs a{};
+    a.rowptr = rowptr; a.col = col; a.perm = perm; a.items = items; a.n_items = n_items;
+    a.splits = splits; a.n_splits = n_splits; a.F = (int)F; a.X = X; a.ldx = ldx;
+    a.norm_row = norm_row; a.norm_col = norm_col; a.mean = mean; a.out = out; a.ldo = ldo; a.partial = partial;
+    return finish(fn, sir::run_seg_sum(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
+}
+
+int sir_edge_broadcast(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                       int64_t F, const float* dS, int64_t lds, const float* norm_row, const float* norm_col,
+                       int mean, float* dM, int64_t ldm, void* stream) {
+    const char* fn = "sir_edge_broadcast";
+    int rc = check_generic(fn, n_items, F, items);
+    if (rc) return rc;
+    if (lds < F || ldm < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if ((norm_row == nullptr) != (norm_col == nullptr)) return fail(SIR_EINVAL, fn, "norm_row/norm_col pairing");
+    if (mean && rowptr == nullptr && n_items > 0) return fail(SIR_EINVAL, fn, "mean needs rowptr");
+    sir::GenericArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.F = (int)F;
+    a.X = dS; a.ldx = lds; a.norm_row = norm_row; a.norm_col = norm_col; a.mean = mean; a.out = dM; a.ldo = ldm;
+    return finish(fn, sir::run_edge_bcast(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
+}
+
+int sir_segment_max(const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
+                    int64_t F, const float* M, int64_t ldm, float* Y, int64_t ldy, int32_t* arg, int64_t lda,
+                    float* pval, int32_t* parg, void* stream) {
+    const char* fn = "sir_segment_max";
+    int rc = check_generic(fn, n_items, F, items);
+    if (rc) return rc;
+    if (ldm < F || ldy < F || lda < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if (n_splits > 0 && (splits == nullptr || pval == nullptr || parg == nullptr))
+        return fail(SIR_EINVAL, fn, "split rows need splits + pval + parg");
+    sir::GenericArgs a{};
+    a.items = items; a.n_items = n_items; a.splits = splits; a.n_splits = n_splits; a.F = (int)F;
+    a.X = M; a.ldx = ldm; a.out = Y; a.ldo = ldy; a.arg = arg; a.lda = lda; a.partial = pval; a.parg = parg;
+    return finish(fn, sir::run_seg_max(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
+}
+
+int sir_segment_max_bwd(const int32_t* items, int64_t n_items, int64_t F, const int32_t* arg, int64_t lda,
+                        const float* dY, int64_t ldy, float* dM, int64_t ldm, void* stream) {
+    const char* fn = "sir_segment_max_bwd";
+    int rc = check_generic(fn, n_items, F, items);
+    if (rc) return rc;
+    if (ldm < F || ldy < F || lda < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    sir::GenericArgs a{};
+    a.items = items; a.n_items = n_items; a.F = (int)F; a.arg = const_cast<int*>(arg); a.lda = lda;
+    a.X = dY; a.ldx = ldy; a.out = dM; a.ldo = ldm;
+    return finish(fn, sir::run_seg_max_bwd(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
+}
+
 }  // extern "C"

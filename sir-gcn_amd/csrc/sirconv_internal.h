@@ -37,6 +37,33 @@ hipError_t launch_mode_fwd(const EdgeArgs& a, int agg, int act, Shape s, hipStre
 hipError_t launch_mode_bwd_dst(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
 hipError_t launch_mode_bwd_src(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
 
+// edge-materialised (generic) path, sirconv_generic.hip
+struct GenericArgs {
+    const int* rowptr;
+    const int* col;
+    const int* perm;
+    const int32_t* items;
+    int64_t n_items;
+    const int32_t* splits;
+    int64_t n_splits;
+    int F;
+    const float* X;  int64_t ldx;
+    const float* X2; int64_t ldx2;
+    const float* norm_row;
+    const float* norm_col;
+    int mean;
+    float* out;  int64_t ldo;
+    float* partial;
+    int* arg;  int64_t lda;
+    int* parg;
+};
+
+hipError_t run_gather_add(const GenericArgs& a, hipStream_t st);
+hipError_t run_seg_sum(const GenericArgs& a, hipStream_t st);
+hipError_t run_edge_bcast(const GenericArgs& a, hipStream_t st);
+hipError_t run_seg_max(const GenericArgs& a, hipStream_t st);
+hipError_t run_seg_max_bwd(const GenericArgs& a, hipStream_t st);
+
 hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
                             int64_t n, hipStream_t st);
 

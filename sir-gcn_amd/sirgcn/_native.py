@@ -25,6 +25,12 @@ SIGNATURES = {
     "sir_mask_words": (ctypes.c_int64, [_I64, _I]),
     "sir_degree_norms": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P]),
     "sir_col_sum": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _P, _P]),
+    "sir_edge_gather_add": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P]),
+    "sir_segment_sum": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64,
+                                       _P, _P]),
+    "sir_edge_broadcast": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64, _P]),
+    "sir_segment_max": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _P]),
+    "sir_segment_max_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
@@ -169,4 +175,54 @@ def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, p
             _ptr(K), _ldx(K, H), _ptr(Q), _ldx(Q, H), _ptr(mask), _ptr(Gd), _ld(Gd, H),
             _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
             _ptr(dK), _ld(dK, H), _ptr(partial), _stream(dK.device))
+    _check(rc, lib)
+
+
+# ------------------------------------------------------------------------------ generic path
+def edge_gather_add(csr, Q, K, Z):
+    lib = load()
+    F = Z.shape[1]
+    with _Timed("sir_edge_gather_add", Z.device):
+        rc = lib.sir_edge_gather_add(_ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, F,
+                                     _ptr(Q), _ld(Q, F), _ptr(K), _ld(K, F), _ptr(Z), _ld(Z, F), _stream(Z.device))
+    _check(rc, lib)
+
+
+def segment_sum(csr, X, out, norm_row=None, norm_col=None, mean=False, perm=None, partial=None):
+    lib = load()
+    F = out.shape[1]
+    with _Timed("sir_segment_sum", out.device):
+        rc = lib.sir_segment_sum(_ptr(csr.rowptr), _ptr(csr.col), _ptr(perm), _ptr(csr.items), csr.n_items,
+                                 _ptr(csr.splits), csr.n_splits, F, _ptr(X), _ld(X, F), _ptr(norm_row),
+                                 _ptr(norm_col), int(bool(mean)), _ptr(out), _ld(out, F), _ptr(partial),
+                                 _stream(out.device))
+    _check(rc, lib)
+
+
+def edge_broadcast(csr, dS, dM, norm_row=None, norm_col=None, mean=False):
+    lib = load()
+    F = dM.shape[1]
+    with _Timed("sir_edge_broadcast", dM.device):
+        rc = lib.sir_edge_broadcast(_ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, F,
+                                    _ptr(dS), _ld(dS, F), _ptr(norm_row), _ptr(norm_col), int(bool(mean)),
+                                    _ptr(dM), _ld(dM, F), _stream(dM.device))
+    _check(rc, lib)
+
+
+def segment_max(csr, M, Y, arg, pval=None, parg=None):
+    lib = load()
+    F = Y.shape[1]
+    with _Timed("sir_segment_max", Y.device):
+        rc = lib.sir_segment_max(_ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits, F,
+                                 _ptr(M), _ld(M, F), _ptr(Y), _ld(Y, F), _ptr(arg), _ld(arg, F),
+                                 _ptr(pval), _ptr(parg), _stream(Y.device))
+    _check(rc, lib)
+
+
+def segment_max_bwd(csr, arg, dY, dM):
+    lib = load()
+    F = dM.shape[1]
+    with _Timed("sir_segment_max_bwd", dM.device):
+        rc = lib.sir_segment_max_bwd(_ptr(csr.items), csr.n_items, F, _ptr(arg), _ld(arg, F),
+                                     _ptr(dY), _ld(dY, F), _ptr(dM), _ld(dM, F), _stream(dM.device))
     _check(rc, lib)

@@ -202,9 +202,9 @@ class SIRConv(nn.Module):
 
     .. math::  h_u^* = \sum_{v \in \mathcal{N}(u)} W_R \, \sigma(W_Q h_u + W_K h_v)
 
-    Same parameters as the reference (``conv.py:13-31``).  ``agg_type`` in
-    {``sum``, ``mean``, ``sym``} runs natively; ``max`` is accepted by the constructor for
-    state-dict compatibility but raises at ``forward`` until its kernel lands.
+    Same parameters as the reference (``conv.py:13-31``).  ``sum``/``mean``/``sym`` with an
+    elementwise sigma (ReLU, LeakyReLU, GELU, Identity) run on the fused edge kernels; ``max`` and
+    any other sigma callable run on the edge-materialised native path (``sirgcn.generic``).
     """
 
     use_fused = True      # whole-layer Function when dropout is off and inputs are fp32
@@ -238,18 +238,24 @@ class SIRConv(nn.Module):
         return QK
 
     def forward(self, graph, feat):
-        if self._agg_type == "max":
-            raise NotImplementedError("SIRConv(agg_type='max'): native kernel not built yet (SURVEY §8f #1)")
         if isinstance(feat, tuple):          # expand_as_pair: (src feats, dst feats)
             feat_key, feat_query = feat
         else:
             feat_key = feat_query = feat
         if feat_query.dim() != 2:
             raise ValueError("SIRConv expects 2-D node features [V, input_dim]")
-        act, slope = activation_code(self.activation)
+        if feat_query.device.type != "cuda":
+            raise RuntimeError("SIRConv native path needs a ROCm GPU tensor (no CPU fallback)")
         plan = get_plan(graph, feat_query.device, self.chunk)
         if plan.num_nodes != feat_query.shape[0]:
             raise ValueError(f"feat has {feat_query.shape[0]} rows, graph has {plan.num_nodes} nodes")
+        try:
+            act, slope = activation_code(self.activation)
+        except NotImplementedError:
+            act = None
+        if act is None or self._agg_type == "max":
+            from .generic import generic_forward       # edge-materialised native path
+            return generic_forward(self, plan, feat_key, feat_query)
         H = self.linear_query.out_features
         fused = (self.use_fused and feat_key is feat_query and feat_query.dtype == torch.float32 and feat_query.is_cuda
                  and not torch.is_autocast_enabled() and not (self.training and self.dropout.p > 0)

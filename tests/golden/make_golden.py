@@ -87,6 +87,19 @@ def graph_long(seed=13):
     return V, np.asarray(src, np.int64)[perm], np.asarray(dst, np.int64)[perm]
 
 
+def graph_small_nodup(seed=11):
+    """graph_small without duplicate edges: continuous data then has no max ties, where the shim's
+    amax backward (tie-splitting) and DGL's first-arg-max backward would differ."""
+    V, src, dst = graph_small(seed)
+    seen, keep = set(), []
+    for i, (u, v) in enumerate(zip(src.tolist(), dst.tolist())):
+        if (u, v) not in seen:
+            seen.add((u, v))
+            keep.append(i)
+    keep = np.asarray(keep)
+    return V, src[keep], dst[keep]
+
+
 def graph_empty():
     return 16, np.zeros(0, np.int64), np.zeros(0, np.int64)
 
@@ -99,6 +112,8 @@ def make_act(kind, H, seed):
         return nn.LeakyReLU(0.2, inplace=True), {}
     if kind == "gelu":
         return nn.GELU(), {}
+    if kind == "tanh":  # a sigma callable without a fused kernel (generic native path)
+        return nn.Tanh(), {}
     if kind == "seq":  # dictionary-lookup/model.py:17
         torch.manual_seed(seed + 7)
         act = nn.Sequential(nn.ReLU(inplace=True), nn.Linear(H, H), nn.ReLU(inplace=True))
@@ -202,6 +217,18 @@ def main():
     cases.append(run_case(conv_mod, "empty_sum_leaky_f32", empty, 16, 32, 8, "sum", "leaky", torch.float32, seed))
     seed += 1
     cases.append(run_case(conv_mod, "empty_sym_relu_f32", empty, 16, 32, 8, "sym", "relu", torch.float32, seed))
+    # round-1 additions (appended so earlier fixtures keep their seeds): max aggregation on a
+    # duplicate-free graph (no ties), and sigma callables without a fused kernel
+    nodup = graph_small_nodup()
+    for act in ("relu", "leaky", "gelu"):
+        seed += 1
+        cases.append(run_case(conv_mod, f"nodup_max_{act}_f32", nodup, 16, 32, 8, "max", act, torch.float32, seed))
+    seed += 1
+    cases.append(run_case(conv_mod, "nodup_max_leaky_h256_f32", nodup, 32, 256, 40, "max", "leaky", torch.float32, seed))
+    seed += 1
+    cases.append(run_case(conv_mod, "small_sym_tanh_f32", small, 16, 32, 8, "sym", "tanh", torch.float32, seed))
+    seed += 1
+    cases.append(run_case(conv_mod, "small_mean_seq_f32", small, 16, 64, 16, "mean", "seq", torch.float32, seed))
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "reference": "briangodwinlim/SIR-GCN models/conv.py:7-67 (snapshot 2025-08-24), via DGL-2.1.0 semantics shim",

@@ -10,7 +10,7 @@ import oracle
 from conftest import assert_close, golden_manifest, load_case
 
 CASES = golden_manifest()
-KERNEL_CASES = [c for c in CASES if c["agg"] in oracle.AGGS and c["act"] != "seq"]
+KERNEL_CASES = [c for c in CASES if c["agg"] in oracle.AGGS and c["act"] in oracle.ACTS]
 
 
 def _t(x):
@@ -83,3 +83,43 @@ def test_isolated_nodes_output_bias():
     """Appendix A.6: sum/mean/sym -> isolated destination outputs b_R."""
     z = load_case("empty_sum_leaky_f32")
     assert np.array_equal(z["Y"], np.broadcast_to(z["b_R"], z["Y"].shape))
+
+
+# ------------------------------------------------------------------ max / sigma callables
+def _act_from_case(case, z, dtype=None):
+    from torch import nn
+    if case["act"] == "tanh":
+        return nn.Tanh()
+    if case["act"] == "seq":
+        lin = nn.Linear(case["H"], case["H"])
+        with torch.no_grad():
+            lin.weight.copy_(_t(z["act_W"])); lin.bias.copy_(_t(z["act_b"]))
+        seq = nn.Sequential(nn.ReLU(), lin, nn.ReLU())
+        return seq.to(dtype) if dtype is not None else seq
+    return case["act"]
+
+
+GENERIC = [c for c in CASES if c["agg"] == "max" or c["act"] in ("seq", "tanh")]
+
+
+@pytest.mark.parametrize("case", GENERIC, ids=[c["name"] for c in GENERIC])
+def test_generic_layer_matches_reference(case):
+    """max (DGL first-arg-max) and sigma callables through the oracle's general UDF dataflow."""
+    z = load_case(case["name"])
+    args = [_t(z[k]) for k in ("X", "W_Q", "b_Q", "W_K", "W_R", "b_R", "dY")]
+    act = _act_from_case(case, z)
+    ref = oracle.reference_cpu_step(z["src"], z["dst"], case["V"], *args, case["agg"], act, case["slope"])
+    assert_close(ref["Y"], z["Y"], 1e-5, f"{case['name']} Y")
+    ties_possible = case["agg"] == "max" and not case["name"].startswith("nodup")
+    if ties_possible:
+        return      # duplicate edges tie in max: the shim splits tie gradients, DGL gives them to the first
+    for key in ("dX", "dW_Q", "db_Q", "dW_K", "dW_R", "db_R"):
+        assert_close(ref[key], z[key], 1e-5, f"{case['name']} {key}")
+
+
+def test_max_first_wins_semantics():
+    M = torch.tensor([[1.0, 5.0], [3.0, 5.0], [3.0, 0.0]])
+    dst = torch.tensor([0, 0, 0])
+    Y, arg = oracle.max_first_wins(dst, 2, M)
+    assert Y.tolist() == [[3.0, 5.0], [0.0, 0.0]]
+    assert arg.tolist() == [[1, 0], [-1, -1]]           # ties -> earliest edge; empty row -> -1
