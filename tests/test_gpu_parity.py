@@ -403,7 +403,7 @@ def test_max_split_rows_and_isolated_nodes(chunk):
 
 
 def test_segment_max_first_wins_on_ties():
-    plan = GraphPlan(torch.tensor([0, 1, 2, 3]), torch.tensor([0, 0, 0, 1]), 3, DEV)
+    plan = GraphPlan(torch.tensor([0, 1, 2, 2]), torch.tensor([0, 0, 0, 1]), 3, DEV)
     M = torch.tensor([[1.0, 5.0], [3.0, 5.0], [3.0, 0.0], [-7.0, -2.0]], device=DEV)
     Y = torch.empty(3, 2, device=DEV); arg = torch.empty(3, 2, device=DEV, dtype=torch.int32)
     _native.segment_max(plan.dst, M, Y, arg)
