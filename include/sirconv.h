@@ -178,6 +178,27 @@ int sir_segment_max(const int32_t* items, int64_t n_items, const int32_t* splits
 int sir_segment_max_bwd(const int32_t* items, int64_t n_items, int64_t F, const int32_t* arg, int64_t lda,
                         const float* dY, int64_t ldy, float* dM, int64_t ldm, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * GraphNorm (models/norm.py:7-29) on a batched graph: graph b owns node rows [off[b], off[b+1])
+ * (off = int64 [B+1], the prefix sum of batch_num_nodes).  Per graph and feature:
+ *   mean = sum x / n,  d = x - mean * mean_scale,  std = sqrt(sum d^2 / n + eps),
+ *   y = (weight * d) / std + bias
+ * Sums run in node order (the reference's scatter_add_ order).  bias / mean_scale may be NULL
+ * (the reference's bias=False -> + 0, mean_scale=False -> * 1).  mean/std: [B, F] outputs kept
+ * for the backward.  F <= 65536.
+ * ------------------------------------------------------------------------------------------- */
+int sir_graph_norm_fwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                       const float* weight, const float* bias, const float* mean_scale, float eps,
+                       float* Y, int64_t ldy, float* mean, float* std_, void* stream);
+
+/* Backward: dX (fully written) and per-graph partials [B, F] of the parameter gradients
+ * (dweight = sum_b dw_part, dmean_scale = sum_b dms_part, dbias = sum_b db_part; dms_part may be
+ * NULL when mean_scale is NULL). */
+int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                       const float* dY, int64_t ldg, const float* weight, const float* mean_scale,
+                       const float* mean, const float* std_, float* dX, int64_t lddx,
+                       float* dw_part, float* dms_part, float* db_part, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

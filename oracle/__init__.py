@@ -12,3 +12,4 @@ from .sirconv_oracle import (  # noqa: F401
     ACTS, AGGS, act_fwd, act_bwd, csr_by_dst, csr_by_src, degree_norms,
     edge_agg_fwd, edge_agg_bwd, layer_fwd_bwd, max_first_wins, reference_cpu_step,
 )
+from .graphnorm_oracle import graph_norm_fwd, graph_norm_bwd  # noqa: F401

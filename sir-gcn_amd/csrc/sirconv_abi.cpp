@@ -278,4 +278,34 @@ int sir_segment_max_bwd(const int32_t* items, int64_t n_items, int64_t F, const 
     return finish(fn, sir::run_seg_max_bwd(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
 }
 
+// ------------------------------------------------------------------------------ GraphNorm
+int sir_graph_norm_fwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                       const float* weight, const float* bias, const float* mean_scale, float eps,
+                       float* Y, int64_t ldy, float* mean, float* std_, void* stream) {
+    const char* fn = "sir_graph_norm_fwd";
+    if (B < 0 || F <= 0 || F > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if (ldx < F || ldy < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if (B > 0 && (off == nullptr || X == nullptr || weight == nullptr || Y == nullptr || mean == nullptr ||
+                  std_ == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    return finish(fn, sir::run_graph_norm_fwd(off, B, (int)F, X, ldx, weight, bias, mean_scale, eps, Y, ldy,
+                                              mean, std_, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                       const float* dY, int64_t ldg, const float* weight, const float* mean_scale,
+                       const float* mean, const float* std_, float* dX, int64_t lddx,
+                       float* dw_part, float* dms_part, float* db_part, void* stream) {
+    const char* fn = "sir_graph_norm_bwd";
+    if (B < 0 || F <= 0 || F > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if (ldx < F || ldg < F || lddx < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if (B > 0 && (off == nullptr || X == nullptr || dY == nullptr || weight == nullptr || mean == nullptr ||
+                  std_ == nullptr || dX == nullptr || dw_part == nullptr || db_part == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (mean_scale != nullptr && dms_part == nullptr && B > 0) return fail(SIR_EINVAL, fn, "dms_part needed");
+    return finish(fn, sir::run_graph_norm_bwd(off, B, (int)F, X, ldx, dY, ldg, weight, mean_scale, mean, std_,
+                                              dX, lddx, dw_part, dms_part, db_part,
+                                              static_cast<hipStream_t>(stream)), nullptr);
+}
+
 }  // extern "C"

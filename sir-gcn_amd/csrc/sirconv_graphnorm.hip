@@ -1,0 +1,203 @@
+// sirconv_graphnorm.hip — fused GraphNorm (reference models/norm.py:7-29) for batched graphs.
+//
+// Nodes of graph b are rows [off[b], off[b+1]).  One wave per (graph, 64-lane column chunk); the
+// graph's rows are walked sequentially, so every per-graph sum is taken in node order — the
+// order of the reference's CPU scatter_add_ (norm.py:20,26) — and the forward reproduces it.
+//   forward : mean = sum x / n;  d = x - mean * ms;  std = sqrt(sum d^2 / n + eps);
+//             y = (w * d) / std + b                        (three passes over the graph's rows)
+//   backward: A = sum gy*d, G = sum gy;  gd = w*gy/std - w*d*A/(n*std^3);  Bs = sum gd;
+//             dx = gd - ms*Bs/n;  per-graph partials A/std, -mean*Bs, G for dw, dms, db
+//             (reduced over graphs by the host with the deterministic column sum).
+// The whole graph is re-read from L2 by each pass (molecule-sized graphs: a few KB).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sirconv_internal.h"
+
+namespace sir {
+namespace {
+
+template <int VW>
+__device__ __forceinline__ void gld(float (&d)[VW], const float* __restrict__ p) {
+    if constexpr (VW == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        d[0] = t.x; d[1] = t.y; d[2] = t.z; d[3] = t.w;
+    } else {
+        d[0] = p[0];
+    }
+}
+
+template <int VW>
+__device__ __forceinline__ void gst(float* __restrict__ p, const float (&s)[VW]) {
+    if constexpr (VW == 4) *reinterpret_cast<float4*>(p) = make_float4(s[0], s[1], s[2], s[3]);
+    else p[0] = s[0];
+}
+
+template <int VW>
+__global__ void __launch_bounds__(256)
+k_gn_fwd(const int64_t* __restrict__ off, int64_t B, int F, int n_cc,
+         const float* __restrict__ X, int64_t ldx, const float* __restrict__ w, const float* __restrict__ bias,
+         const float* __restrict__ ms, float eps, float* __restrict__ Y, int64_t ldy,
+         float* __restrict__ mean_out, float* __restrict__ std_out) {
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave >= B * n_cc) return;
+    const int64_t b = wave / n_cc;
+    const int cc = (int)(wave - b * n_cc);
+    const int c = cc * 64 + (threadIdx.x & 63);          // in units of VW floats
+    if (c * VW >= F) return;
+    const int64_t r0 = off[b], r1 = off[b + 1];
+    const float nf = (float)(r1 - r0);
+    float s[VW], q[VW], t[VW], wv[VW], bv[VW], mv[VW];
+#pragma unroll
+    for (int x = 0; x < VW; ++x) { s[x] = 0.f; q[x] = 0.f; }
+    for (int64_t i = r0; i < r1; ++i) {                   // norm.py:20 scatter_add_ (node order)
+        float v[VW];
+        gld<VW>(v, X + i * ldx + c * VW);
+#pragma unroll
+        for (int x = 0; x < VW; ++x) s[x] += v[x];
+    }
+    gld<VW>(wv, w + c * VW);
+    if (bias) gld<VW>(bv, bias + c * VW);
+    if (ms) gld<VW>(mv, ms + c * VW);
+#pragma unroll
+    for (int x = 0; x < VW; ++x) {
+        s[x] = (r1 > r0) ? s[x] / nf : 0.f;               // norm.py:21 mean
+        t[x] = ms ? s[x] * mv[x] : s[x];                  // norm.py:23 mean * mean_scale
+    }
+    for (int64_t i = r0; i < r1; ++i) {                   // norm.py:26 scatter_add_(demean^2)
+        float v[VW];
+        gld<VW>(v, X + i * ldx + c * VW);
+#pragma unroll
+        for (int x = 0; x < VW; ++x) {
+            const float d = v[x] - t[x];
+            q[x] += d * d;
+        }
+    }
+    float sd[VW];
+#pragma unroll
+    for (int x = 0; x < VW; ++x) sd[x] = (r1 > r0) ? sqrtf(q[x] / nf + eps) : 0.f;   // norm.py:27
+    for (int64_t i = r0; i < r1; ++i) {                   // norm.py:29
+        float v[VW];
+        gld<VW>(v, X + i * ldx + c * VW);
+#pragma unroll
+        for (int x = 0; x < VW; ++x) {
+            const float d = v[x] - t[x];
+            float y = wv[x] * d / sd[x];
+            if (bias) y = y + bv[x];
+            v[x] = y;
+        }
+        gst<VW>(Y + i * ldy + c * VW, v);
+    }
+    gst<VW>(mean_out + b * F + c * VW, s);
+    gst<VW>(std_out + b * F + c * VW, sd);
+}
+
+template <int VW>
+__global__ void __launch_bounds__(256)
+k_gn_bwd(const int64_t* __restrict__ off, int64_t B, int F, int n_cc,
+         const float* __restrict__ X, int64_t ldx, const float* __restrict__ dY, int64_t ldg,
+         const float* __restrict__ w, const float* __restrict__ ms, const float* __restrict__ mean,
+         const float* __restrict__ sdv, float* __restrict__ dX, int64_t lddx,
+         float* __restrict__ dw_part, float* __restrict__ dms_part, float* __restrict__ db_part) {
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave >= B * n_cc) return;
+    const int64_t b = wave / n_cc;
+    const int cc = (int)(wave - b * n_cc);
+    const int c = cc * 64 + (threadIdx.x & 63);
+    if (c * VW >= F) return;
+    const int64_t r0 = off[b], r1 = off[b + 1];
+    const float nf = (float)(r1 - r0);
+    float wv[VW], mv[VW], mu[VW], sd[VW], t[VW], A[VW], G[VW], Bs[VW];
+    gld<VW>(wv, w + c * VW);
+    if (ms) gld<VW>(mv, ms + c * VW);
+    else {
+#pragma unroll
+        for (int x = 0; x < VW; ++x) mv[x] = 1.f;
+    }
+    gld<VW>(mu, mean + b * F + c * VW);
+    gld<VW>(sd, sdv + b * F + c * VW);
+#pragma unroll
+    for (int x = 0; x < VW; ++x) { t[x] = ms ? mu[x] * mv[x] : mu[x]; A[x] = 0.f; G[x] = 0.f; Bs[x] = 0.f; }
+    for (int64_t i = r0; i < r1; ++i) {
+        float v[VW], g[VW];
+        gld<VW>(v, X + i * ldx + c * VW);
+        gld<VW>(g, dY + i * ldg + c * VW);
+#pragma unroll
+        for (int x = 0; x < VW; ++x) { A[x] += g[x] * (v[x] - t[x]); G[x] += g[x]; }
+    }
+    float k1[VW], k2[VW];
+#pragma unroll
+    for (int x = 0; x < VW; ++x) {
+        k1[x] = wv[x] / sd[x];                                       // w / s
+        k2[x] = wv[x] * A[x] / (nf * sd[x] * sd[x] * sd[x]);          // w A / (n s^3)
+    }
+    for (int64_t i = r0; i < r1; ++i) {
+        float v[VW], g[VW];
+        gld<VW>(v, X + i * ldx + c * VW);
+        gld<VW>(g, dY + i * ldg + c * VW);
+#pragma unroll
+        for (int x = 0; x < VW; ++x) Bs[x] += k1[x] * g[x] - k2[x] * (v[x] - t[x]);
+    }
+    for (int64_t i = r0; i < r1; ++i) {
+        float v[VW], g[VW];
+        gld<VW>(v, X + i * ldx + c * VW);
+        gld<VW>(g, dY + i * ldg + c * VW);
+#pragma unroll
+        for (int x = 0; x < VW; ++x) v[x] = (k1[x] * g[x] - k2[x] * (v[x] - t[x])) - mv[x] * Bs[x] / nf;
+        gst<VW>(dX + i * lddx + c * VW, v);
+    }
+    float pw[VW], pm[VW];
+#pragma unroll
+    for (int x = 0; x < VW; ++x) {
+        pw[x] = (r1 > r0) ? A[x] / sd[x] : 0.f;
+        pm[x] = -(mu[x] * Bs[x]);
+    }
+    gst<VW>(dw_part + b * F + c * VW, pw);
+    if (dms_part) gst<VW>(dms_part + b * F + c * VW, pm);
+    gst<VW>(db_part + b * F + c * VW, G);
+}
+
+bool al(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+hipError_t run_graph_norm_fwd(const int64_t* off, int64_t B, int F, const float* X, int64_t ldx,
+                              const float* w, const float* bias, const float* ms, float eps,
+                              float* Y, int64_t ldy, float* mean, float* sd, hipStream_t st) {
+    if (B == 0) return hipSuccess;
+    const bool v4 = F % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al(X) && al(Y) && al(w) && al(bias) &&
+                    al(ms) && al(mean) && al(sd);
+    const int vw = v4 ? 4 : 1;
+    const int n_cc = (F / vw + 63) / 64;
+    const int64_t waves = B * n_cc;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    if (v4)
+        hipLaunchKernelGGL((k_gn_fwd<4>), dim3(blocks), dim3(256), 0, st, off, B, F, n_cc, X, ldx, w, bias, ms,
+                           eps, Y, ldy, mean, sd);
+    else
+        hipLaunchKernelGGL((k_gn_fwd<1>), dim3(blocks), dim3(256), 0, st, off, B, F, n_cc, X, ldx, w, bias, ms,
+                           eps, Y, ldy, mean, sd);
+    return hipGetLastError();
+}
+
+hipError_t run_graph_norm_bwd(const int64_t* off, int64_t B, int F, const float* X, int64_t ldx,
+                              const float* dY, int64_t ldg, const float* w, const float* ms,
+                              const float* mean, const float* sd, float* dX, int64_t lddx,
+                              float* dw_part, float* dms_part, float* db_part, hipStream_t st) {
+    if (B == 0) return hipSuccess;
+    const bool v4 = F % 4 == 0 && ldx % 4 == 0 && ldg % 4 == 0 && lddx % 4 == 0 && al(X) && al(dY) && al(dX) &&
+                    al(w) && al(ms) && al(mean) && al(sd) && al(dw_part) && al(dms_part) && al(db_part);
+    const int vw = v4 ? 4 : 1;
+    const int n_cc = (F / vw + 63) / 64;
+    const int64_t waves = B * n_cc;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    if (v4)
+        hipLaunchKernelGGL((k_gn_bwd<4>), dim3(blocks), dim3(256), 0, st, off, B, F, n_cc, X, ldx, dY, ldg, w, ms,
+                           mean, sd, dX, lddx, dw_part, dms_part, db_part);
+    else
+        hipLaunchKernelGGL((k_gn_bwd<1>), dim3(blocks), dim3(256), 0, st, off, B, F, n_cc, X, ldx, dY, ldg, w, ms,
+                           mean, sd, dX, lddx, dw_part, dms_part, db_part);
+    return hipGetLastError();
+}
+
+}  // namespace sir

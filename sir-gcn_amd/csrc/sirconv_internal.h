@@ -64,6 +64,14 @@ hipError_t run_edge_bcast(const GenericArgs& a, hipStream_t st);
 hipError_t run_seg_max(const GenericArgs& a, hipStream_t st);
 hipError_t run_seg_max_bwd(const GenericArgs& a, hipStream_t st);
 
+hipError_t run_graph_norm_fwd(const int64_t* off, int64_t B, int F, const float* X, int64_t ldx,
+                              const float* w, const float* bias, const float* ms, float eps,
+                              float* Y, int64_t ldy, float* mean, float* sd, hipStream_t st);
+hipError_t run_graph_norm_bwd(const int64_t* off, int64_t B, int F, const float* X, int64_t ldx,
+                              const float* dY, int64_t ldg, const float* w, const float* ms,
+                              const float* mean, const float* sd, float* dX, int64_t lddx,
+                              float* dw_part, float* dms_part, float* db_part, hipStream_t st);
+
 hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
                             int64_t n, hipStream_t st);
 

@@ -4,7 +4,9 @@
     from sirgcn import SIRConv, Graph      # drop-in for `from models.conv import SIRConv`
 """
 from .conv import SIRConv, EdgeAggregate, activation_code  # noqa: F401
-from .graph import Graph, GraphPlan, RowCSR, get_plan, build_row_csr  # noqa: F401
+from .graph import Graph, GraphPlan, RowCSR, batch, get_plan, build_row_csr  # noqa: F401
+from .norm import GraphNorm  # noqa: F401
 from . import _native  # noqa: F401
 
-__all__ = ["SIRConv", "Graph", "GraphPlan", "RowCSR", "EdgeAggregate", "get_plan", "build_row_csr"]
+__all__ = ["SIRConv", "GraphNorm", "Graph", "GraphPlan", "RowCSR", "EdgeAggregate", "batch", "get_plan",
+           "build_row_csr"]

@@ -25,6 +25,9 @@ SIGNATURES = {
     "sir_mask_words": (ctypes.c_int64, [_I64, _I]),
     "sir_degree_norms": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P]),
     "sir_col_sum": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _P, _P]),
+    "sir_graph_norm_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _F, _P, _I64, _P, _P, _P]),
+    "sir_graph_norm_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I64,
+                                          _P, _P, _P, _P]),
     "sir_edge_gather_add": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P]),
     "sir_segment_sum": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64,
                                        _P, _P]),
@@ -225,4 +228,25 @@ def segment_max_bwd(csr, arg, dY, dM):
     with _Timed("sir_segment_max_bwd", dM.device):
         rc = lib.sir_segment_max_bwd(_ptr(csr.items), csr.n_items, F, _ptr(arg), _ld(arg, F),
                                      _ptr(dY), _ld(dY, F), _ptr(dM), _ld(dM, F), _stream(dM.device))
+    _check(rc, lib)
+
+
+# ------------------------------------------------------------------------------ GraphNorm
+def graph_norm_fwd(off, X, weight, bias, mean_scale, eps, Y, mean, std):
+    lib = load()
+    B, F = mean.shape
+    with _Timed("sir_graph_norm_fwd", Y.device):
+        rc = lib.sir_graph_norm_fwd(_ptr(off), B, F, _ptr(X), _ld(X, F), _ptr(weight), _ptr(bias),
+                                    _ptr(mean_scale), float(eps), _ptr(Y), _ld(Y, F), _ptr(mean), _ptr(std),
+                                    _stream(Y.device))
+    _check(rc, lib)
+
+
+def graph_norm_bwd(off, X, dY, weight, mean_scale, mean, std, dX, dw_part, dms_part, db_part):
+    lib = load()
+    B, F = mean.shape
+    with _Timed("sir_graph_norm_bwd", dX.device):
+        rc = lib.sir_graph_norm_bwd(_ptr(off), B, F, _ptr(X), _ld(X, F), _ptr(dY), _ld(dY, F), _ptr(weight),
+                                    _ptr(mean_scale), _ptr(mean), _ptr(std), _ptr(dX), _ld(dX, F),
+                                    _ptr(dw_part), _ptr(dms_part), _ptr(db_part), _stream(dX.device))
     _check(rc, lib)

@@ -30,7 +30,7 @@ class Graph:
     """Minimal homogeneous graph with the ``DGLGraph`` surface ``SIRConv`` needs
     (``conv.py:50-63``: ``local_scope``, ``in_degrees``, ``out_degrees``, ``num_nodes``, ``device``)."""
 
-    def __init__(self, src, dst, num_nodes=None):
+    def __init__(self, src, dst, num_nodes=None, batch_num_nodes=None):
         src = torch.as_tensor(src, dtype=torch.int64)
         dst = torch.as_tensor(dst, dtype=torch.int64)
         if src.shape != dst.shape or src.dim() != 1:
@@ -38,6 +38,11 @@ class Graph:
         if num_nodes is None:
             num_nodes = int(max(src.max().item(), dst.max().item()) + 1) if src.numel() else 0
         self._src, self._dst, self._n = src, dst.to(src.device), int(num_nodes)
+        if batch_num_nodes is None:
+            batch_num_nodes = [self._n]
+        self._bnn = torch.as_tensor(batch_num_nodes, dtype=torch.int64)
+        if int(self._bnn.sum()) != self._n:
+            raise ValueError("batch_num_nodes must sum to num_nodes")
         self.ndata, self.edata = {}, {}
         self._plans = {}
 
@@ -65,8 +70,15 @@ class Graph:
         return torch.bincount(self._src, minlength=self._n)
 
     def to(self, device):
-        g = Graph(self._src.to(device), self._dst.to(device), self._n)
-        return g
+        return Graph(self._src.to(device), self._dst.to(device), self._n, self._bnn)
+
+    # batched graphs (dgl.batch semantics; used by GraphNorm, models/norm.py:16-17)
+    def batch_num_nodes(self):
+        return self._bnn
+
+    @property
+    def batch_size(self):
+        return int(self._bnn.numel())
 
     @contextlib.contextmanager
     def local_scope(self):
@@ -78,6 +90,35 @@ class Graph:
 
     def __repr__(self):
         return f"Graph(num_nodes={self._n}, num_edges={self.num_edges()}, device={self.device})"
+
+
+def batch(graphs):
+    """``dgl.batch``: one graph whose node / edge ids are the inputs' concatenated with offsets."""
+    offs, src, dst, bnn = 0, [], [], []
+    for g in graphs:
+        s_, d_ = g.edges()
+        src.append(torch.as_tensor(s_, dtype=torch.int64) + offs)
+        dst.append(torch.as_tensor(d_, dtype=torch.int64) + offs)
+        n = int(g.num_nodes())
+        bnn.append(n)
+        offs += n
+    if not graphs:
+        return Graph(torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64), 0, [])
+    return Graph(torch.cat(src), torch.cat(dst), offs, bnn)
+
+
+def node_offsets(graph, device):
+    """int64 [B+1] node offsets of a batched graph (cached per device)."""
+    cache = getattr(graph, "_plans", None)
+    key = ("offsets", str(device))
+    if cache is not None and key in cache:
+        return cache[key]
+    bnn = torch.as_tensor(graph.batch_num_nodes(), dtype=torch.int64).to(device)
+    off = torch.zeros(bnn.numel() + 1, dtype=torch.int64, device=device)
+    torch.cumsum(bnn, 0, out=off[1:])
+    if cache is not None:
+        cache[key] = off
+    return off
 
 
 @dataclass

@@ -19,6 +19,9 @@ Restated DGL 2.1.0 behaviour:
     ``scatter_reduce('amax')`` whose backward splits ties -> max-tie gradients are
     parity-unpinned (documented in DESIGN.md).
   * ``expand_as_pair(x, g)`` returns ``(x, x)`` for a non-block graph.
+  * ``dgl.batch`` concatenates node/edge ids with offsets and records ``batch_num_nodes``;
+    ``dgl.broadcast_nodes(g, feat)`` repeats row b of ``feat`` for every node of graph b
+    (used by ``models/norm.py:17`` GraphNorm).
 
 This package is put on ``sys.path`` only by ``make_golden.py``; nothing on the product
 path, the GPU box or the test-suite imports it.
@@ -54,12 +57,22 @@ class EdgeBatch:
 
 
 class DGLGraph:
-    def __init__(self, src, dst, num_nodes):
+    def __init__(self, src, dst, num_nodes, batch_num_nodes=None):
         self._src = torch.as_tensor(src, dtype=torch.int64)
         self._dst = torch.as_tensor(dst, dtype=torch.int64)
         self._n = int(num_nodes)
+        self._bnn = (torch.tensor([self._n], dtype=torch.int64) if batch_num_nodes is None
+                     else torch.as_tensor(batch_num_nodes, dtype=torch.int64))
         self.ndata = _Frame()
         self.edata = _Frame()
+
+    # --- batching (dgl.batch semantics: node ids concatenated with offsets) -----------
+    def batch_num_nodes(self):
+        return self._bnn
+
+    @property
+    def batch_size(self):
+        return int(self._bnn.numel())
 
     # --- structure ---------------------------------------------------------------
     def num_nodes(self):
@@ -108,6 +121,21 @@ class DGLGraph:
         else:
             raise NotImplementedError(reduce_func.name)
         self.ndata[reduce_func.out_field] = out
+
+
+def batch(graphs):
+    offs, src, dst, bnn = 0, [], [], []
+    for g in graphs:
+        src.append(g._src + offs)
+        dst.append(g._dst + offs)
+        bnn.append(g._n)
+        offs += g._n
+    return DGLGraph(torch.cat(src), torch.cat(dst), offs, torch.tensor(bnn, dtype=torch.int64))
+
+
+def broadcast_nodes(graph, feat):
+    """dgl.broadcast_nodes: row b of ``feat`` repeated for every node of graph b."""
+    return torch.repeat_interleave(feat, graph.batch_num_nodes(), dim=0)
 
 
 def graph(data, num_nodes=None):

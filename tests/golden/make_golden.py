@@ -34,6 +34,53 @@ REF = "/root/reference"
 SHIM = os.path.join(HERE, "dgl_shim")
 
 
+def load_reference_module(name):
+    sys.dont_write_bytecode = True
+    if SHIM not in sys.path:
+        sys.path.insert(0, SHIM)
+    import dgl  # noqa: F401  (the shim)
+
+    path = os.path.join(REF, "models", name + ".py")
+    with open(path, "r") as f:
+        src = f.read()
+    mod = types.ModuleType("ref_models_" + name)
+    mod.__file__ = path
+    exec(compile(src, path, "exec"), mod.__dict__)
+    return mod
+
+
+def run_graphnorm_case(norm_mod, name, sizes, F, bias, mean_scale, seed):
+    """models/norm.py:7-29 GraphNorm on a dgl.batch of len(sizes) graphs (node features only)."""
+    import dgl
+    graphs = [dgl.graph((torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64)), num_nodes=n)
+              for n in sizes]
+    bg = dgl.batch(graphs)
+    torch.manual_seed(seed)
+    gn = norm_mod.GraphNorm(F, bias=bias, mean_scale=mean_scale)
+    with torch.no_grad():   # non-trivial affine parameters
+        gn.weight.copy_(torch.randn(F) * 0.5 + 1.0)
+        if bias:
+            gn.bias.copy_(torch.randn(F) * 0.1)
+        if mean_scale:
+            gn.mean_scale.copy_(torch.rand(F) + 0.25)
+    gen = torch.Generator().manual_seed(seed + 1)
+    X = (torch.randn(sum(sizes), F, generator=gen) * 2.0 + 0.5).requires_grad_(True)
+    dY = torch.randn(sum(sizes), F, generator=gen)
+    Y = gn(bg, X)
+    Y.backward(dY)
+    t = lambda x: x.detach().numpy()
+    out = {"batch_num_nodes": np.asarray(sizes, np.int64), "X": t(X), "dY": t(dY), "Y": t(Y), "dX": t(X.grad),
+           "weight": t(gn.weight), "dweight": t(gn.weight.grad)}
+    if bias:
+        out["bias"] = t(gn.bias); out["dbias"] = t(gn.bias.grad)
+    if mean_scale:
+        out["mean_scale"] = t(gn.mean_scale); out["dmean_scale"] = t(gn.mean_scale.grad)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    return {"name": name, "kind": "graphnorm", "sizes": list(map(int, sizes)), "F": F, "bias": bias,
+            "mean_scale": mean_scale, "seed": seed, "agg": "graphnorm", "act": "none", "dtype": "float32",
+            "keys": sorted(out.keys())}
+
+
 def load_reference_conv():
     sys.dont_write_bytecode = True
     sys.path.insert(0, SHIM)
@@ -229,6 +276,14 @@ def main():
     cases.append(run_case(conv_mod, "small_sym_tanh_f32", small, 16, 32, 8, "sym", "tanh", torch.float32, seed))
     seed += 1
     cases.append(run_case(conv_mod, "small_mean_seq_f32", small, 16, 64, 16, "mean", "seq", torch.float32, seed))
+    # GraphNorm (models/norm.py:7-29), SURVEY §8(f) row 2: batched small graphs incl. a 1-node graph
+    norm_mod = load_reference_module("norm")
+    rng = np.random.default_rng(5)
+    mol_sizes = [int(x) for x in rng.integers(5, 40, size=24)] + [1, 57]
+    cases.append(run_graphnorm_case(norm_mod, "graphnorm_mol_f300", mol_sizes, 300, True, True, 501))
+    cases.append(run_graphnorm_case(norm_mod, "graphnorm_mol_f64_nobias", mol_sizes[:10], 64, False, True, 502))
+    cases.append(run_graphnorm_case(norm_mod, "graphnorm_f256_noscale", [3, 700, 12], 256, True, False, 503))
+    cases.append(run_graphnorm_case(norm_mod, "graphnorm_f30_odd", [9, 4, 33], 30, True, True, 504))
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "reference": "briangodwinlim/SIR-GCN models/conv.py:7-67 (snapshot 2025-08-24), via DGL-2.1.0 semantics shim",

@@ -412,3 +412,36 @@ def test_segment_max_first_wins_on_ties():
     dM = torch.empty_like(M)
     _native.segment_max_bwd(plan.dst, arg, torch.ones(3, 2, device=DEV), dM)
     assert dM.cpu().tolist() == [[0.0, 1.0], [1.0, 0.0], [0.0, 0.0], [1.0, 1.0]]
+
+
+# ------------------------------------------------------------------ GraphNorm (models/norm.py:7-29)
+GN = [c for c in golden_manifest() if c.get("kind") == "graphnorm"]
+
+
+@pytest.mark.parametrize("case", GN, ids=[c["name"] for c in GN])
+def test_graph_norm_vs_reference_golden(case):
+    from sirgcn import GraphNorm, batch
+    z = load_case(case["name"])
+    sizes = z["batch_num_nodes"].tolist()
+    g = batch([Graph(torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64), n) for n in sizes])
+    gn = GraphNorm(case["F"], bias=case["bias"], mean_scale=case["mean_scale"]).to(DEV)
+    with torch.no_grad():
+        gn.weight.copy_(_t(z["weight"]))
+        if case["bias"]:
+            gn.bias.copy_(_t(z["bias"]))
+        if case["mean_scale"]:
+            gn.mean_scale.copy_(_t(z["mean_scale"]))
+    X = _t(z["X"]).requires_grad_(True)
+    Y = gn(g, X)
+    Y.backward(_t(z["dY"]))
+    torch.cuda.synchronize()
+    assert torch.equal(Y.detach().cpu(), torch.from_numpy(z["Y"])), "forward is not bit-exact"
+    f64 = lambda k: torch.from_numpy(z[k]).double() if k in z else None
+    _, mean, std = oracle.graph_norm_fwd(f64("X"), sizes, f64("weight"), f64("bias"), f64("mean_scale"))
+    dX, dw, db, dms = oracle.graph_norm_bwd(f64("X"), f64("dY"), sizes, f64("weight"), f64("mean_scale"), mean, std)
+    assert_parity(X.grad.cpu(), z["dX"], dX, 1e-5, "dX")
+    assert_parity(gn.weight.grad.cpu(), z["dweight"], dw, 1e-5, "dweight")
+    if case["bias"]:
+        assert_parity(gn.bias.grad.cpu(), z["dbias"], db, 1e-5, "dbias")
+    if case["mean_scale"]:
+        assert_parity(gn.mean_scale.grad.cpu(), z["dmean_scale"], dms, 1e-5, "dmean_scale")

@@ -123,3 +123,26 @@ def test_max_first_wins_semantics():
     Y, arg = oracle.max_first_wins(dst, 2, M)
     assert Y.tolist() == [[3.0, 5.0], [0.0, 0.0]]
     assert arg.tolist() == [[1, 0], [-1, -1]]           # ties -> earliest edge; empty row -> -1
+
+
+# ------------------------------------------------------------------ GraphNorm (models/norm.py:7-29)
+GN = [c for c in CASES if c.get("kind") == "graphnorm"]
+
+
+@pytest.mark.parametrize("case", GN, ids=[c["name"] for c in GN])
+def test_graph_norm_oracle_matches_reference(case):
+    z = load_case(case["name"])
+    f = lambda k: _t(z[k]) if k in z else None
+    Y, mean, std = oracle.graph_norm_fwd(f("X"), z["batch_num_nodes"], f("weight"), f("bias"), f("mean_scale"))
+    assert torch.equal(Y, f("Y")), case["name"]           # same op order as the reference: bit-exact
+    dX, dw, db, dms = oracle.graph_norm_bwd(f("X").double(), f("dY").double(), z["batch_num_nodes"],
+                                            f("weight").double(),
+                                            f("mean_scale").double() if "mean_scale" in z else None,
+                                            mean.double(), std.double())
+    assert_close(dX, z["dX"], 1e-5, "dX")
+    assert_close(dw, z["dweight"], 1e-5, "dweight")
+    if "dbias" in z:
+        assert_close(db, z["dbias"], 1e-5, "dbias")
+    if "dmean_scale" in z:   # a cancelling sum over graphs: the fp32 fixture is ~1e-6 off fp64 elementwise
+        from conftest import rel_err
+        assert rel_err(dms, z["dmean_scale"]) < 1e-5
