@@ -11,7 +11,7 @@ as DGL's cached CSC is.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--graph S2|S1|S1u|arxiv] [--agg sum]
   N > 1: launched by torch.distributed.run, one rank per GPU; dst-range edge-cut of the SAME
-  graph (strong scaling) with RCCL all-gather of K / reduce-scatter of dK (sirgcn.dist).
+  graph (strong scaling) with a sparse RCCL all-to-all of halo K rows fwd and its transpose for dK bwd (sirgcn.dist).
 
 Prints ONE JSON line (rank 0).  `roofline` is for the dominant edge kernel, timed live with
 HIP events on the launching stream; `cpu_baseline` is the reference CPU dataflow restated in
@@ -158,6 +158,7 @@ def main():
         dY = dY_full.to(dev)
         layer = lambda: conv(g, X)
         rows_local, edges_local = V, E
+        rows_src = V
     else:
         from sirgcn.dist import DistGraph, DistSIRConv
         dg = DistGraph.from_global(src, dst, V, rank, world, dev, chunk=args.chunk or DEFAULT_CHUNK)
@@ -167,6 +168,7 @@ def main():
         dY = dY_full[r0:r1].to(dev)
         layer = lambda: dconv(dg, X)
         rows_local, edges_local = r1 - r0, dg.num_local_edges
+        rows_src = dg.n_ext
     del X_full, dY_full
 
     def step():
@@ -202,7 +204,7 @@ def main():
     kernels = {}
     for name, evs in timing.items():
         t = sum(a.elapsed_time(b) for a, b in evs) / len(evs)    # ms per launch
-        bytes_ = edge_pass_bytes(name, rows_local if name != "sir_edge_agg_bwd_src" else V, edges_local, H,
+        bytes_ = edge_pass_bytes(name, rows_local if name != "sir_edge_agg_bwd_src" else rows_src, edges_local, H,
                                  args.agg, masked)
         kernels[name] = {"ms": round(t, 4), "launches": len(evs), "bytes": bytes_,
                          "GBps": round(bytes_ / (t * 1e-3) / 1e9, 1)}
@@ -229,8 +231,17 @@ def main():
            "config": {"workload": f"{args.graph}: Chung-Lu power-law V={V} E={E} alpha={alpha}; 1 SIRConv layer "
                                   f"d_in=H=d_out={H}, agg={args.agg}, LeakyReLU(0.2); fwd+bwd incl. projections",
                       "graph": args.graph, "V": V, "E": E, "hidden": H, "agg": args.agg,
-                      "parallelism": f"edge-cut dst-range x{world}" if world > 1 else "single GPU"},
+                      "parallelism": f"edge-cut dst-range x{world}, sparse halo all-to-all" if world > 1
+                      else "single GPU"},
            "roofline": roofline}
+    if dconv is not None:     # halo exchange volume per rank (rows of H fp32), max over ranks
+        ex = torch.tensor([dg.n_halo, int(dg.send_idx.numel()), edges_local], dtype=torch.float64,
+                          device=dev if args.dist_backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        out["exchange"] = {"halo_rows_max": int(ex[0]), "send_rows_max": int(ex[1]), "local_edges_max": int(ex[2]),
+                           "bytes_per_direction_max": int(ex[0]) * H * 4,
+                           "dense_allgather_rows": V - min(dg.bounds[i + 1] - dg.bounds[i] for i in range(world))}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, H)
     if rank == 0:

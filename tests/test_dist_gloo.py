@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, agg, outdir):
+def _worker(rank, world, port, agg, outdir, fused=True):
     for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -41,25 +41,29 @@ def _worker(rank, world, port, agg, outdir):
     conv = SIRConv(d, H, O, nn.LeakyReLU(0.2), 0, agg_type=agg)
     dg = DistGraph.from_global(src, dst, V, rank, world, "cpu", chunk=64)
     dconv = DistSIRConv(conv, backend=cpu_edge_backend)
+    dconv.use_fused = fused
     r0, r1 = dg.row_begin, dg.row_end
     Xl = X[r0:r1].clone().requires_grad_(True)
     Y = dconv(dg, Xl)
     Y.backward(dY[r0:r1])
     dconv.allreduce_grads()
     torch.save({"r0": r0, "r1": r1, "Y": Y.detach(), "dX": Xl.grad, "E_local": dg.num_local_edges,
-                "bounds": dg.bounds, "grads": {n: p.grad for n, p in conv.named_parameters()}},
+                "bounds": dg.bounds, "grads": {n: p.grad for n, p in conv.named_parameters()},
+                "halo": dg.halo_ids, "recv_splits": dg.recv_splits, "send_splits": dg.send_splits,
+                "send_idx": dg.send_idx, "out_deg": dg.out_deg()},
                os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,agg", [(2, "sum"), (2, "sym"), (3, "mean")])
-def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg):
+@pytest.mark.parametrize("world,agg,fused", [(2, "sum", True), (2, "sym", True), (3, "mean", True),
+                                             (4, "sym", True), (3, "sum", False), (2, "mean", False)])
+def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg, fused):
     import oracle
     from sirgcn.synth import powerlaw_edges
     from torch import nn
     from sirgcn import SIRConv
-    mp.spawn(_worker, args=(world, _free_port(), agg, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), agg, str(tmp_path), fused), nprocs=world, join=True)
     parts = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     V, E, d, H, O = 500, 6000, 16, 40, 12
     src, dst = powerlaw_edges(V, E, 0.8, seed=7)
@@ -75,6 +79,28 @@ def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg):
     assert all(parts[i]["r1"] == parts[i + 1]["r0"] for i in range(world - 1))
     assert sum(p["E_local"] for p in parts) == E
     assert max(p["E_local"] for p in parts) <= E / world + int(torch.bincount(dst, minlength=V).max())
+    # halo exchange plan: every rank's halo = its distinct remote sources, grouped by owner;
+    # what owner q sends to rank p is exactly p's halo slice owned by q, in the same order
+    for p, part in enumerate(parts):
+        r0, r1 = part["r0"], part["r1"]
+        sel = (dst >= r0) & (dst < r1)
+        s_ = src[sel]
+        want = torch.unique(s_[(s_ < r0) | (s_ >= r1)])
+        assert torch.equal(part["halo"], want)
+        off = 0
+        for q in range(world):
+            n = part["recv_splits"][q]
+            mine = part["halo"][off:off + n]
+            off += n
+            if n:
+                assert int(mine.min()) >= parts[q]["r0"] and int(mine.max()) < parts[q]["r1"]
+            so = sum(parts[q]["send_splits"][:p])
+            sent = parts[q]["send_idx"][so:so + parts[q]["send_splits"][p]] + parts[q]["r0"]
+            assert torch.equal(sent, mine)
+        # global out-degree of own + halo rows
+        gdeg = torch.bincount(src, minlength=V)
+        ext = torch.cat([torch.arange(r0, r1), part["halo"]])
+        assert torch.equal(part["out_deg"], gdeg[ext])
     Y = torch.cat([p["Y"] for p in parts])
     dX = torch.cat([p["dX"] for p in parts])
     assert_close(Y, ref["Y"], 1e-5, "Y")
@@ -98,3 +124,45 @@ def test_partition_rows_balances_edges():
         loads = [int(deg[b[i]:b[i + 1]].sum()) for i in range(world)]
         assert sum(loads) == E
         assert max(loads) <= E / world + int(deg.max())
+
+
+@pytest.mark.parametrize("world,agg", [(2, "sum"), (3, "sym"), (4, "mean")])
+def test_edge_cut_fused_function_threads(world, agg):
+    """DistSIRConvFunction driven by hand on one thread per rank (tests/thread_comm.py), the
+    same harness the -m gpu test uses on device tensors, here with the CPU edge backend."""
+    import cpu_edge_backend
+    import oracle
+    from torch import nn
+    from conftest import assert_parity
+    from sirgcn import SIRConv, _native
+    from sirgcn.dist import DistGraph, DistSIRConvFunction, partition_rows
+    from sirgcn.synth import powerlaw_edges
+    from thread_comm import FakeCtx, ThreadComm, run_ranks
+    V, E, H = 600, 9000, 24
+    src, dst = powerlaw_edges(V, E, 0.8, seed=6)
+    X = torch.randn(V, 16, generator=torch.Generator().manual_seed(1))
+    dY = torch.randn(V, 8, generator=torch.Generator().manual_seed(2))
+    torch.manual_seed(3)
+    conv = SIRConv(16, H, 8, nn.LeakyReLU(0.2), 0, agg_type=agg)
+    w = [p.detach() for p in (conv.linear_query.weight, conv.linear_query.bias, conv.linear_key.weight,
+                              conv.linear_relation.weight, conv.linear_relation.bias)]
+    comms = ThreadComm.make(world)
+    bounds = partition_rows(torch.bincount(dst, minlength=V), world)
+
+    def fn(r):
+        dg = DistGraph(src, dst, V, bounds, r, world, "cpu", chunk=64, group=comms[r])
+        ctx = FakeCtx((True,) * 6 + (False,) * 6)
+        Y = DistSIRConvFunction.forward(ctx, X[dg.row_begin:dg.row_end], *w, dg, agg, _native.ACT_LEAKY, 0.2,
+                                        cpu_edge_backend, True)
+        return dg.n_halo, Y, DistSIRConvFunction.backward(ctx, dY[dg.row_begin:dg.row_end])
+
+    outs = run_ranks(world, fn)
+    assert all(o[0] > 0 for o in outs)
+    Y = torch.cat([o[1] for o in outs])
+    dX = torch.cat([o[2][0] for o in outs])
+    t = oracle.layer_fwd_bwd(src, dst, V, X.double(), *[x.double() for x in w], dY.double(), agg, "leaky", 0.2)
+    r = oracle.reference_cpu_step(src, dst, V, X, *w, dY, agg, "leaky", 0.2)
+    assert_parity(Y, r["Y"], t["Y"], 1e-5, "Y")
+    assert_parity(dX, r["dX"], t["dX"], 1e-5, "dX")
+    for i, k in enumerate(("dW_Q", "db_Q", "dW_K", "dW_R", "db_R")):
+        assert_parity(sum(o[2][i + 1] for o in outs), r[k], t[k], 1e-5, k)

@@ -264,8 +264,8 @@ def test_sign_mask_backward_bit_identical_to_recompute(case):
 
 @pytest.mark.parametrize("agg", ["sum", "sym", "mean"])
 def test_edge_cut_path_single_rank_equals_single_gpu(agg):
-    """sirgcn.dist with world=1 (padded remap, all-gather/reduce-scatter degenerate) must give
-    the same bits as the single-GPU layer (collectives themselves: tests/test_dist_gloo.py)."""
+    """sirgcn.dist with world=1 (no halo, exchanges degenerate) against the single-GPU layer
+    (collectives: tests/test_dist_gloo.py and test_edge_cut_halo_exchange_on_device)."""
     from sirgcn.dist import DistGraph, DistSIRConv
     from sirgcn.synth import powerlaw_edges
     V, E, H = 3000, 60000, 256
@@ -293,6 +293,54 @@ def test_edge_cut_path_single_rank_equals_single_gpu(agg):
              "linear_relation.weight": "dW_R", "linear_relation.bias": "db_R"}
     for n, p in conv.named_parameters():
         assert_parity(p.grad.cpu(), g1[n].cpu(), truth[names[n]], 1e-5, n)
+
+
+@pytest.mark.parametrize("world,agg", [(2, "sum"), (3, "sym"), (2, "mean"), (4, "sum")])
+def test_edge_cut_halo_exchange_on_device(world, agg):
+    """Multi-rank edge-cut on the GPU in one process: one thread per rank, device tensors,
+    in-process all-to-all (tests/thread_comm.py).  Exercises the halo plan, the packed sends,
+    K_ext kernels, the reverse dK exchange and its deterministic add against the fp64 oracle."""
+    from sirgcn.dist import DistGraph, DistSIRConvFunction
+    from sirgcn.synth import powerlaw_edges
+    from thread_comm import FakeCtx, ThreadComm, run_ranks
+    V, E, H = 4000, 80000, 256
+    src, dst = powerlaw_edges(V, E, 0.8, seed=6)
+    X = torch.randn(V, H, generator=torch.Generator().manual_seed(1)).to(DEV)
+    dY = torch.randn(V, H, generator=torch.Generator().manual_seed(2)).to(DEV)
+    torch.manual_seed(3)
+    conv = SIRConv(H, H, H, nn.LeakyReLU(0.2), 0, agg_type=agg).to(DEV)
+    w = [conv.linear_query.weight.detach(), conv.linear_query.bias.detach(), conv.linear_key.weight.detach(),
+         conv.linear_relation.weight.detach(), conv.linear_relation.bias.detach()]
+    comms = ThreadComm.make(world)
+    in_deg = torch.bincount(dst, minlength=V)
+    from sirgcn.dist import partition_rows
+    bounds = partition_rows(in_deg, world)
+
+    def rank_fn(r):
+        dg = DistGraph(src, dst, V, bounds, r, world, DEV, group=comms[r])
+        ctx = FakeCtx((True,) * 6 + (False,) * 6)
+        x = X[dg.row_begin:dg.row_end]
+        with torch.no_grad():
+            Y = DistSIRConvFunction.forward(ctx, x, w[0], w[1], w[2], w[3], w[4], dg, agg, _native.ACT_LEAKY, 0.2,
+                                            _native, True)
+            grads = DistSIRConvFunction.backward(ctx, dY[dg.row_begin:dg.row_end])
+        torch.cuda.synchronize()
+        return dg.n_halo, Y, grads
+
+    outs = run_ranks(world, rank_fn)
+    assert sum(o[0] for o in outs) > 0                     # real halos were exchanged
+    Y = torch.cat([o[1] for o in outs]).cpu()
+    dX = torch.cat([o[2][0] for o in outs]).cpu()
+    gsum = [sum(o[2][i] for o in outs).cpu() for i in range(1, 6)]
+    x1 = X.clone().requires_grad_(True)
+    Y1 = conv(Graph(src, dst, V), x1)
+    Y1.backward(dY)
+    wd = [t.cpu().double() for t in w]
+    truth = oracle.layer_fwd_bwd(src, dst, V, X.cpu().double(), *wd, dY.cpu().double(), agg, "leaky", 0.2)
+    assert_parity(Y, Y1.detach().cpu(), truth["Y"], 1e-5, "Y")
+    assert_parity(dX, x1.grad.cpu(), truth["dX"], 1e-5, "dX")
+    for g, (name, p), key in zip(gsum, conv.named_parameters(), ("dW_Q", "db_Q", "dW_K", "dW_R", "db_R")):
+        assert_parity(g, p.grad.cpu(), truth[key], 1e-5, name)
 
 
 @pytest.mark.parametrize("n,m", [(0, 8), (1, 4), (1000, 256), (2_000_003, 256), (5000, 512), (777, 1028)])
