@@ -13,3 +13,4 @@ from .sirconv_oracle import (  # noqa: F401
     edge_agg_fwd, edge_agg_bwd, layer_fwd_bwd, max_first_wins, reference_cpu_step,
 )
 from .graphnorm_oracle import graph_norm_fwd, graph_norm_bwd  # noqa: F401
+from .sireconv_oracle import sire_reference_step  # noqa: F401

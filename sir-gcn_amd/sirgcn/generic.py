@@ -1,6 +1,7 @@
 """Edge-materialised SIRConv path: ``agg_type='max'`` and arbitrary ``activation`` callables.
 
-The reference runs every variant through DGL's edge-UDF path (``conv.py:43-47,63``): gather
+Sparse steps compute in fp32 (results are returned in the caller's dtype).  The reference
+runs every variant through DGL's edge-UDF path (``conv.py:43-47,63``): gather
 ``eq[v] + ek[u]`` per edge, apply the UDF (sigma, and for ``max`` also ``linear_relation``), then
 reduce.  The fused kernels (``conv.py`` here) cover elementwise sigma with sum/mean/sym.  For the
 rest this module keeps the UDF dataflow but runs every sparse step natively (``sir_edge_gather_add``,
@@ -26,12 +27,13 @@ class EdgeGatherAdd(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, QK, plan, H):
+        ctx.in_dtype = QK.dtype
         QK = QK.contiguous().float()
         E = plan.dst.col.numel()
         Z = torch.empty((E, H), device=QK.device, dtype=torch.float32)
         _native.edge_gather_add(plan.dst, QK[:, :H], QK[:, H:], Z)
         ctx.plan, ctx.H, ctx.V = plan, H, QK.shape[0]
-        return Z
+        return Z.to(ctx.in_dtype)
 
     @staticmethod
     def backward(ctx, dZ):
@@ -42,7 +44,7 @@ class EdgeGatherAdd(torch.autograd.Function):
         partial = _ws(n_slots, H, dZ.device)
         _native.segment_sum(plan.dst, dZ, dQK[:, :H], partial=partial)                   # dQ: index_add by dst
         _native.segment_sum(plan.src, dZ, dQK[:, H:], perm=plan.src.perm, partial=partial)  # dK: by src
-        return dQK, None, None
+        return dQK.to(ctx.in_dtype), None, None
 
 
 class EdgeSum(torch.autograd.Function):
@@ -50,6 +52,7 @@ class EdgeSum(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, M, plan, agg):
+        ctx.in_dtype = M.dtype
         M = M.contiguous().float()
         F = M.shape[1]
         in_norm, out_norm = plan.norms(agg)
@@ -57,7 +60,7 @@ class EdgeSum(torch.autograd.Function):
         _native.segment_sum(plan.dst, M, S, in_norm, out_norm, agg == "mean",
                             partial=_ws(plan.dst.n_slots, F, M.device))
         ctx.plan, ctx.agg, ctx.E = plan, agg, M.shape[0]
-        return S
+        return S.to(ctx.in_dtype)
 
     @staticmethod
     def backward(ctx, dS):
@@ -66,7 +69,7 @@ class EdgeSum(torch.autograd.Function):
         in_norm, out_norm = plan.norms(agg)
         dM = torch.empty((ctx.E, dS.shape[1]), device=dS.device, dtype=torch.float32)
         _native.edge_broadcast(plan.dst, dS, dM, in_norm, out_norm, agg == "mean")
-        return dM, None, None
+        return dM.to(ctx.in_dtype), None, None
 
 
 class EdgeMax(torch.autograd.Function):
@@ -74,6 +77,7 @@ class EdgeMax(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, M, plan):
+        ctx.in_dtype = M.dtype
         M = M.contiguous().float()
         F = M.shape[1]
         V = plan.dst.n_rows
@@ -83,7 +87,7 @@ class EdgeMax(torch.autograd.Function):
         _native.segment_max(plan.dst, M, Y, arg, _ws(n, F, M.device), _ws(n, F, M.device, torch.int32))
         ctx.save_for_backward(arg)
         ctx.plan, ctx.E = plan, M.shape[0]
-        return Y
+        return Y.to(ctx.in_dtype)
 
     @staticmethod
     def backward(ctx, dY):
@@ -91,7 +95,7 @@ class EdgeMax(torch.autograd.Function):
         dY = dY.contiguous().float()
         dM = torch.empty((ctx.E, dY.shape[1]), device=dY.device, dtype=torch.float32)
         _native.segment_max_bwd(ctx.plan.dst, arg, dY, dM)
-        return dM, None
+        return dM.to(ctx.in_dtype), None
 
 
 def generic_forward(conv, plan, feat_key, feat_query):

@@ -19,9 +19,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
 
 
-def golden_manifest():
+def golden_manifest(kind="sirconv"):
+    """Fixture cases of one kind: "sirconv" (conv.py SIRConv), "sire" (SIREConv),
+    "graphnorm" (norm.py GraphNorm); None = all."""
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
-        return json.load(f)["cases"]
+        cases = json.load(f)["cases"]
+    return [c for c in cases if kind is None or c.get("kind", "sirconv") == kind]
 
 
 def load_case(name):

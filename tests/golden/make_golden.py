@@ -230,6 +230,37 @@ def run_case(conv_mod, name, graph, d, H, O, agg, act_kind, dtype, seed):
     return meta
 
 
+def run_sire_case(conv_mod, name, graph, d, de, H, O, agg, act_kind, dtype, seed):
+    """models/conv.py:70-134 SIREConv: sigma((eq[v] + ek[u]) + e_uv) with e = linear_edge(efeat)."""
+    import dgl
+    V, src, dst = graph
+    g = dgl.graph((torch.from_numpy(src), torch.from_numpy(dst)), num_nodes=V)
+    act, _ = make_act(act_kind, H, seed)
+    torch.manual_seed(seed)
+    m = conv_mod.SIREConv(d, de, H, O, act, 0, agg_type=agg).to(dtype)
+    m.train()
+    gen = torch.Generator().manual_seed(seed + 1)
+    X = torch.randn(V, d, generator=gen, dtype=torch.float64).to(dtype).requires_grad_(True)
+    Ef = torch.randn(src.size, de, generator=gen, dtype=torch.float64).to(dtype).requires_grad_(True)
+    dY = torch.randn(V, O, generator=gen, dtype=torch.float64).to(dtype)
+    Y = m(g, X, Ef)
+    Y.backward(dY)
+    t = lambda x: x.detach().cpu().numpy()
+    out = {
+        "src": src, "dst": dst, "X": t(X), "efeat": t(Ef),
+        "W_Q": t(m.linear_query.weight), "b_Q": t(m.linear_query.bias), "W_K": t(m.linear_key.weight),
+        "W_E": t(m.linear_edge.weight), "W_R": t(m.linear_relation.weight), "b_R": t(m.linear_relation.bias),
+        "Y": t(Y), "dY": t(dY), "dX": t(X.grad), "defeat": t(Ef.grad),
+        "dW_Q": t(m.linear_query.weight.grad), "db_Q": t(m.linear_query.bias.grad),
+        "dW_K": t(m.linear_key.weight.grad), "dW_E": t(m.linear_edge.weight.grad),
+        "dW_R": t(m.linear_relation.weight.grad), "db_R": t(m.linear_relation.bias.grad),
+    }
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    return {"name": name, "kind": "sire", "V": int(V), "E": int(src.size), "d": d, "de": de, "H": H, "O": O,
+            "agg": agg, "act": act_kind, "slope": 0.2 if act_kind == "leaky" else 0.0,
+            "dtype": str(dtype).replace("torch.", ""), "seed": seed, "keys": sorted(out.keys())}
+
+
 def main():
     conv_mod = load_reference_conv()
     small = graph_small()
@@ -284,9 +315,35 @@ def main():
     cases.append(run_graphnorm_case(norm_mod, "graphnorm_mol_f64_nobias", mol_sizes[:10], 64, False, True, 502))
     cases.append(run_graphnorm_case(norm_mod, "graphnorm_f256_noscale", [3, 700, 12], 256, True, False, 503))
     cases.append(run_graphnorm_case(norm_mod, "graphnorm_f30_odd", [9, 4, 33], 30, True, True, 504))
+    # SIREConv (models/conv.py:70-134), SURVEY §8(f) row 4: the edge-feature term
+    seed = 700
+    for agg in ("sum", "mean", "sym"):
+        for act in ("relu", "leaky", "gelu"):
+            seed += 1
+            cases.append(run_sire_case(conv_mod, f"sire_small_{agg}_{act}_f32", small, 16, 6, 32, 8, agg, act,
+                                       torch.float32, seed))
+    for act in ("leaky", "gelu"):
+        seed += 1
+        cases.append(run_sire_case(conv_mod, f"sire_nodup_max_{act}_f32", nodup, 16, 6, 32, 8, "max", act,
+                                   torch.float32, seed))
+    seed += 1
+    cases.append(run_sire_case(conv_mod, "sire_wide_sum_leaky_h256_f32", wide, 64, 16, 256, 64, "sum", "leaky",
+                               torch.float32, seed))
+    seed += 1
+    cases.append(run_sire_case(conv_mod, "sire_long_sym_leaky_h256_f32", long_, 32, 8, 256, 32, "sym", "leaky",
+                               torch.float32, seed))
+    seed += 1
+    cases.append(run_sire_case(conv_mod, "sire_small_sum_leaky_f64", small, 16, 6, 32, 8, "sum", "leaky",
+                               torch.float64, seed))
+    seed += 1
+    cases.append(run_sire_case(conv_mod, "sire_empty_sum_relu_f32", empty, 16, 6, 32, 8, "sum", "relu",
+                               torch.float32, seed))
+    seed += 1
+    cases.append(run_sire_case(conv_mod, "sire_small_sum_tanh_f32", small, 16, 6, 32, 8, "sum", "tanh",
+                               torch.float32, seed))
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
-                   "reference": "briangodwinlim/SIR-GCN models/conv.py:7-67 (snapshot 2025-08-24), via DGL-2.1.0 semantics shim",
+                   "reference": "briangodwinlim/SIR-GCN models/conv.py:7-134, models/norm.py:7-29 (snapshot 2025-08-24), via DGL-2.1.0 semantics shim",
                    "torch": torch.__version__, "cases": cases}, f, indent=1)
     print(f"wrote {len(cases)} cases")
 

@@ -126,7 +126,7 @@ def test_max_first_wins_semantics():
 
 
 # ------------------------------------------------------------------ GraphNorm (models/norm.py:7-29)
-GN = [c for c in CASES if c.get("kind") == "graphnorm"]
+GN = golden_manifest("graphnorm")
 
 
 @pytest.mark.parametrize("case", GN, ids=[c["name"] for c in GN])
@@ -146,3 +146,18 @@ def test_graph_norm_oracle_matches_reference(case):
     if "dmean_scale" in z:   # a cancelling sum over graphs: the fp32 fixture is ~1e-6 off fp64 elementwise
         from conftest import rel_err
         assert rel_err(dms, z["dmean_scale"]) < 1e-5
+
+
+# ------------------------------------------------------------------ SIREConv (models/conv.py:70-134)
+SIRE = golden_manifest("sire")
+
+
+@pytest.mark.parametrize("case", SIRE, ids=[c["name"] for c in SIRE])
+def test_sire_oracle_matches_reference(case):
+    z = load_case(case["name"])
+    args = [_t(z[k]) for k in ("X", "efeat", "W_Q", "b_Q", "W_K", "W_E", "W_R", "b_R", "dY")]
+    act = _act_from_case(case, z)
+    ref = oracle.sire_reference_step(z["src"], z["dst"], case["V"], *args, case["agg"], act, case["slope"])
+    tol = 1e-12 if case["dtype"] == "float64" else 1e-5
+    for key in ("Y", "dX", "defeat", "dW_Q", "db_Q", "dW_K", "dW_E", "dW_R", "db_R"):
+        assert_close(ref[key], z[key], tol, f"{case['name']} {key}")
