@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 1
+#define SIR_ABI_VERSION 2
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -198,6 +198,32 @@ int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X,
                        const float* dY, int64_t ldg, const float* weight, const float* mean_scale,
                        const float* mean, const float* std_, float* dX, int64_t lddx,
                        float* dw_part, float* dms_part, float* db_part, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Device-side graph plan build.  Replaces DGL's lazily built in-edge CSC
+ * (the COO -> CSR counting sort DGL runs on the first update_all, conv.py:63) and this repo's
+ * work-plan construction, for batched graphs / DropEdge re-builds (models/utils.py:96-102).
+ *
+ * rows, cols: int64 [E] device (for the in-edge CSR: rows = dst, cols = src); ids are checked
+ * against [0, n_rows) / [0, n_cols) ON THE DEVICE: the count of bad ids lands in counts[4] and
+ * the caller must check it (the plan is garbage when it is non-zero).  Outputs (device):
+ *   rowptr int32 [n_rows+1]; col int32 [E]; eid int64 [E] (edge ids, ascending inside a row —
+ *   a stable sort, DGL's order); items int32 [n_rows + E/chunk][4] and splits int32
+ *   [min(n_rows, E/(chunk+1)) + 1][4] (capacities; the used counts are written to counts);
+ *   counts int64 [5] = {n_items, n_splits, n_slots, max_degree, n_bad_ids}.
+ * workspace: sir_csr_build_workspace(n_rows, E) bytes.  E < 2^31, 1 <= chunk.
+ * ------------------------------------------------------------------------------------------- */
+int64_t sir_csr_build_workspace(int64_t n_rows, int64_t E);
+
+int sir_csr_build(const int64_t* rows, const int64_t* cols, int64_t E, int64_t n_rows, int64_t n_cols,
+                  int64_t chunk, int32_t* rowptr, int32_t* col, int64_t* eid, int32_t* items, int32_t* splits,
+                  int64_t* counts, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* perm[j] = position in CSR A of the edge at position j of CSR B (eid_a, eid_b: the two CSRs'
+ * edge-id arrays over the same E edges).  pos_ws: int32 [E] scratch.  Used for the src-CSR ->
+ * dst-CSR map of the sign-mask backward. */
+int sir_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int32_t* pos_ws, int32_t* perm,
+                 void* stream);
 
 #ifdef __cplusplus
 }

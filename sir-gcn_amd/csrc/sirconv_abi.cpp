@@ -6,6 +6,7 @@
 // buffer.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <string>
 
 #include "sirconv.h"
@@ -306,6 +307,39 @@ int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X,
     return finish(fn, sir::run_graph_norm_bwd(off, B, (int)F, X, ldx, dY, ldg, weight, mean_scale, mean, std_,
                                               dX, lddx, dw_part, dms_part, db_part,
                                               static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int64_t sir_csr_build_workspace(int64_t n_rows, int64_t E) {
+    if (n_rows < 0 || E < 0 || E >= INT32_MAX || n_rows >= INT32_MAX) return -1;
+    return sir::csr_build_workspace(n_rows, E);
+}
+
+int sir_csr_build(const int64_t* rows, const int64_t* cols, int64_t E, int64_t n_rows, int64_t n_cols,
+                  int64_t chunk, int32_t* rowptr, int32_t* col, int64_t* eid, int32_t* items, int32_t* splits,
+                  int64_t* counts, void* workspace, int64_t workspace_bytes, void* stream) {
+    const char* fn = "sir_csr_build";
+    if (n_rows < 0 || E < 0 || n_cols < 0) return fail(SIR_EINVAL, fn, "negative size");
+    if (E >= INT32_MAX || n_rows >= INT32_MAX) return fail(SIR_EINVAL, fn, "int32 plan: E and n_rows must be < 2^31");
+    if (chunk < 1 || chunk > (1 << 24)) return fail(SIR_EINVAL, fn, "chunk must be in [1, 2^24]");
+    if (rowptr == nullptr || counts == nullptr) return fail(SIR_EINVAL, fn, "NULL rowptr/counts");
+    if (E > 0 && (rows == nullptr || cols == nullptr || col == nullptr || eid == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL edge buffer");
+    if (n_rows > 0 && (items == nullptr || splits == nullptr)) return fail(SIR_EINVAL, fn, "NULL items/splits");
+    const int64_t need = sir::csr_build_workspace(n_rows, E);
+    if (need < 0) return fail(SIR_ELAUNCH, fn, "workspace query failed");
+    if (workspace == nullptr || workspace_bytes < need) return fail(SIR_EINVAL, fn, "workspace too small");
+    return finish(fn, sir::run_csr_build(rows, cols, E, n_rows, n_cols, (int)chunk, rowptr, col, eid, items, splits,
+                                         counts, workspace, workspace_bytes, static_cast<hipStream_t>(stream)),
+                  "workspace too small");
+}
+
+int sir_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int32_t* pos_ws, int32_t* perm,
+                 void* stream) {
+    const char* fn = "sir_csr_perm";
+    if (E < 0 || E >= INT32_MAX) return fail(SIR_EINVAL, fn, "E must be in [0, 2^31)");
+    if (E > 0 && (eid_a == nullptr || eid_b == nullptr || pos_ws == nullptr || perm == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    return finish(fn, sir::run_csr_perm(eid_a, eid_b, E, pos_ws, perm, static_cast<hipStream_t>(stream)), nullptr);
 }
 
 }  // extern "C"

@@ -82,4 +82,11 @@ hipError_t run_edge(int mode, const EdgeArgs& a, int agg, int act,
                     const int32_t* splits, int64_t n_splits, float* out_final, int64_t ld_final,
                     bool mean_div, hipStream_t st, const char** why);
 
+int64_t csr_build_workspace(int64_t n_rows, int64_t E);
+hipError_t run_csr_build(const int64_t* rows, const int64_t* cols, int64_t E, int64_t n_rows, int64_t n_cols,
+                         int chunk, int* rowptr, int* col, int64_t* eid, int32_t* items, int32_t* splits,
+                         int64_t* counts, void* ws, int64_t ws_bytes, hipStream_t st);
+hipError_t run_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int* pos_ws, int* perm,
+                        hipStream_t st);
+
 }  // namespace sir

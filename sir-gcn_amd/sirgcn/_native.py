@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16 = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
 _P, _I64, _I, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
@@ -34,6 +34,9 @@ SIGNATURES = {
     "sir_edge_broadcast": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64, _P]),
     "sir_segment_max": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _P]),
     "sir_segment_max_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P]),
+    "sir_csr_build_workspace": (ctypes.c_int64, [_I64, _I64]),
+    "sir_csr_build": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "sir_csr_perm": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
@@ -229,6 +232,44 @@ def segment_max_bwd(csr, arg, dY, dM):
         rc = lib.sir_segment_max_bwd(_ptr(csr.items), csr.n_items, F, _ptr(arg), _ld(arg, F),
                                      _ptr(dY), _ld(dY, F), _ptr(dM), _ld(dM, F), _stream(dM.device))
     _check(rc, lib)
+
+
+# ------------------------------------------------------------------------------ plan build
+def csr_build(rows, cols, n_rows, n_cols, chunk):
+    """Device COO -> row CSR + work plan (async).  Returns (rowptr, col, eid, items_cap, splits_cap,
+    counts); ``counts`` = int64 [5] {n_items, n_splits, n_slots, max_degree, n_bad_ids} on the device."""
+    lib = load()
+    dev = rows.device
+    E = rows.numel()
+    rows = rows.to(torch.int64).contiguous()
+    cols = cols.to(torch.int64).contiguous()
+    ws_bytes = lib.sir_csr_build_workspace(n_rows, E)
+    if ws_bytes < 0:
+        raise RuntimeError("sir_csr_build_workspace failed (sizes out of range or no device)")
+    ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+    rowptr = torch.empty((n_rows + 1,), dtype=torch.int32, device=dev)
+    col = torch.empty((E,), dtype=torch.int32, device=dev)
+    eid = torch.empty((E,), dtype=torch.int64, device=dev)
+    items = torch.empty((n_rows + E // chunk + 1, 4), dtype=torch.int32, device=dev)
+    splits = torch.empty((min(n_rows, E // (chunk + 1)) + 1, 4), dtype=torch.int32, device=dev)
+    counts = torch.empty((5,), dtype=torch.int64, device=dev)
+    with _Timed("sir_csr_build", dev):
+        rc = lib.sir_csr_build(_ptr(rows), _ptr(cols), E, n_rows, n_cols, chunk, _ptr(rowptr), _ptr(col),
+                               _ptr(eid), _ptr(items), _ptr(splits), _ptr(counts), _ptr(ws), ws_bytes,
+                               _stream(dev))
+    _check(rc, lib)
+    return rowptr, col, eid, items, splits, counts
+
+
+def csr_perm(eid_a, eid_b):
+    """perm[j] = position in CSR A of the edge at position j of CSR B (int32, async)."""
+    lib = load()
+    E = eid_a.numel()
+    pos = torch.empty((E,), dtype=torch.int32, device=eid_a.device)
+    perm = torch.empty((E,), dtype=torch.int32, device=eid_a.device)
+    rc = lib.sir_csr_perm(_ptr(eid_a), _ptr(eid_b), E, _ptr(pos), _ptr(perm), _stream(eid_a.device))
+    _check(rc, lib)
+    return perm
 
 
 # ------------------------------------------------------------------------------ GraphNorm

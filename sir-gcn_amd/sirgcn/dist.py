@@ -32,7 +32,7 @@ import torch.distributed as dist
 
 from . import _native
 from .conv import _tn, activation_code
-from .graph import DEFAULT_CHUNK, build_row_csr
+from .graph import DEFAULT_CHUNK, build_plans_native, build_row_csr
 
 
 def _host_staged(group, t):
@@ -132,12 +132,15 @@ class DistGraph:
                 raise RuntimeError(f"rank {rank}: peers requested rows outside [0, {self.n_rows})")
         self._send_parts = list(torch.split(self.send_idx, self.send_splits))
         # ---- kernel plans over the K_ext layout ----
-        self.dst = build_row_csr(ldst, col, self.n_rows, chunk)
-        self.src = build_row_csr(col, ldst, self.n_ext, chunk)
-        E = self.num_local_edges
-        pos_in_dst = torch.empty(E, dtype=torch.int64, device=dev)
-        pos_in_dst[self.dst.eid] = torch.arange(E, device=dev)
-        self.src.perm = pos_in_dst[self.src.eid].to(torch.int32).contiguous()
+        if dev.type == "cuda":
+            self.dst, self.src = build_plans_native(col, ldst, self.n_rows, self.n_ext, chunk)
+        else:
+            self.dst = build_row_csr(ldst, col, self.n_rows, chunk)
+            self.src = build_row_csr(col, ldst, self.n_ext, chunk)
+            E = self.num_local_edges
+            pos_in_dst = torch.empty(E, dtype=torch.int64, device=dev)
+            pos_in_dst[self.dst.eid] = torch.arange(E, device=dev)
+            self.src.perm = pos_in_dst[self.src.eid].to(torch.int32).contiguous()
         self.in_deg = (self.dst.rowptr[1:] - self.dst.rowptr[:-1]).to(torch.int64)
         self.local_out_deg = (self.src.rowptr[1:] - self.src.rowptr[:-1]).to(torch.int64)
         self._out_deg = None

@@ -185,8 +185,36 @@ def plan_from_rowptr(rowptr, col, eid, n_rows, chunk=DEFAULT_CHUNK):
                   n_slots=n_slots, max_degree=int(deg.max().item()) if n_rows else 0)
 
 
+def build_plans_native(src, dst, n_dst_rows, n_src_rows, chunk=DEFAULT_CHUNK):
+    """Both row CSRs + plans + the src->dst position map on the device (``sir_csr_build``,
+    ``sir_csr_perm``) with ONE host synchronisation (the plan sizes).  Same result as
+    :func:`build_row_csr` bit for bit (stable order, same items/splits)."""
+    from . import _native
+    E = src.numel()
+    if E >= 2 ** 31 - 1:
+        raise ValueError("int32 edge indices: E must be < 2^31")
+    d = _native.csr_build(dst, src, n_dst_rows, n_src_rows, chunk)
+    s = _native.csr_build(src, dst, n_src_rows, n_dst_rows, chunk)
+    perm = _native.csr_perm(d[2], s[2])
+    counts = torch.stack([d[5], s[5]]).cpu().tolist()
+    if counts[0][4] or counts[1][4]:
+        raise ValueError(f"edge endpoint out of range: {counts[0][4]} bad edges "
+                         f"(dst must be in [0, {n_dst_rows}), src in [0, {n_src_rows}))")
+    csrs = []
+    for (rowptr, col, eid, items, splits, _), cnt, n in ((d, counts[0], n_dst_rows), (s, counts[1], n_src_rows)):
+        n_items, n_splits, n_slots, max_deg = cnt[:4]
+        csrs.append(RowCSR(n_rows=n, rowptr=rowptr, col=col, eid=eid, items=items[:n_items],
+                           splits=splits[:n_splits] if n_splits else None, n_items=n_items,
+                           n_splits=n_splits, n_slots=n_slots, max_degree=max_deg))
+    csrs[1].perm = perm
+    return csrs[0], csrs[1]
+
+
 class GraphPlan:
-    """Everything per (graph, device) that the SIRConv kernels need; built once and cached."""
+    """Everything per (graph, device) that the SIRConv kernels need; built once and cached.
+
+    On a GPU the plan is built by the native device builder (:func:`build_plans_native`); host
+    plans (CPU tests) use the torch restatement (:func:`build_row_csr`)."""
 
     def __init__(self, src, dst, num_nodes, device, chunk=DEFAULT_CHUNK, csc=None):
         self.num_nodes = int(num_nodes)
@@ -194,23 +222,26 @@ class GraphPlan:
         src = src.to(self.device, torch.int64)
         dst = dst.to(self.device, torch.int64)
         self.num_edges = int(src.numel())
-        if self.num_edges:
-            lo = int(torch.minimum(src.min(), dst.min()).item())
-            hi = int(torch.maximum(src.max(), dst.max()).item())
-            if lo < 0 or hi >= self.num_nodes:      # the kernels index node rows by these ids
-                raise ValueError(f"edge endpoint out of range [0, {self.num_nodes}): min {lo}, max {hi}")
-        if csc is not None:             # a DGL-provided in-edge CSC (indptr, indices, eids)
-            indptr, indices, eids = (t.to(self.device) for t in csc)
-            self.dst = plan_from_rowptr(indptr, indices.to(torch.int32), eids.to(torch.int64),
-                                        self.num_nodes, chunk)
+        if self.device.type == "cuda" and csc is None:
+            self.dst, self.src = build_plans_native(src, dst, self.num_nodes, self.num_nodes, chunk)
         else:
-            self.dst = build_row_csr(dst, src, self.num_nodes, chunk)
-        self.src = build_row_csr(src, dst, self.num_nodes, chunk)
-        # sign-mask backward: the mask is written in dst-CSR order; the src pass finds an
-        # edge's mask through its dst-CSR position
-        pos_in_dst = torch.empty(self.num_edges, dtype=torch.int64, device=self.device)
-        pos_in_dst[self.dst.eid] = torch.arange(self.num_edges, device=self.device)
-        self.src.perm = pos_in_dst[self.src.eid].to(torch.int32).contiguous()
+            if self.num_edges:
+                lo = int(torch.minimum(src.min(), dst.min()).item())
+                hi = int(torch.maximum(src.max(), dst.max()).item())
+                if lo < 0 or hi >= self.num_nodes:      # the kernels index node rows by these ids
+                    raise ValueError(f"edge endpoint out of range [0, {self.num_nodes}): min {lo}, max {hi}")
+            if csc is not None:             # a DGL-provided in-edge CSC (indptr, indices, eids)
+                indptr, indices, eids = (t.to(self.device) for t in csc)
+                self.dst = plan_from_rowptr(indptr, indices.to(torch.int32), eids.to(torch.int64),
+                                            self.num_nodes, chunk)
+            else:
+                self.dst = build_row_csr(dst, src, self.num_nodes, chunk)
+            self.src = build_row_csr(src, dst, self.num_nodes, chunk)
+            # sign-mask backward: the mask is written in dst-CSR order; the src pass finds an
+            # edge's mask through its dst-CSR position
+            pos_in_dst = torch.empty(self.num_edges, dtype=torch.int64, device=self.device)
+            pos_in_dst[self.dst.eid] = torch.arange(self.num_edges, device=self.device)
+            self.src.perm = pos_in_dst[self.src.eid].to(torch.int32).contiguous()
         self.in_deg = (self.dst.rowptr[1:] - self.dst.rowptr[:-1]).to(torch.int64)
         self.out_deg = (self.src.rowptr[1:] - self.src.rowptr[:-1]).to(torch.int64)
         self._norms = {}

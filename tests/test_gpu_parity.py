@@ -555,3 +555,91 @@ def test_graph_norm_vs_reference_golden(case):
         assert_parity(gn.bias.grad.cpu(), z["dbias"], db, 1e-5, "dbias")
     if case["mean_scale"]:
         assert_parity(gn.mean_scale.grad.cpu(), z["dmean_scale"], dms, 1e-5, "dmean_scale")
+
+
+# ------------------------------------------------------------------ device plan build (§8 f4)
+def _plan_graphs():
+    from sirgcn.synth import powerlaw_edges
+    out = []
+    for name in ("small_sum_leaky_f32", "long_sum_leaky_h256_f32", "empty_sum_leaky_f32"):
+        z = load_case(name)
+        out.append((name, torch.from_numpy(z["src"]), torch.from_numpy(z["dst"]), int(z["in_deg"].size)))
+    s, d = powerlaw_edges(20000, 400000, 0.8, seed=3)
+    out.append(("powerlaw_20k", s, d, 20000))
+    out.append(("no_edges_V5", torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64), 5))
+    return out
+
+
+@pytest.mark.parametrize("chunk", [4, 256])
+def test_native_plan_build_equals_reference_order(chunk):
+    """sir_csr_build / sir_csr_perm == the torch restatement == the oracle's stable CSR, bit for bit."""
+    from sirgcn.graph import build_plans_native, build_row_csr
+    for name, src, dst, V in _plan_graphs():
+        nd, ns = build_plans_native(src.to(DEV), dst.to(DEV), V, V, chunk)
+        td = build_row_csr(dst, src, V, chunk)
+        ts = build_row_csr(src, dst, V, chunk)
+        for a, b in ((nd, td), (ns, ts)):
+            assert (a.n_items, a.n_splits, a.n_slots, a.max_degree) == (b.n_items, b.n_splits, b.n_slots,
+                                                                        b.max_degree), name
+            for f in ("rowptr", "col", "eid", "items"):
+                assert torch.equal(getattr(a, f).cpu(), getattr(b, f).cpu()), (name, f)
+            assert (a.splits is None) == (b.splits is None), name
+            if a.splits is not None:
+                assert torch.equal(a.splits.cpu(), b.splits.cpu()), name
+        pos = torch.empty(src.numel(), dtype=torch.int64)
+        pos[td.eid] = torch.arange(src.numel())
+        assert torch.equal(ns.perm.cpu().long(), pos[ts.eid]), name
+        if src.numel():
+            rowptr, col, eid = oracle.csr_by_dst(src.numpy(), dst.numpy(), V)
+            assert np.array_equal(nd.rowptr.cpu().numpy(), rowptr) and np.array_equal(nd.eid.cpu().numpy(), eid)
+
+
+def test_native_plan_build_rejects_bad_ids():
+    from sirgcn.graph import build_plans_native
+    src = torch.tensor([0, 1, 7], device=DEV)
+    dst = torch.tensor([1, 2, 0], device=DEV)
+    with pytest.raises(ValueError, match="out of range"):
+        build_plans_native(src, dst, 3, 3)
+    with pytest.raises(ValueError, match="out of range"):
+        build_plans_native(torch.tensor([0], device=DEV), torch.tensor([-1], device=DEV), 3, 3)
+    with pytest.raises(ValueError, match="out of range"):
+        GraphPlan(torch.tensor([0, 5]), torch.tensor([1, 1]), 3, DEV)
+
+
+def test_native_plan_build_batched_molecules_speed():
+    """Batched small graphs (ZINC-shaped, SURVEY cfg2): the device builder must agree with the
+    torch restatement and not be slower than it (printed for the record)."""
+    import time
+    from sirgcn.graph import batch, build_plans_native, build_row_csr
+    gen = torch.Generator().manual_seed(0)
+    gs = []
+    for _ in range(128):
+        n = int(torch.randint(10, 38, (1,), generator=gen))
+        m = int(n * 2.15)
+        gs.append(Graph(torch.randint(0, n, (m,), generator=gen), torch.randint(0, n, (m,), generator=gen), n))
+    bg = batch(gs)
+    src, dst = (t.to(DEV) for t in bg.edges())
+    V = bg.num_nodes()
+
+    def torch_plans():
+        d = build_row_csr(dst, src, V)
+        s_ = build_row_csr(src, dst, V)
+        pos = torch.empty(src.numel(), dtype=torch.int64, device=DEV)
+        pos[d.eid] = torch.arange(src.numel(), device=DEV)
+        return d, s_, pos[s_.eid].to(torch.int32)
+
+    ts = {}
+    for name, f in (("torch", torch_plans), ("native", lambda: build_plans_native(src, dst, V, V))):
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            f()
+        torch.cuda.synchronize()
+        ts[name] = (time.perf_counter() - t0) / 20 * 1e3
+    print(f"plan build, {V} nodes / {src.numel()} edges: torch {ts['torch']:.3f} ms, native {ts['native']:.3f} ms")
+    nd, ns = build_plans_native(src, dst, V, V)
+    td, tsr, tperm = torch_plans()
+    assert torch.equal(nd.items, td.items) and torch.equal(ns.perm, tperm)
+    assert ts["native"] <= ts["torch"] * 1.5
