@@ -35,6 +35,7 @@ from torch import nn  # noqa: E402
 METRIC = "edges/sec SIRConv fwd+bwd, d_hidden=256, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 FP32_PEAK_TFLOPS = 157.3    # fp32 MFMA = vector peak (no xf32 on gfx950)
+FP16_PEAK_FLOPS = 2.5e15    # dense fp16/bf16 MFMA (MI355X_MICROARCH.md; the 5 PF figure is 2:1 sparse)
 
 
 def parse():
@@ -52,6 +53,8 @@ def parse():
                     help="nccl (= RCCL) for real runs; gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the edge-cut (sirgcn.dist) code path even at world size 1")
+    ap.add_argument("--torch-gemm", action="store_true",
+                    help="A/B only: projections on torch fp32 GEMMs instead of the native MFMA kernels")
     ap.add_argument("--pmc-file", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default profiles/pmc_traffic_<graph>.json")
     return ap.parse_args()
@@ -135,7 +138,9 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    from sirgcn import SIRConv, _native
+    from sirgcn import SIRConv, _native, linalg
+    if args.torch_gemm:
+        linalg.USE_NATIVE = False
     from sirgcn.graph import DEFAULT_CHUNK
     from sirgcn.synth import NAMED, powerlaw_edges
     H = args.hidden
@@ -201,9 +206,16 @@ def main():
 
     from sirgcn.conv import EdgeAggregate
     masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY))
-    kernels = {}
+    kernels, gemm = {}, {}
     for name, evs in timing.items():
-        t = sum(a.elapsed_time(b) for a, b in evs) / len(evs)    # ms per launch
+        t = sum(a.elapsed_time(b) for a, b, _ in evs) / len(evs)    # ms per launch
+        if name.startswith("sir_gemm_"):       # MFMA-bound projections: flops per launch
+            if name == "sir_gemm_pack":
+                continue
+            fl = sum(w for _, _, w in evs) / len(evs)
+            gemm[name] = {"ms": round(t, 4), "launches": len(evs), "flops": fl,
+                          "TFLOPs": round(fl / (t * 1e-3) / 1e12, 1)}
+            continue
         bytes_ = edge_pass_bytes(name, rows_local if name != "sir_edge_agg_bwd_src" else rows_src, edges_local, H,
                                  args.agg, masked)
         kernels[name] = {"ms": round(t, 4), "launches": len(evs), "bytes": bytes_,
@@ -234,6 +246,14 @@ def main():
                       "parallelism": f"edge-cut dst-range x{world}, sparse halo all-to-all" if world > 1
                       else "single GPU"},
            "roofline": roofline}
+    if gemm:   # projections (split-fp16 MFMA): fp32-equivalent flops; raw fp16 MFMA work is 3x that
+        fl = sum(g["flops"] * g["launches"] for g in gemm.values()) / args.steps
+        tg = sum(g["ms"] * g["launches"] for g in gemm.values()) / args.steps
+        out["projections"] = {"bound": "mfma", "ms_per_step": round(tg, 3), "flops_per_step": fl,
+                              "achieved_fp32_equiv_TFLOPs": round(fl / (tg * 1e-3) / 1e12, 1),
+                              "fp16_mfma_util": round(3 * fl / (tg * 1e-3) / FP16_PEAK_FLOPS, 4),
+                              "vs_fp32_peak": round(fl / (tg * 1e-3) / (FP32_PEAK_TFLOPS * 1e12), 3),
+                              "kernels": gemm}
     if dconv is not None:     # halo exchange volume per rank (rows of H fp32), max over ranks
         ex = torch.tensor([dg.n_halo, int(dg.send_idx.numel()), edges_local], dtype=torch.float64,
                           device=dev if args.dist_backend == "nccl" else "cpu")

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 2
+#define SIR_ABI_VERSION 3
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -224,6 +224,34 @@ int sir_csr_build(const int64_t* rows, const int64_t* cols, int64_t E, int64_t n
  * dst-CSR map of the sign-mask backward. */
 int sir_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int32_t* pos_ws, int32_t* perm,
                  void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Projection GEMMs of the layer: the nn.Linear calls conv.py:60-61 (Q, K), conv.py:65 (W_R) and
+ * their autograd (G = dY W_R, dX, dW_R, dW_Q, dW_K).  fp32 in / fp32 out, computed on fp16 MFMA
+ * with every operand split into two fp16 terms under a power-of-two scale per contraction row
+ * (hi*hi + hi*lo + lo*hi, fp32 accumulation): the accuracy of an fp32 GEMM (tests hold it to
+ * <= 2x torch fp32's error against fp64).  Not bit-identical to any fp32 BLAS (neither is one
+ * BLAS to another).  Elements more than 2^29 below their row's maximum lose relative precision
+ * (absolute error <= 2^-40 of that maximum).
+ * ------------------------------------------------------------------------------------------- */
+
+/* Weight operand B [N, K] for sir_gemm_nt: B[n][k] = W[n*ldw + k] (trans = 0, an nn.Linear
+ * weight used as x W^T) or W[k*ldw + n] (trans = 1, x W).  packed: sir_gemm_pack_bytes(N, K)
+ * bytes, 16-B aligned; re-pack whenever W changes. */
+int64_t sir_gemm_pack_bytes(int64_t N, int64_t K);
+int sir_gemm_pack(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, void* packed, void* stream);
+
+/* C[M, N] = A[M, K] B^T + bias  (bias [N] or NULL).  A, C row-major; K, N, lda, ldc multiples of
+ * 4; A, C, bias 16-B aligned.  Replaces addmm(b, X, W^T) / mm(X, W). */
+int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
+                const float* bias, float* C, int64_t ldc, void* stream);
+
+/* C[M, N] = A^T B with A [R, M] (lda), B [R, N] (ldb): the weight gradients (contraction over the
+ * R node rows, split over row ranges; the partial products are added in a fixed order, so the
+ * result is run-to-run deterministic).  workspace: sir_gemm_tn_workspace(R, M, N) bytes. */
+int64_t sir_gemm_tn_workspace(int64_t R, int64_t M, int64_t N);
+int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int64_t M, int64_t N,
+                float* C, int64_t ldc, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

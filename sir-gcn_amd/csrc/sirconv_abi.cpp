@@ -342,4 +342,52 @@ int sir_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int32_t*
     return finish(fn, sir::run_csr_perm(eid_a, eid_b, E, pos_ws, perm, static_cast<hipStream_t>(stream)), nullptr);
 }
 
+int64_t sir_gemm_pack_bytes(int64_t N, int64_t K) {
+    if (N <= 0 || K <= 0 || N > 65536 || K > 65536) return 0;
+    return sir::gemm_pack_bytes(N, K);
+}
+
+int sir_gemm_pack(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, void* packed, void* stream) {
+    const char* fn = "sir_gemm_pack";
+    if (N <= 0 || K <= 0 || N > 65536 || K > 65536) return fail(SIR_EINVAL, fn, "N and K must be in [1, 65536]");
+    if (W == nullptr || packed == nullptr) return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (ldw < (trans ? N : K)) return fail(SIR_EINVAL, fn, "ldw too small");
+    if ((reinterpret_cast<uintptr_t>(packed) & 15u) != 0) return fail(SIR_EINVAL, fn, "packed must be 16-B aligned");
+    hipError_t err = sir::run_gemm_pack(W, ldw, (int)N, (int)K, trans ? 1 : 0, packed, static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
+int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
+                const float* bias, float* C, int64_t ldc, void* stream) {
+    const char* fn = "sir_gemm_nt";
+    if (M < 0 || N <= 0 || K <= 0 || N > 65536 || K > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if ((M + 255) / 256 * ((N + 127) / 128) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
+    if (K % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldc % 4 != 0 || lda < K || ldc < N)
+        return fail(SIR_EINVAL, fn, "K, N, lda, ldc must be multiples of 4 (lda >= K, ldc >= N)");
+    if (M > 0 && (A == nullptr || C == nullptr || packed == nullptr)) return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(bias) |
+          reinterpret_cast<uintptr_t>(packed)) & 15u) != 0)
+        return fail(SIR_EINVAL, fn, "A, C, bias and packed must be 16-B aligned");
+    hipError_t err = sir::run_gemm_nt(A, lda, M, (int)K, packed, (int)N, bias, C, ldc, static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
+int64_t sir_gemm_tn_workspace(int64_t R, int64_t M, int64_t N) {
+    if (R < 0 || M <= 0 || N <= 0 || M > 65536 || N > 65536) return 0;
+    return sir::gemm_tn_workspace(R, M, N);
+}
+
+int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int64_t M, int64_t N,
+                float* C, int64_t ldc, void* workspace, int64_t workspace_bytes, void* stream) {
+    const char* fn = "sir_gemm_tn";
+    if (R < 0 || M <= 0 || N <= 0 || M > 65536 || N > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if (lda < M || ldb < N || ldc < N) return fail(SIR_EINVAL, fn, "leading dimension too small");
+    if (C == nullptr || workspace == nullptr || (R > 0 && (A == nullptr || B == nullptr)))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (workspace_bytes < sir::gemm_tn_workspace(R, M, N)) return fail(SIR_EINVAL, fn, "workspace too small");
+    hipError_t err = sir::run_gemm_tn(A, lda, B, ldb, R, (int)M, (int)N, C, ldc, workspace,
+                                      static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
 }  // extern "C"

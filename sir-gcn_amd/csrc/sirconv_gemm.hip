@@ -1,0 +1,527 @@
+// sirconv_gemm.hip — the layer's projection GEMMs (conv.py:60-61,65 and their autograd) on
+// gfx950 fp16 MFMA with a two-term operand split: fp32 accuracy at ~16x the f32-MFMA rate.
+//
+// Numerics.  Every operand element x is represented as (hi + lo) / s with hi = fp16(x*s),
+// lo = fp16(x*s - hi) and s a power of two chosen per operand row (the contraction runs along
+// the row), so that |x*s| < 2^15.  The product x*w is then hi*hi' + hi*lo' + lo*hi' (the lo*lo'
+// term, < 2^-22 relative, is dropped), each fp16 x fp16 product exact in the fp32 MFMA
+// accumulator: three v_mfma_f32_32x32x16_f16 per 32x32x16 step and ~22 significant bits per
+// operand — an error comparable to an fp32 GEMM's own rounding (tests/test_gemm_gpu.py holds
+// it to <= 2x torch fp32's error against fp64).  The scale of a data row is not known before
+// its last k-chunk has been read, so it is a RUNNING maximum: when a chunk raises a row's
+// maximum into a higher binade, the accumulators of that row are multiplied by the (exact,
+// power of two) ratio of the new and old scales before the chunk is added.
+//
+// Kernels
+//   k_pack_weight : B[n][k] (= W or W^T) -> fp16 hi/lo in MFMA fragment order + 1/scale per n
+//   k_gemm_nt     : C[M,N] = A[M,K] B[N,K]^T + bias   (QK = X [W_Q;W_K]^T, Y = S W_R^T,
+//                   G = dY W_R, dX = [dQ dK][W_Q;W_K]).  MFMA rows = features (packed B),
+//                   MFMA columns = data rows, so a lane's accumulator column IS the data row
+//                   whose running scale it needs.  A streamed once per feature tile (the
+//                   feature tiles of one data tile run back to back on one XCD: L2 reuse).
+//   k_gemm_tn     : part[p] = A[rows_p]^T B[rows_p]  (the weight gradients dW_R = dY^T S,
+//                   [dW_Q; dW_K] = [dQ dK]^T X; contraction over the V node rows, split over
+//                   P row ranges), running scales per column of A and of B.
+//   k_gemm_reduce : C = sum_p part[p] in p order (deterministic).
+// LDS stage image (both kernels): [part hi/lo][k-step 0/1][row][16 halves] — one k-step of 32
+// rows is 1 KiB contiguous, exactly one ds_read_b128 per lane (conflict-free).
+#include "sirconv_internal.h"
+
+namespace sir {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+constexpr int KC = 32;          // contraction elements per LDS stage (two k16 MFMA steps)
+
+// Smallest e with |m| < 2^e for normal m (e = -126 for 0 and subnormals, 129 for inf/nan).
+__device__ inline int bexp(float m) { return (int)((__float_as_uint(m) >> 23) & 255u) - 126; }
+// scale exponent for a running binade e: |x| * 2^(15 - e) < 2^15, clamped to a normal float
+__device__ inline int scale_exp(int e) { int s = 15 - e; return s > 126 ? 126 : s; }
+__device__ inline float pow2(int e) { e = e < -126 ? -126 : (e > 127 ? 127 : e); return __uint_as_float((uint32_t)(e + 127) << 23); }
+
+// hi/lo fp16 split of 8 floats scaled by s (exact power of two)
+#define SIR_SPLIT1(x, i) { const float y_ = (x) * s; const _Float16 h_ = (_Float16)y_; hi[i] = h_; lo[i] = (_Float16)(y_ - (float)h_); }
+__device__ inline void split8(float4 a, float4 b, float s, h8& hi, h8& lo) {
+    SIR_SPLIT1(a.x, 0) SIR_SPLIT1(a.y, 1) SIR_SPLIT1(a.z, 2) SIR_SPLIT1(a.w, 3)
+    SIR_SPLIT1(b.x, 4) SIR_SPLIT1(b.y, 5) SIR_SPLIT1(b.z, 6) SIR_SPLIT1(b.w, 7)
+}
+#undef SIR_SPLIT1
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// raw buffer resource over [p, p + bytes): out-of-range loads return 0 (gfx9 word3 0x00020000)
+__device__ inline rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+__device__ inline float fmax4(float m, float4 v) {
+    return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+
+// Bijective XCD-aware remap: consecutive wgids land on the same XCD (blocks are dispatched
+// round-robin over the 8 XCDs).
+__device__ inline int xcd_remap(int bid, int nblk) {
+    const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// ------------------------------------------------------------------------------------------
+// weight packing: one block of 64 threads per feature n (Npad blocks)
+// out layout: halves [Kc][2 part][2 ks][Npad][16], then float inv_scale[Npad]
+__global__ void __launch_bounds__(64)
+k_pack_weight(const float* __restrict__ W, int64_t ldw, int N, int K, int trans, int Npad, int Kc,
+              _Float16* __restrict__ out, float* __restrict__ inv_scale) {
+    const int n = blockIdx.x, l = threadIdx.x;
+    float m = 0.f;
+    if (n < N)
+        for (int k = l; k < K; k += 64) m = fmaxf(m, fabsf(trans ? W[(int64_t)k * ldw + n] : W[(int64_t)n * ldw + k]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const int se = scale_exp(bexp(m));
+    const float s = pow2(se);
+    for (int k = l; k < Kc * KC; k += 64) {
+        float x = 0.f;
+        if (n < N && k < K) x = trans ? W[(int64_t)k * ldw + n] : W[(int64_t)n * ldw + k];
+        const float y = x * s;
+        const _Float16 h = (_Float16)y;
+        const int kc = k / KC, ks = (k / 16) & 1, j = k & 15;
+        out[((((int64_t)kc * 2 + 0) * 2 + ks) * Npad + n) * 16 + j] = h;
+        out[((((int64_t)kc * 2 + 1) * 2 + ks) * Npad + n) * 16 + j] = (_Float16)(y - (float)h);
+    }
+    if (l == 0) inv_scale[n] = (n < N) ? pow2(-se) : 0.f;
+}
+
+// ------------------------------------------------------------------------------------------
+// NT GEMM.  WD x WF waves, each TDT x TFT tiles of 32 data rows x 32 features.
+template <int WD, int WF, int TDT, int TFT>
+__global__ void __launch_bounds__(64 * WD * WF)
+k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
+          const u4v* __restrict__ Wp, int Npad, const float* __restrict__ inv_t,
+          const float* __restrict__ bias, int N, float* __restrict__ C, int64_t ldc, int n_ftiles) {
+    constexpr int NT = 64 * WD * WF;
+    constexpr int BD = 32 * TDT * WD;        // data rows per block
+    constexpr int BF = 32 * TFT * WF;        // features per block
+    constexpr int TPR = NT / BD;             // loader threads per data row
+    static_assert(TPR == 1 || TPR == 2 || TPR == 4, "loader mapping");
+    constexpr int FPT = KC / TPR;            // floats per loader thread per stage
+    constexpr int WPT = BF * 8 / NT;         // 16-B weight pieces per thread per stage
+    static_assert(WPT >= 1 && BF * 8 % NT == 0, "weight loader mapping");
+    constexpr int D_BYTES = BD * 128, W_BYTES = BF * 128;
+    constexpr int STAGE = D_BYTES + W_BYTES + BD * 4;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+    const int t = threadIdx.x;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t d0 = (int64_t)(wg / n_ftiles) * BD;
+    const int f0 = (wg % n_ftiles) * BF;
+    const int nc = (K + KC - 1) / KC;
+
+    // loader role: buffer loads off wave-uniform bases (rows past M read as 0 by the range check)
+    const int rho = t / TPR, kp = t % TPR;
+    const int64_t rows_here = (M - d0 < BD) ? M - d0 : BD;
+    const rsrc_t arsrc = mk_rsrc(A + d0 * lda, (uint32_t)(rows_here * lda * 4));
+    const int aoff = (rho * (int)lda + kp * FPT) * 4;
+    const rsrc_t wrsrc = mk_rsrc(Wp, (uint32_t)((int64_t)nc * Npad * 128));
+    int woff[WPT];
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+        const int p = t + i * NT;
+        const int part = p / (BF * 4), ks = (p / (BF * 2)) & 1, nl = (p >> 1) % BF, q = p & 1;
+        woff[i] = (((part * 2 + ks) * Npad + f0 + nl) * 2 + q) * 16;
+    }
+    int e_run = -126;                       // running binade of this data row
+
+    // compute role
+    const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    const int d_w = (w / WF) * TDT * 32, f_w = (w % WF) * TFT * 32;
+
+    float4 dv[FPT / 4];
+    u4v wv[WPT];
+
+    auto load = [&](int c) {
+#pragma unroll
+        for (int i = 0; i < FPT / 4; ++i) {
+            const int k = c * KC + kp * FPT + 4 * i;
+            const u4v u = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff + 16 * i, c * KC * 4, 0);
+            dv[i] = (k < K) ? make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                                          __uint_as_float(u.w))
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < WPT; ++i)
+            wv[i] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, woff[i], c * Npad * 128, 0);
+    };
+
+    // split the loaded chunk into stage `buf`; returns whether this row's scale changed
+    auto store = [&](int buf) -> bool {
+        char* st = lds + buf * STAGE;
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < FPT / 4; ++i) m = fmax4(m, dv[i]);
+        if (TPR > 1) m = fmaxf(m, __shfl_xor(m, 1));
+        if (TPR > 2) m = fmaxf(m, __shfl_xor(m, 2));
+        const int e_new = max(e_run, bexp(m));
+        const int se_old = scale_exp(e_run), se = scale_exp(e_new);
+        e_run = e_new;
+        const float s = pow2(se);
+        // k_local = kp*FPT + j -> ks = k_local / 16, position k_local % 16
+#pragma unroll
+        for (int j = 0; j < FPT; j += 8) {
+            const int kl = kp * FPT + j, ks = kl >> 4, pos = kl & 15;
+            h8 hv, lv;
+            split8(dv[j / 4], dv[j / 4 + 1], s, hv, lv);
+            *reinterpret_cast<h8*>(st + ((0 * 2 + ks) * BD + rho) * 32 + pos * 2) = hv;
+            *reinterpret_cast<h8*>(st + ((1 * 2 + ks) * BD + rho) * 32 + pos * 2) = lv;
+        }
+        if (kp == 0) reinterpret_cast<float*>(st + D_BYTES + W_BYTES)[rho] = pow2(se - se_old);
+#pragma unroll
+        for (int i = 0; i < WPT; ++i)
+            *reinterpret_cast<u4v*>(st + D_BYTES + (t + i * NT) * 16) = wv[i];
+        return se != se_old;
+    };
+
+    f16v acc[TFT][TDT];
+#pragma unroll
+    for (int a = 0; a < TFT; ++a)
+#pragma unroll
+        for (int b = 0; b < TDT; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+    load(0);
+    store(0);
+    int any = 0;
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+        const int buf = c & 1;
+        const bool more = c + 1 < nc;
+        if (more) load(c + 1);
+        const char* st = lds + buf * STAGE;
+        if (any) {
+            const float* fac = reinterpret_cast<const float*>(st + D_BYTES + W_BYTES);
+#pragma unroll
+            for (int b = 0; b < TDT; ++b) {
+                const float f = fac[d_w + 32 * b + r];
+#pragma unroll
+                for (int a = 0; a < TFT; ++a) acc[a][b] *= f;
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            h8 wf[TFT][2], df[TDT][2];
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+#pragma unroll
+                for (int a = 0; a < TFT; ++a)
+                    wf[a][pt] = *reinterpret_cast<const h8*>(st + D_BYTES + ((pt * 2 + ks) * BF + f_w + 32 * a + r) * 32 + h * 16);
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    df[b][pt] = *reinterpret_cast<const h8*>(st + ((pt * 2 + ks) * BD + d_w + 32 * b + r) * 32 + h * 16);
+            }
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][0], df[b][0], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][0], df[b][1], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][1], df[b][0], acc[a][b], 0, 0, 0);
+        }
+        bool changed = false;
+        if (more) changed = store(buf ^ 1);
+        any = __syncthreads_or(changed);
+    }
+
+    // epilogue: C[m][n] = acc * 2^-se(m) * inv_t[n] + bias[n]
+    float* sc = reinterpret_cast<float*>(lds);
+    if (kp == 0) sc[rho] = pow2(-scale_exp(e_run));
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < TDT; ++b) {
+        const int dl = d_w + 32 * b + r;
+        const int64_t m = d0 + dl;
+        const float is = sc[dl];
+#pragma unroll
+        for (int a = 0; a < TFT; ++a) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = f0 + f_w + 32 * a + 8 * g + 4 * h;
+                const float4 it = *reinterpret_cast<const float4*>(inv_t + n);
+                float4 o;
+                o.x = acc[a][b][4 * g + 0] * is * it.x;
+                o.y = acc[a][b][4 * g + 1] * is * it.y;
+                o.z = acc[a][b][4 * g + 2] * is * it.z;
+                o.w = acc[a][b][4 * g + 3] * is * it.w;
+                if (bias != nullptr && n < N) {
+                    const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                    o.x += bb.x; o.y += bb.y; o.z += bb.z; o.w += bb.w;
+                }
+                if (m < M && n < N) *reinterpret_cast<float4*>(C + m * ldc + n) = o;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// TN GEMM (split over row ranges).  WM x WN waves, each TMT x TNT tiles of 32 x 32.
+// Loader: one slot per thread — threads [0, 2BM) own column t/2 of the A block, threads
+// [2BM, 2BM+2BN) column (t-2BM)/2 of the B block; t&1 selects the k-step (16 rows of the chunk).
+template <int WM, int WN, int TMT, int TNT>
+__global__ void __launch_bounds__(64 * WM * WN)
+k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
+          int64_t R, int Mc, int Nc, float* __restrict__ part, int n_mtiles, int n_ntiles,
+          int64_t rows_per_split) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int BM = 32 * TMT * WM, BN = 32 * TNT * WN;
+    static_assert(2 * (BM + BN) == NT, "loader mapping: one column slot per thread");
+    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+    constexpr int STAGE = A_BYTES + B_BYTES + (BM + BN) * 4;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+    const int t = threadIdx.x;
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int tiles = n_mtiles * n_ntiles;
+    const int p = wg / tiles, tile = wg % tiles;
+    const int m0 = (tile / n_ntiles) * BM, n0 = (tile % n_ntiles) * BN;
+    const int64_t v_begin = (int64_t)p * rows_per_split;
+    const int64_t v_end = (v_begin + rows_per_split < R) ? v_begin + rows_per_split : R;
+    const int nc = (int)((v_end - v_begin + KC - 1) / KC);
+
+    // loader slot (A or B is wave-uniform: waves [0, BM/32) load A)
+    const bool is_a = __builtin_amdgcn_readfirstlane(t >> 6) < 2 * BM / 64;
+    const int cl = is_a ? (t >> 1) : ((t - 2 * BM) >> 1), kse = t & 1;
+    const bool col_ok = is_a ? (m0 + cl < Mc) : (n0 + cl < Nc);
+    const float* xbase = is_a ? A : B;
+    const int ldx = (int)(is_a ? lda : ldb);
+    const int xoff = 16 * kse * ldx + (is_a ? m0 : n0) + (col_ok ? cl : 0);   // within a chunk
+    const int img = is_a ? 0 : A_BYTES, rows_img = is_a ? BM : BN, fac_off = is_a ? cl : BM + cl;
+    int e_run = -126;
+
+    const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    const int m_w = (w / WN) * TMT * 32, n_w = (w % WN) * TNT * 32;
+
+    float4 xv[4];
+    auto load = [&](int c) {
+        const int64_t vc = v_begin + (int64_t)c * KC;
+        const float* src = xbase + vc * ldx;                 // wave-uniform chunk base
+        float x[16];
+        if (vc + KC <= v_end) {
+            const rsrc_t rs = mk_rsrc(src, (uint32_t)(KC * ldx * 4));
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, xoff * 4, j * ldx * 4, 0));
+        } else {   // tail chunk: rows past v_end fail the range check and read as 0
+            const rsrc_t rs = mk_rsrc(src, (uint32_t)((v_end - vc) * ldx * 4));
+            int o = xoff * 4;
+            asm volatile("" : "+v"(o));      // keep the 16 offsets out of the loop preheader
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + j * ldx * 4, 0, 0));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            xv[j].x = col_ok ? x[4 * j + 0] : 0.f;
+            xv[j].y = col_ok ? x[4 * j + 1] : 0.f;
+            xv[j].z = col_ok ? x[4 * j + 2] : 0.f;
+            xv[j].w = col_ok ? x[4 * j + 3] : 0.f;
+        }
+    };
+    auto store = [&](int buf) -> bool {
+        char* st = lds + buf * STAGE;
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m = fmax4(m, xv[j]);
+        m = fmaxf(m, __shfl_xor(m, 1));
+        const int e_new = max(e_run, bexp(m));
+        const int se_old = scale_exp(e_run), se = scale_exp(e_new);
+        e_run = e_new;
+        const float s = pow2(se);
+        h8 hv[2], lv[2];
+        split8(xv[0], xv[1], s, hv[0], lv[0]);
+        split8(xv[2], xv[3], s, hv[1], lv[1]);
+        h8* hd = reinterpret_cast<h8*>(st + img + ((0 * 2 + kse) * rows_img + cl) * 32);
+        h8* ld = reinterpret_cast<h8*>(st + img + ((1 * 2 + kse) * rows_img + cl) * 32);
+        hd[0] = hv[0]; hd[1] = hv[1];
+        ld[0] = lv[0]; ld[1] = lv[1];
+        if (kse == 0) reinterpret_cast<float*>(st + A_BYTES + B_BYTES)[fac_off] = pow2(se - se_old);
+        return se != se_old;
+    };
+
+    f16v acc[TMT][TNT];
+#pragma unroll
+    for (int a = 0; a < TMT; ++a)
+#pragma unroll
+        for (int b = 0; b < TNT; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+    if (nc > 0) {
+        load(0);
+        store(0);
+    }
+    int any = 0;
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+        const int buf = c & 1;
+        const bool more = c + 1 < nc;
+        if (more) load(c + 1);
+        const char* st = lds + buf * STAGE;
+        if (any) {
+            const float* fac = reinterpret_cast<const float*>(st + A_BYTES + B_BYTES);
+#pragma unroll
+            for (int a = 0; a < TMT; ++a) {
+                float fa[16];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 f4 = *reinterpret_cast<const float4*>(fac + m_w + 32 * a + 8 * g + 4 * h);
+                    fa[4 * g] = f4.x; fa[4 * g + 1] = f4.y; fa[4 * g + 2] = f4.z; fa[4 * g + 3] = f4.w;
+                }
+#pragma unroll
+                for (int b = 0; b < TNT; ++b) {
+                    const float fb = fac[BM + n_w + 32 * b + r];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) acc[a][b][i] *= fa[i] * fb;
+                }
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            __builtin_amdgcn_sched_barrier(0);
+            h8 af[TMT][2], bf[TNT][2];
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+#pragma unroll
+                for (int a = 0; a < TMT; ++a)
+                    af[a][pt] = *reinterpret_cast<const h8*>(st + ((pt * 2 + ks) * BM + m_w + 32 * a + r) * 32 + h * 16);
+#pragma unroll
+                for (int b = 0; b < TNT; ++b)
+                    bf[b][pt] = *reinterpret_cast<const h8*>(st + A_BYTES + ((pt * 2 + ks) * BN + n_w + 32 * b + r) * 32 + h * 16);
+            }
+#pragma unroll
+            for (int a = 0; a < TMT; ++a)
+#pragma unroll
+                for (int b = 0; b < TNT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][0], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TMT; ++a)
+#pragma unroll
+                for (int b = 0; b < TNT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][0], bf[b][1], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TMT; ++a)
+#pragma unroll
+                for (int b = 0; b < TNT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][1], bf[b][0], acc[a][b], 0, 0, 0);
+        }
+        bool changed = false;
+        if (more) changed = store(buf ^ 1);
+        any = __syncthreads_or(changed);
+    }
+
+    // epilogue: part[p][m][n] = acc * 2^-se_a(m) * 2^-se_b(n)
+    float* sc = reinterpret_cast<float*>(lds);
+    if (kse == 0) sc[fac_off] = pow2(-scale_exp(e_run));
+    __syncthreads();
+    float* out = part + (int64_t)p * Mc * Nc;
+#pragma unroll
+    for (int b = 0; b < TNT; ++b) {
+        const int nl = n_w + 32 * b + r;
+        const int n = n0 + nl;
+        const float ib = sc[BM + nl];
+#pragma unroll
+        for (int a = 0; a < TMT; ++a) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int ml = m_w + 32 * a + (i & 3) + 8 * (i >> 2) + 4 * h;
+                const int m = m0 + ml;
+                if (m < Mc && n < Nc) out[(int64_t)m * Nc + n] = acc[a][b][i] * sc[ml] * ib;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_gemm_reduce(const float* __restrict__ part, int P, int64_t count, int Nc, float* __restrict__ C, int64_t ldc) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    float s = 0.f;
+    for (int q = 0; q < P; ++q) s += part[(int64_t)q * count + i];
+    C[(i / Nc) * ldc + i % Nc] = s;
+}
+
+}  // namespace
+
+int64_t gemm_pack_npad(int64_t N) { return (N + 255) / 256 * 256; }
+int64_t gemm_pack_bytes(int64_t N, int64_t K) {
+    const int64_t np = gemm_pack_npad(N), kc = (K + KC - 1) / KC;
+    return kc * 4 * np * 32 + np * 4;
+}
+
+hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st) {
+    const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
+    _Float16* out = static_cast<_Float16*>(packed);
+    float* inv = reinterpret_cast<float*>(static_cast<char*>(packed) + (int64_t)kc * 4 * np * 32);
+    hipLaunchKernelGGL(k_pack_weight, dim3(np), dim3(64), 0, st, W, ldw, N, K, trans, np, kc, out, inv);
+    return hipGetLastError();
+}
+
+hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
+                       const float* bias, float* C, int64_t ldc, hipStream_t st) {
+    if (M == 0 || N == 0) return hipSuccess;
+    const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
+    const u4v* wp = static_cast<const u4v*>(packed);
+    const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
+    if (N > 128) {
+        constexpr int BD = 256, BF = 256;
+        const int nft = (N + BF - 1) / BF;
+        const int64_t nblk = (M + BD - 1) / BD * nft;
+        hipLaunchKernelGGL((k_gemm_nt<2, 4, 4, 2>), dim3((unsigned)nblk), dim3(512), 0, st,
+                           A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+    } else {
+        constexpr int BD = 256, BF = 128;
+        const int nft = (N + BF - 1) / BF;
+        const int64_t nblk = (M + BD - 1) / BD * nft;
+        hipLaunchKernelGGL((k_gemm_nt<4, 2, 2, 2>), dim3((unsigned)nblk), dim3(512), 0, st,
+                           A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+    }
+    return hipGetLastError();
+}
+
+int gemm_tn_splits(int64_t R, int64_t Mc, int64_t Nc) {
+    const int64_t tiles = ((Mc + 255) / 256) * ((Nc + 255) / 256);
+    int64_t P = (256 + tiles - 1) / tiles;
+    const int64_t pmax = (R + 2047) / 2048;      // >= 2048 rows per split
+    if (P > pmax) P = pmax;
+    if (P < 1) P = 1;
+    return (int)P;
+}
+
+int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc) {
+    return (int64_t)gemm_tn_splits(R, Mc, Nc) * Mc * Nc * 4;
+}
+
+hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
+                       float* C, int64_t ldc, void* workspace, hipStream_t st) {
+    if (Mc == 0 || Nc == 0) return hipSuccess;
+    const int P = gemm_tn_splits(R, Mc, Nc);
+    const int64_t rps = (R + P - 1) / P;
+    const int nmt = (Mc + 255) / 256, nnt = (Nc + 255) / 256;
+    float* part = static_cast<float*>(workspace);
+    hipLaunchKernelGGL((k_gemm_tn<4, 4, 2, 2>), dim3((unsigned)(P * nmt * nnt)), dim3(1024), 0, st,
+                       A, lda, B, ldb, R, Mc, Nc, part, nmt, nnt, rps);
+    const int64_t count = (int64_t)Mc * Nc;
+    hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
+                       part, P, count, Nc, C, ldc);
+    return hipGetLastError();
+}
+
+}  // namespace sir

@@ -89,4 +89,13 @@ hipError_t run_csr_build(const int64_t* rows, const int64_t* cols, int64_t E, in
 hipError_t run_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int* pos_ws, int* perm,
                         hipStream_t st);
 
+// projection GEMMs, sirconv_gemm.hip
+int64_t gemm_pack_bytes(int64_t N, int64_t K);
+hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st);
+hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
+                       const float* bias, float* C, int64_t ldc, hipStream_t st);
+int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc);
+hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
+                       float* C, int64_t ldc, void* workspace, hipStream_t st);
+
 }  // namespace sir

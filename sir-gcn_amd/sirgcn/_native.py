@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16 = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
 _P, _I64, _I, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
@@ -37,6 +37,11 @@ SIGNATURES = {
     "sir_csr_build_workspace": (ctypes.c_int64, [_I64, _I64]),
     "sir_csr_build": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "sir_csr_perm": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
+    "sir_gemm_pack_bytes": (ctypes.c_int64, [_I64, _I64]),
+    "sir_gemm_pack": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _P, _P]),
+    "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
+    "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
+    "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
@@ -61,10 +66,11 @@ def enable_timing(on=True):
 
 
 class _Timed:
-    __slots__ = ("name", "dev", "ev")
+    """Records (start, end, work) on the launching stream; ``work`` = flops for the GEMMs."""
+    __slots__ = ("name", "dev", "ev", "work")
 
-    def __init__(self, name, dev):
-        self.name, self.dev, self.ev = name, dev, None
+    def __init__(self, name, dev, work=0):
+        self.name, self.dev, self.ev, self.work = name, dev, None, work
 
     def __enter__(self):
         if _timing is not None:
@@ -75,7 +81,7 @@ class _Timed:
     def __exit__(self, *exc):
         if self.ev is not None:
             self.ev[1].record(torch.cuda.current_stream(self.dev))
-            _timing.setdefault(self.name, []).append(self.ev)
+            _timing.setdefault(self.name, []).append((self.ev[0], self.ev[1], self.work))
 
 
 def load():
@@ -291,3 +297,52 @@ def graph_norm_bwd(off, X, dY, weight, mean_scale, mean, std, dX, dw_part, dms_p
                                     _ptr(mean_scale), _ptr(mean), _ptr(std), _ptr(dX), _ld(dX, F),
                                     _ptr(dw_part), _ptr(dms_part), _ptr(db_part), _stream(dX.device))
     _check(rc, lib)
+
+
+# ------------------------------------------------------------------------------ projection GEMMs
+def gemm_pack(W, trans=False):
+    """Pack the weight operand of ``gemm_nt``: B = W ([N, K], an nn.Linear weight used as x W^T)
+    or, with trans=True, B = W^T (W [K, N], used as x W).  Returns (packed uint8 tensor, N, K)."""
+    lib = load()
+    assert W.dtype == torch.float32 and W.dim() == 2 and W.stride(1) == 1
+    N, K = (W.shape[1], W.shape[0]) if trans else (W.shape[0], W.shape[1])
+    nbytes = lib.sir_gemm_pack_bytes(N, K)
+    if nbytes <= 0:
+        raise RuntimeError(f"sir_gemm_pack_bytes({N}, {K}) failed")
+    packed = torch.empty((nbytes,), dtype=torch.uint8, device=W.device)
+    with _Timed("sir_gemm_pack", W.device):
+        rc = lib.sir_gemm_pack(_ptr(W), W.stride(0), N, K, int(bool(trans)), _ptr(packed), _stream(W.device))
+    _check(rc, lib)
+    return packed, N, K
+
+
+def gemm_nt(A, packed, bias=None, out=None):
+    """C = A B^T (+ bias) on the split-fp16 MFMA kernel; ``packed`` from gemm_pack."""
+    lib = load()
+    pk, N, K = packed
+    M = A.shape[0]
+    assert A.dim() == 2 and A.shape[1] == K and A.stride(1) == 1
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    with _Timed("sir_gemm_nt", A.device, 2 * M * N * K):
+        rc = lib.sir_gemm_nt(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(bias), _ptr(out), out.stride(0),
+                             _stream(A.device))
+    _check(rc, lib)
+    return out
+
+
+def gemm_tn(A, B, out=None):
+    """C = A^T B (A [R, M], B [R, N]) on the split-fp16 MFMA kernel (split over row ranges)."""
+    lib = load()
+    R, M = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == R and A.stride(1) == 1 and B.stride(1) == 1
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    ws_bytes = lib.sir_gemm_tn_workspace(R, M, N)
+    ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=A.device)
+    with _Timed("sir_gemm_tn", A.device, 2 * R * M * N):
+        rc = lib.sir_gemm_tn(_ptr(A), A.stride(0), _ptr(B), B.stride(0), R, M, N, _ptr(out), out.stride(0),
+                             _ptr(ws), ws.numel(), _stream(A.device))
+    _check(rc, lib)
+    return out

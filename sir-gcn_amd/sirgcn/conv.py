@@ -12,16 +12,17 @@ Mirrors briangodwinlim/SIR-GCN ``models/conv.py:7-67``:
   clamp(deg, 1)) / sym aggregation (``conv.py:41,63``), ``Y = W_R S + b_R`` (``conv.py:65``) so
   isolated destinations output ``b_R``.
 
-What runs where: the two node projections are ONE GEMM against the concatenated [W_Q; W_K]
-(rocBLAS/hipBLASLt through torch), the edge aggregation and its backward are the HIP kernels
-of ``libsirconv.so`` (C ABI, ``include/sirconv.h``), W_R is a torch GEMM.  There is no CPU
+What runs where: the two node projections are ONE GEMM against the concatenated [W_Q; W_K],
+the edge aggregation and its backward are the edge kernels, W_R and every backward GEMM are the
+split-fp16 MFMA GEMMs (``linalg``) — all HIP kernels of ``libsirconv.so`` (C ABI,
+``include/sirconv.h``).  There is no CPU
 path: a CPU tensor, a missing library or an unsupported sigma/agg raises.
 """
 import torch
 from torch import nn
 import torch.nn.functional as F
 
-from . import _native
+from . import _native, linalg
 from .graph import DEFAULT_CHUNK, get_plan
 
 
@@ -106,23 +107,7 @@ def _partial(plan, H, device):
     return torch.empty((max(n, 1) * H,), device=device, dtype=torch.float32) if n else None
 
 
-def _tn(A, B):
-    """A^T B for tall A [V, m], B [V, n] (the weight-gradient GEMMs, K = V).
-
-    hipBLASLt runs these long-K shapes at ~60-75 TF/s fp32; splitting K into k row blocks as one
-    batched GEMM and summing the k partial products runs at 130-150 TF/s on MI355X
-    (tools/gemm_probe.py).  Deterministic (fixed split)."""
-    V = A.shape[0]
-    k = 32
-    while k > 1 and V // k < 4096:
-        k //= 2
-    if k == 1:
-        return A.t() @ B
-    n = (V // k) * k
-    out = torch.bmm(A[:n].view(k, n // k, A.shape[1]).transpose(1, 2), B[:n].view(k, n // k, B.shape[1])).sum(0)
-    if n < V:
-        out += A[n:].t() @ B[n:]
-    return out
+_tn = linalg.mm_tn
 
 
 def _bias_grad(G):
@@ -145,10 +130,7 @@ class SIRConvFunction(torch.autograd.Function):
         H = W_Q.shape[0]
         X = X.contiguous()
         W_cat = torch.cat([W_Q, W_K], 0)
-        if b_Q is not None:
-            QK = torch.addmm(torch.cat([b_Q, b_Q.new_zeros(H)]), X, W_cat.t())
-        else:
-            QK = torch.mm(X, W_cat.t())
+        QK = linalg.mm_wt(X, W_cat, torch.cat([b_Q, b_Q.new_zeros(H)]) if b_Q is not None else None)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=torch.float32)
@@ -157,7 +139,7 @@ class SIRConvFunction(torch.autograd.Function):
         nw = _native.mask_words(H, act) if (EdgeAggregate.use_mask and training) else 0
         mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=X.device, dtype=torch.int64) if nw else None
         _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, act, slope, S, partial, mask)
-        Y = torch.addmm(b_R, S, W_R.t()) if b_R is not None else torch.mm(S, W_R.t())
+        Y = linalg.mm_wt(S, W_R, b_R)
         ctx.save_for_backward(X, W_cat, W_R, S, mask if mask is not None else QK)
         ctx.masked = mask is not None
         ctx.plan, ctx.agg, ctx.act, ctx.slope = plan, agg, act, slope
@@ -171,7 +153,7 @@ class SIRConvFunction(torch.autograd.Function):
         H = W_R.shape[1]
         V = X.shape[0]
         dY = dY.contiguous()
-        G = torch.mm(dY, W_R)
+        G = linalg.mm_w(dY, W_R)
         dW_R = _tn(dY, S) if ctx.needs_input_grad[4] else None
         db_R = _bias_grad(dY) if ctx.has_br and ctx.needs_input_grad[5] else None
         in_norm, out_norm = plan.norms(agg)
@@ -188,7 +170,7 @@ class SIRConvFunction(torch.autograd.Function):
                                  dQK[:, :H], Gm, partial, mask)
         _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
                                  agg, act, slope, dQK[:, H:], partial, mask)
-        dX = torch.mm(dQK, W_cat) if ctx.needs_input_grad[0] else None
+        dX = linalg.mm_w(dQK, W_cat) if ctx.needs_input_grad[0] else None
         dW_Q = dW_K = None
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
             dW = _tn(dQK, X)

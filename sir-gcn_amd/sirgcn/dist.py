@@ -30,7 +30,7 @@ The per-rank edge work uses the same kernels/ABI as one GPU (``_native``).  A di
 import torch
 import torch.distributed as dist
 
-from . import _native
+from . import _native, linalg
 from .conv import _tn, activation_code
 from .graph import DEFAULT_CHUNK, build_plans_native, build_row_csr
 
@@ -236,9 +236,9 @@ class DistSIRConvFunction(torch.autograd.Function):
         dev = X.device
         X = X.contiguous()
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
-        torch.mm(X, W_K.t(), out=K_ext[:n])
+        linalg.mm_wt(X, W_K, out=K_ext[:n])
         work = dg.gather_halo(K_ext[:n], K_ext[n:], async_op=True)
-        Q = torch.addmm(b_Q, X, W_Q.t()) if b_Q is not None else torch.mm(X, W_Q.t())
+        Q = linalg.mm_wt(X, W_Q, b_Q)
         if work is not None:
             work.wait()
         in_norm, out_norm = dg.norms(agg)
@@ -248,7 +248,7 @@ class DistSIRConvFunction(torch.autograd.Function):
         nw = _native.mask_words(H, act) if (use_mask and training and backend is _native) else 0
         mask = torch.empty((max(dg.dst.col.numel(), 1) * nw,), device=dev, dtype=torch.int64) if nw else None
         backend.edge_agg_fwd(dg.dst, Q, K_ext, in_norm, out_norm, agg, act, slope, S, partial, mask)
-        Y = torch.addmm(b_R, S, W_R.t()) if b_R is not None else torch.mm(S, W_R.t())
+        Y = linalg.mm_wt(S, W_R, b_R)
         if mask is not None:
             ctx.save_for_backward(X, W_Q, W_K, W_R, S, mask)
         else:
@@ -271,7 +271,7 @@ class DistSIRConvFunction(torch.autograd.Function):
         n = dg.n_rows
         dev = X.device
         dY = dY.contiguous()
-        G = torch.mm(dY, W_R)
+        G = linalg.mm_w(dY, W_R)
         in_norm, out_norm = dg.norms(agg)
         partial = _workspace(dg, H, dev)
         dQ = torch.empty((n, H), device=dev, dtype=torch.float32)
@@ -289,7 +289,7 @@ class DistSIRConvFunction(torch.autograd.Function):
                                      mask)
         dW_R = _tn(dY, S) if ctx.needs_input_grad[4] else None
         db_R = _colsum(dY) if ctx.has_br and ctx.needs_input_grad[5] else None
-        dX = torch.mm(dQ, W_Q) if ctx.needs_input_grad[0] else None
+        dX = linalg.mm_w(dQ, W_Q) if ctx.needs_input_grad[0] else None
         dW_Q = _tn(dQ, X) if ctx.needs_input_grad[1] else None
         db_Q = _colsum(dQ) if ctx.has_bq and ctx.needs_input_grad[2] else None
         if work is not None:
@@ -298,7 +298,7 @@ class DistSIRConvFunction(torch.autograd.Function):
         if dg.world > 1:
             dg.add_received(dK, recv)
         if dX is not None:
-            dX.addmm_(dK, W_K)
+            dX += linalg.mm_w(dK, W_K)
         dW_K = _tn(dK, X) if ctx.needs_input_grad[3] else None
         return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None
 

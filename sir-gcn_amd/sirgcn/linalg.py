@@ -1,0 +1,64 @@
+"""The layer's projection GEMMs on the native split-fp16 MFMA kernels (``sir_gemm_nt`` /
+``sir_gemm_tn``, include/sirconv.h).
+
+These are the nn.Linear calls of the reference (``conv.py:60-61`` Q/K, ``conv.py:65`` W_R) and
+their autograd: ``mm_wt`` = A W^T (+ b) (forward projections), ``mm_w`` = A W (G = dY W_R,
+dX = dQK [W_Q; W_K]), ``mm_tn`` = A^T B (the weight gradients, contraction over the node rows).
+fp32 in / fp32 out at fp32 accuracy (tests/test_gemm_gpu.py).  Operands the kernels do not take
+(CPU tensors of the gloo rehearsals, non-fp32, feature widths not a multiple of 4, unaligned
+views) go to torch's own GEMM; ``USE_NATIVE = False`` forces that for A/B runs.
+"""
+import torch
+
+from . import _native
+
+USE_NATIVE = True
+
+
+def _ok(t):
+    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+            and t.stride(0) % 4 == 0 and t.shape[1] % 4 == 0 and t.data_ptr() % 16 == 0)
+
+
+def mm_wt(A, W, bias=None, out=None):
+    """A W^T + bias (nn.Linear); W [N, K]."""
+    if (USE_NATIVE and _ok(A) and W.is_cuda and W.dtype == torch.float32 and W.shape[0] % 4 == 0
+            and (bias is None or (bias.is_contiguous() and bias.data_ptr() % 16 == 0))
+            and (out is None or _ok(out))):
+        return _native.gemm_nt(A, _native.gemm_pack(W.contiguous()), bias, out)
+    if out is None:
+        return torch.addmm(bias, A, W.t()) if bias is not None else torch.mm(A, W.t())
+    if bias is not None:
+        return torch.addmm(bias, A, W.t(), out=out)
+    return torch.mm(A, W.t(), out=out)
+
+
+def mm_w(A, W):
+    """A W; W [K, N]."""
+    if USE_NATIVE and _ok(A) and W.is_cuda and W.dtype == torch.float32 and W.shape[1] % 4 == 0:
+        return _native.gemm_nt(A, _native.gemm_pack(W.contiguous(), trans=True))
+    return torch.mm(A, W)
+
+
+def mm_tn(A, B):
+    """A^T B for tall A [R, M], B [R, N] (the weight gradients)."""
+    if (USE_NATIVE and A.is_cuda and B.is_cuda and A.dtype == torch.float32 and B.dtype == torch.float32
+            and A.dim() == 2 and B.dim() == 2 and A.stride(1) == 1 and B.stride(1) == 1):
+        return _native.gemm_tn(A, B)
+    return _tn_torch(A, B)
+
+
+def _tn_torch(A, B):
+    """torch A^T B; long-K shapes run as k row blocks of one batched GEMM (hipBLASLt is 2x faster
+    that way than as one GEMM) summed in a fixed order."""
+    V = A.shape[0]
+    k = 32
+    while k > 1 and V // k < 4096:
+        k //= 2
+    if k == 1:
+        return A.t() @ B
+    n = (V // k) * k
+    out = torch.bmm(A[:n].view(k, n // k, A.shape[1]).transpose(1, 2), B[:n].view(k, n // k, B.shape[1])).sum(0)
+    if n < V:
+        out += A[n:].t() @ B[n:]
+    return out

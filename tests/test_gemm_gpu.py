@@ -1,0 +1,119 @@
+"""GPU numerics of the split-fp16 MFMA projection GEMMs (sir_gemm_nt / sir_gemm_tn, through the
+C ABI) against an fp64 evaluation, with torch's own fp32 GEMM as the yardstick.
+
+Bar (the GEMMs of conv.py:60-61,65 and their autograd are floating point, so "parity" is
+accuracy): per output element |C - C64| <= max(4e-7, 2x torch fp32 worst) * sum_k |a_ik||b_kj| (an fp32 GEMM rounding is
+bounded by ~K * 6e-8 of the same sum; ours measures like torch's), and relative L2 error vs fp64
+<= max(2 * torch fp32's, 1e-6).  Runs: pytest tests -m gpu."""
+import pytest
+import torch
+
+from sirgcn import _native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X box"
+    _native.load()
+
+
+def _rel(a, b):
+    d = b.norm().item()
+    return (a - b).norm().item() / d if d > 0 else (a - b).norm().item()
+
+
+def _check(C, A64, B64, ref32, bias=None, what=""):
+    """C vs fp64 A64 @ B64 (+bias); elementwise bound by the absolute-product sum."""
+    C64 = A64 @ B64
+    absum = A64.abs() @ B64.abs()
+    if bias is not None:
+        C64 = C64 + bias.double()
+        absum = absum + bias.double().abs()
+    den = absum + 1e-300
+    worst = ((C.double() - C64).abs() / den).max().item() if C.numel() else 0.0
+    worst_torch = ((ref32.double() - C64).abs() / den).max().item() if C.numel() else 0.0
+    assert worst <= max(4e-7, 2 * worst_torch), \
+        f"{what}: max |err| / sum|a||b| = {worst:.2e} (torch fp32: {worst_torch:.2e})"
+    e_ours, e_torch = _rel(C.double(), C64), _rel(ref32.double(), C64)
+    assert e_ours <= max(2 * e_torch, 1e-6), f"{what}: relL2 {e_ours:.2e} vs torch fp32 {e_torch:.2e}"
+    return e_ours, e_torch
+
+
+@pytest.mark.parametrize("M", [1, 255, 257, 4099])
+@pytest.mark.parametrize("K,N", [(4, 4), (32, 64), (36, 132), (256, 256), (256, 512), (512, 256), (300, 300),
+                                 (64, 128), (1024, 96)])
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_gemm_nt_vs_fp64(M, K, N, with_bias):
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + K * 3 + N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g) if with_bias else None
+    C = _native.gemm_nt(A, _native.gemm_pack(W), b)
+    ref = torch.addmm(b, A, W.t()) if with_bias else A @ W.t()
+    _check(C, A.double(), W.double().t(), ref, b, f"nt M={M} K={K} N={N}")
+
+
+@pytest.mark.parametrize("K,N", [(256, 256), (512, 256), (128, 64)])
+def test_gemm_nt_transposed_weight(K, N):
+    """B = W^T (W [K, N]): the x W form of G = dY W_R and dX = dQK [W_Q; W_K]."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    A = torch.randn(3001, K, device=DEV, generator=g)
+    W = torch.randn(K, N, device=DEV, generator=g)
+    C = _native.gemm_nt(A, _native.gemm_pack(W, trans=True))
+    _check(C, A.double(), W.double(), A @ W, None, "nt trans")
+
+
+def test_gemm_nt_wide_dynamic_range_and_running_scale():
+    """Rows spanning 2^-40..2^40, zero rows, and rows whose maximum grows along K (every chunk
+    raises the running scale: exercises the accumulator rescale), plus tiny/huge weights (all
+    products stay inside the fp32 range)."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    M, K, N = 1500, 512, 256
+    A = torch.randn(M, K, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-40, 40, (M, 1), device=DEV, generator=g).float())
+    A[7] = 0
+    ramp = torch.exp2(torch.linspace(-30, 30, K, device=DEV))
+    A[100:300] *= ramp                      # maximum rises chunk after chunk
+    A[300:400] *= ramp.flip(0)
+    W = torch.randn(N, K, device=DEV, generator=g) * torch.exp2(torch.randint(-20, 20, (N, 1), device=DEV,
+                                                                                generator=g).float())
+    C = _native.gemm_nt(A, _native.gemm_pack(W))
+    assert torch.all(C[7] == 0)
+    _check(C, A.double(), W.double().t(), A @ W.t(), None, "nt dynamic range")
+
+
+@pytest.mark.parametrize("R", [0, 1, 31, 33, 1000, 70001])
+@pytest.mark.parametrize("M,N", [(4, 4), (32, 36), (256, 256), (512, 256), (300, 100)])
+def test_gemm_tn_vs_fp64(R, M, N):
+    g = torch.Generator(device=DEV).manual_seed(R + 3 * M + N)
+    A = torch.randn(R, M, device=DEV, generator=g)
+    B = torch.randn(R, N, device=DEV, generator=g)
+    C = _native.gemm_tn(A, B)
+    if R == 0:
+        assert torch.all(C == 0)
+        return
+    _check(C, A.double().t(), B.double(), A.t() @ B, None, f"tn R={R} M={M} N={N}")
+
+
+def test_gemm_tn_dynamic_range_strided_and_deterministic():
+    g = torch.Generator(device=DEV).manual_seed(9)
+    R = 50000
+    A0 = torch.randn(R, 600, device=DEV, generator=g)
+    A = A0[:, 40:552]                                       # lda = 600, 512 columns
+    A *= torch.exp2(torch.randint(-40, 40, (1, 512), device=DEV, generator=g).float())
+    B = torch.randn(R, 256, device=DEV, generator=g)
+    B[20000:21000] *= 2.0 ** 30                             # a late row block raises the B scales
+    C1 = _native.gemm_tn(A, B)
+    C2 = _native.gemm_tn(A, B)
+    assert torch.equal(C1, C2), "TN GEMM must be run-to-run deterministic"
+    _check(C1, A.double().t(), B.double(), A.t() @ B, None, "tn dynamic range")
+
+
+def test_gemm_errors_are_loud():
+    A = torch.randn(10, 6, device=DEV)
+    pk = _native.gemm_pack(torch.randn(8, 6, device=DEV))
+    with pytest.raises(RuntimeError, match="multiples of 4"):
+        _native.gemm_nt(A, pk)
