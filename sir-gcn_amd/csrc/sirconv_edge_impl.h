@@ -450,6 +450,47 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
     }
 }
 
+// The edge loop of one item (UNROLL-edge batches, then a binary tail).
+template <int MODE, int ACT, int AGG, int NV, int U>
+__device__ __forceinline__ void mask_item(int e0, int e1, const int* __restrict__ col, const int* __restrict__ perm,
+                                          const float* __restrict__ G, int64_t ldg,
+                                          const uint64_t* __restrict__ mask,
+                                          const float* __restrict__ norm_col, float nr, float slope,
+                                          int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4]) {
+    int e = e0;
+    for (; e + U <= e1; e += U)
+        mask_batch<MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    if constexpr (U > 8) {
+        if (e + 8 <= e1) {
+            mask_batch<MODE, ACT, AGG, NV, 8>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            e += 8;
+        }
+    }
+    if constexpr (U > 4) {
+        if (e + 4 <= e1) {
+            mask_batch<MODE, ACT, AGG, NV, 4>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            e += 4;
+        }
+    }
+    if constexpr (U > 2) {
+        if (e + 2 <= e1) {
+            mask_batch<MODE, ACT, AGG, NV, 2>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            e += 2;
+        }
+    }
+    if (e < e1)
+        mask_batch<MODE, ACT, AGG, NV, 1>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+}
+
+__device__ __forceinline__ int4 uniform_item(const int4* __restrict__ items, int64_t i) {
+    int4 it = items[i];
+    it.x = __builtin_amdgcn_readfirstlane(it.x);
+    it.y = __builtin_amdgcn_readfirstlane(it.y);
+    it.z = __builtin_amdgcn_readfirstlane(it.z);
+    it.w = __builtin_amdgcn_readfirstlane(it.w);
+    return it;
+}
+
 template <int MODE, int ACT, int AGG, int NV, int U>
 __global__ void __launch_bounds__(256)
 k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
@@ -461,11 +502,7 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     const int lane = threadIdx.x & 63;
     const int64_t wave = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     if (wave >= n_items) return;
-    int4 it = items[wave];
-    it.x = __builtin_amdgcn_readfirstlane(it.x);
-    it.y = __builtin_amdgcn_readfirstlane(it.y);
-    it.z = __builtin_amdgcn_readfirstlane(it.z);
-    it.w = __builtin_amdgcn_readfirstlane(it.w);
+    const int4 it = uniform_item(items, wave);
     const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
     const int HC = H / 4;
     float gv[NV][4];
@@ -499,29 +536,7 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     }
     float nr = 1.f;
     if constexpr (AGG == AGG_SYM) nr = norm_row[row];
-    int e = e0;
-    for (; e + U <= e1; e += U)
-        mask_batch<MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
-    if constexpr (U > 8) {
-        if (e + 8 <= e1) {
-            mask_batch<MODE, ACT, AGG, NV, 8>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
-            e += 8;
-        }
-    }
-    if constexpr (U > 4) {
-        if (e + 4 <= e1) {
-            mask_batch<MODE, ACT, AGG, NV, 4>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
-            e += 4;
-        }
-    }
-    if constexpr (U > 2) {
-        if (e + 2 <= e1) {
-            mask_batch<MODE, ACT, AGG, NV, 2>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
-            e += 2;
-        }
-    }
-    if (e < e1)
-        mask_batch<MODE, ACT, AGG, NV, 1>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    mask_item<MODE, ACT, AGG, NV, U>(e0, e1, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
     float* op = (slot < 0) ? out + (int64_t)row * ldo : partial + (int64_t)slot * H;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {

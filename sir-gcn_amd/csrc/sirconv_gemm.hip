@@ -36,6 +36,10 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 constexpr int KC = 32;          // contraction elements per LDS stage (two k16 MFMA steps)
 
+#ifndef SIR_NT_EPI
+#define SIR_NT_EPI 1            // 1: NT epilogue through LDS, full-row stores; 0: fragment stores
+#endif
+
 // Smallest e with |m| < 2^e for normal m (e = -126 for 0 and subnormals, 129 for inf/nan).
 __device__ inline int bexp(float m) { return (int)((__float_as_uint(m) >> 23) & 255u) - 126; }
 // scale exponent for a running binade e: |x| * 2^(15 - e) < 2^15, clamped to a normal float
@@ -242,6 +246,56 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
     }
 
     // epilogue: C[m][n] = acc * 2^-se(m) * inv_t[n] + bias[n]
+#if SIR_NT_EPI == 1
+    // Through LDS, one 32-row band of every wave per round: the waves write their scaled float4
+    // fragments into a row-major image (row pitch BF*4 + 16 B: conflict-free ds_write_b128), then
+    // the block stores whole output rows — every wave-instruction writes BF*4 contiguous bytes
+    // (full cache lines) instead of 32 rows x 32 B.
+    constexpr int RR = WD * 32, PITCH = BF * 4 + 16;
+    constexpr int SC_OFF = STAGE + D_BYTES + W_BYTES;
+    static_assert(RR * PITCH <= SC_OFF, "epilogue image overlaps the scale row");
+    static_assert((RR * BF / 4) % NT == 0, "epilogue copy mapping");
+    float* sc = reinterpret_cast<float*>(lds + SC_OFF);
+    if (kp == 0) sc[rho] = pow2(-scale_exp(e_run));
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < TDT; ++b) {
+        const int dl = d_w + 32 * b + r;
+        const float is = sc[dl];
+        char* rowp = lds + ((w / WF) * 32 + r) * PITCH;
+#pragma unroll
+        for (int a = 0; a < TFT; ++a) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int nl = f_w + 32 * a + 8 * g + 4 * h;
+                const int n = f0 + nl;
+                const float4 it = *reinterpret_cast<const float4*>(inv_t + n);
+                float4 o;
+                o.x = acc[a][b][4 * g + 0] * is * it.x;
+                o.y = acc[a][b][4 * g + 1] * is * it.y;
+                o.z = acc[a][b][4 * g + 2] * is * it.z;
+                o.w = acc[a][b][4 * g + 3] * is * it.w;
+                if (bias != nullptr && n < N) {
+                    const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                    o.x += bb.x; o.y += bb.y; o.z += bb.z; o.w += bb.w;
+                }
+                *reinterpret_cast<float4*>(rowp + nl * 4) = o;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < RR * BF / 4 / NT; ++k) {
+            const int idx = t + k * NT;
+            const int row = idx / (BF / 4), c4 = idx % (BF / 4);
+            const int64_t m = d0 + (row >> 5) * (TDT * 32) + 32 * b + (row & 31);
+            const int n = f0 + c4 * 4;
+            const float4 o = *reinterpret_cast<const float4*>(lds + row * PITCH + c4 * 16);
+            if (m < M && n < N) *reinterpret_cast<float4*>(C + m * ldc + n) = o;
+        }
+        __syncthreads();
+    }
+}
+#else
     float* sc = reinterpret_cast<float*>(lds);
     if (kp == 0) sc[rho] = pow2(-scale_exp(e_run));
     __syncthreads();
@@ -270,6 +324,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
         }
     }
 }
+#endif
 
 // ------------------------------------------------------------------------------------------
 // TN GEMM (split over row ranges).  WM x WN waves, each TMT x TNT tiles of 32 x 32.

@@ -2,9 +2,12 @@
 C ABI) against an fp64 evaluation, with torch's own fp32 GEMM as the yardstick.
 
 Bar (the GEMMs of conv.py:60-61,65 and their autograd are floating point, so "parity" is
-accuracy): per output element |C - C64| <= max(4e-7, 2x torch fp32 worst) * sum_k |a_ik||b_kj| (an fp32 GEMM rounding is
-bounded by ~K * 6e-8 of the same sum; ours measures like torch's), and relative L2 error vs fp64
-<= max(2 * torch fp32's, 1e-6).  Runs: pytest tests -m gpu."""
+accuracy): per output element |C - C64| <= max(8e-7, 2x torch fp32 worst) * sum_k |a_ik||b_kj|, and
+relative L2 error vs fp64 <= max(2 * torch fp32's, 1e-6).  The 8e-7 floor is the split's own
+per-product bound: x*w is formed as hi*hi' + hi*lo' + lo*hi' with lo*lo' (< 2^-22 relative) dropped
+and each lo rounded to fp16 (< 2^-22 each), i.e. <= 3 * 2^-22 = 7.2e-7 of |x||w| — visible alone
+only when K (or R) is tiny, where fp32's single rounding is smaller; for real contraction lengths
+the fp32 accumulation dominates both.  Runs: pytest tests -m gpu."""
 import pytest
 import torch
 
@@ -35,7 +38,7 @@ def _check(C, A64, B64, ref32, bias=None, what=""):
     den = absum + 1e-300
     worst = ((C.double() - C64).abs() / den).max().item() if C.numel() else 0.0
     worst_torch = ((ref32.double() - C64).abs() / den).max().item() if C.numel() else 0.0
-    assert worst <= max(4e-7, 2 * worst_torch), \
+    assert worst <= max(8e-7, 2 * worst_torch), \
         f"{what}: max |err| / sum|a||b| = {worst:.2e} (torch fp32: {worst_torch:.2e})"
     e_ours, e_torch = _rel(C.double(), C64), _rel(ref32.double(), C64)
     assert e_ours <= max(2 * e_torch, 1e-6), f"{what}: relL2 {e_ours:.2e} vs torch fp32 {e_torch:.2e}"
