@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 3
+#define SIR_ABI_VERSION 4
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -248,10 +248,13 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
 
 /* C[M, N] = A^T B with A [R, M] (lda), B [R, N] (ldb): the weight gradients (contraction over the
  * R node rows, split over row ranges; the partial products are added in a fixed order, so the
- * result is run-to-run deterministic).  workspace: sir_gemm_tn_workspace(R, M, N) bytes. */
+ * result is run-to-run deterministic).  colsum_a [M] or NULL: also the column sums of A
+ * (sum_r A[r][m]) — the bias gradient of the same linear (db_R = sum dY with A = dY, db_Q with
+ * A = dQ), read from the loads the GEMM does anyway; deterministic.
+ * workspace: sir_gemm_tn_workspace(R, M, N) bytes. */
 int64_t sir_gemm_tn_workspace(int64_t R, int64_t M, int64_t N);
 int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int64_t M, int64_t N,
-                float* C, int64_t ldc, void* workspace, int64_t workspace_bytes, void* stream);
+                float* C, int64_t ldc, float* colsum_a, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

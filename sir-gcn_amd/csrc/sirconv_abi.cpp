@@ -378,14 +378,14 @@ int64_t sir_gemm_tn_workspace(int64_t R, int64_t M, int64_t N) {
 }
 
 int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int64_t M, int64_t N,
-                float* C, int64_t ldc, void* workspace, int64_t workspace_bytes, void* stream) {
+                float* C, int64_t ldc, float* colsum_a, void* workspace, int64_t workspace_bytes, void* stream) {
     const char* fn = "sir_gemm_tn";
     if (R < 0 || M <= 0 || N <= 0 || M > 65536 || N > 65536) return fail(SIR_EINVAL, fn, "bad shape");
     if (lda < M || ldb < N || ldc < N) return fail(SIR_EINVAL, fn, "leading dimension too small");
     if (C == nullptr || workspace == nullptr || (R > 0 && (A == nullptr || B == nullptr)))
         return fail(SIR_EINVAL, fn, "NULL buffer");
     if (workspace_bytes < sir::gemm_tn_workspace(R, M, N)) return fail(SIR_EINVAL, fn, "workspace too small");
-    hipError_t err = sir::run_gemm_tn(A, lda, B, ldb, R, (int)M, (int)N, C, ldc, workspace,
+    hipError_t err = sir::run_gemm_tn(A, lda, B, ldb, R, (int)M, (int)N, C, ldc, colsum_a, workspace,
                                       static_cast<hipStream_t>(stream));
     return finish(fn, err, nullptr);
 }

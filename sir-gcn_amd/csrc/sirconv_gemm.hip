@@ -22,6 +22,8 @@
 //   k_gemm_tn     : part[p] = A[rows_p]^T B[rows_p]  (the weight gradients dW_R = dY^T S,
 //                   [dW_Q; dW_K] = [dQ dK]^T X; contraction over the V node rows, split over
 //                   P row ranges), running scales per column of A and of B.
+//                   With csum_part the same pass also sums the columns of A (the bias gradient
+//                   of that linear: db_R = sum dY, db_Q = sum dQ) from the loaded fp32 values.
 //   k_gemm_reduce : C = sum_p part[p] in p order (deterministic).
 // LDS stage image (both kernels): [part hi/lo][k-step 0/1][row][16 halves] — one k-step of 32
 // rows is 1 KiB contiguous, exactly one ds_read_b128 per lane (conflict-free).
@@ -333,8 +335,8 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 template <int WM, int WN, int TMT, int TNT>
 __global__ void __launch_bounds__(64 * WM * WN)
 k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
-          int64_t R, int Mc, int Nc, float* __restrict__ part, int n_mtiles, int n_ntiles,
-          int64_t rows_per_split) {
+          int64_t R, int Mc, int Nc, float* __restrict__ part, float* __restrict__ csum_part,
+          int n_mtiles, int n_ntiles, int64_t rows_per_split) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * TMT * WM, BN = 32 * TNT * WN;
     static_assert(2 * (BM + BN) == NT, "loader mapping: one column slot per thread");
@@ -365,6 +367,10 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     const int m_w = (w / WN) * TMT * 32, n_w = (w % WN) * TNT * 32;
 
     float4 xv[4];
+    // bias gradient of the same linear (column sums of A) rides on the A loads: one partial row
+    // per split, written by the blocks of the first n-tile
+    const bool do_cs = csum_part != nullptr && is_a;
+    float cs = 0.f;
     auto load = [&](int c) {
         const int64_t vc = v_begin + (int64_t)c * KC;
         const float* src = xbase + vc * ldx;                 // wave-uniform chunk base
@@ -408,6 +414,10 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
         hd[0] = hv[0]; hd[1] = hv[1];
         ld[0] = lv[0]; ld[1] = lv[1];
         if (kse == 0) reinterpret_cast<float*>(st + A_BYTES + B_BYTES)[fac_off] = pow2(se - se_old);
+        if (do_cs) {           // column sums of A from the fp32 values, in row order
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { cs += xv[j].x; cs += xv[j].y; cs += xv[j].z; cs += xv[j].w; }
+        }
         return se != se_old;
     };
 
@@ -502,6 +512,10 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
             }
         }
     }
+    if (do_cs && tile % n_ntiles == 0) {
+        const float other = __shfl_xor(cs, 1);          // the partner thread holds rows 16..31 of each chunk
+        if (kse == 0 && col_ok) csum_part[(int64_t)p * Mc + m0 + cl] = cs + other;
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -561,21 +575,25 @@ int gemm_tn_splits(int64_t R, int64_t Mc, int64_t Nc) {
 }
 
 int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc) {
-    return (int64_t)gemm_tn_splits(R, Mc, Nc) * Mc * Nc * 4;
+    return (int64_t)gemm_tn_splits(R, Mc, Nc) * (Mc * Nc + Mc) * 4;    // partial products + column sums
 }
 
 hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
-                       float* C, int64_t ldc, void* workspace, hipStream_t st) {
+                       float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st) {
     if (Mc == 0 || Nc == 0) return hipSuccess;
     const int P = gemm_tn_splits(R, Mc, Nc);
     const int64_t rps = (R + P - 1) / P;
     const int nmt = (Mc + 255) / 256, nnt = (Nc + 255) / 256;
     float* part = static_cast<float*>(workspace);
+    float* cpart = colsum != nullptr ? part + (int64_t)P * Mc * Nc : nullptr;
     hipLaunchKernelGGL((k_gemm_tn<4, 4, 2, 2>), dim3((unsigned)(P * nmt * nnt)), dim3(1024), 0, st,
-                       A, lda, B, ldb, R, Mc, Nc, part, nmt, nnt, rps);
+                       A, lda, B, ldb, R, Mc, Nc, part, cpart, nmt, nnt, rps);
     const int64_t count = (int64_t)Mc * Nc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
                        part, P, count, Nc, C, ldc);
+    if (colsum != nullptr)      // colsum = sum_p cpart[p] in split order
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((Mc + 255) / 256)), dim3(256), 0, st,
+                           cpart, P, (int64_t)Mc, Mc, colsum, (int64_t)0);
     return hipGetLastError();
 }
 

@@ -96,6 +96,6 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
                        const float* bias, float* C, int64_t ldc, hipStream_t st);
 int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc);
 hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
-                       float* C, int64_t ldc, void* workspace, hipStream_t st);
+                       float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st);
 
 }  // namespace sir

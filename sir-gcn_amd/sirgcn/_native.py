@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16 = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
 _P, _I64, _I, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
@@ -41,7 +41,7 @@ SIGNATURES = {
     "sir_gemm_pack": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _P, _P]),
     "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
-    "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _P]),
+    "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
@@ -331,18 +331,21 @@ def gemm_nt(A, packed, bias=None, out=None):
     return out
 
 
-def gemm_tn(A, B, out=None):
-    """C = A^T B (A [R, M], B [R, N]) on the split-fp16 MFMA kernel (split over row ranges)."""
+def gemm_tn(A, B, out=None, colsum=False):
+    """C = A^T B (A [R, M], B [R, N]) on the split-fp16 MFMA kernel (split over row ranges).
+    With ``colsum=True`` returns ``(C, A.sum(0))``: the column sums (a linear's bias gradient)
+    come out of the same pass over A."""
     lib = load()
     R, M = A.shape
     N = B.shape[1]
     assert B.shape[0] == R and A.stride(1) == 1 and B.stride(1) == 1
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    cs = torch.empty((M,), dtype=torch.float32, device=A.device) if colsum else None
     ws_bytes = lib.sir_gemm_tn_workspace(R, M, N)
     ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=A.device)
     with _Timed("sir_gemm_tn", A.device, 2 * R * M * N):
         rc = lib.sir_gemm_tn(_ptr(A), A.stride(0), _ptr(B), B.stride(0), R, M, N, _ptr(out), out.stride(0),
-                             _ptr(ws), ws.numel(), _stream(A.device))
+                             _ptr(cs), _ptr(ws), ws.numel(), _stream(A.device))
     _check(rc, lib)
-    return out
+    return (out, cs) if colsum else out

@@ -112,9 +112,20 @@ _tn = linalg.mm_tn
 
 def _bias_grad(G):
     """sum over rows (native deterministic column sum when the layout allows)."""
-    if G.shape[1] % 4 == 0 and G.stride(1) == 1 and G.stride(0) % 4 == 0 and G.data_ptr() % 16 == 0:
+    if (G.is_cuda and G.shape[1] % 4 == 0 and G.stride(1) == 1 and G.stride(0) % 4 == 0
+            and G.data_ptr() % 16 == 0):
         return _native.col_sum(G)
     return G.sum(0)
+
+
+def _weight_and_bias_grad(G, X, need_w, need_b):
+    """nn.Linear autograd: dW = G^T X and db = sum_rows G.  When both are needed the column sums
+    come out of the weight-gradient GEMM's own pass over G (``sir_gemm_tn`` colsum_a)."""
+    if need_w and need_b:
+        return _tn(G, X, colsum=True)
+    if need_w:
+        return _tn(G, X), None
+    return None, (_bias_grad(G) if need_b else None)
 
 
 class SIRConvFunction(torch.autograd.Function):
@@ -154,8 +165,7 @@ class SIRConvFunction(torch.autograd.Function):
         V = X.shape[0]
         dY = dY.contiguous()
         G = linalg.mm_w(dY, W_R)
-        dW_R = _tn(dY, S) if ctx.needs_input_grad[4] else None
-        db_R = _bias_grad(dY) if ctx.has_br and ctx.needs_input_grad[5] else None
+        dW_R, db_R = _weight_and_bias_grad(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
         in_norm, out_norm = plan.norms(agg)
         partial = _partial(plan, H, X.device)
         Gm = torch.empty((V, H), device=X.device, dtype=torch.float32) if agg == "mean" else None
@@ -171,11 +181,14 @@ class SIRConvFunction(torch.autograd.Function):
         _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
                                  agg, act, slope, dQK[:, H:], partial, mask)
         dX = linalg.mm_w(dQK, W_cat) if ctx.needs_input_grad[0] else None
-        dW_Q = dW_K = None
+        dW_Q = dW_K = db_Q = None
+        need_bq = ctx.has_bq and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
-            dW = _tn(dQK, X)
+            dW, cs = _weight_and_bias_grad(dQK, X, True, need_bq)     # cs: column sums of [dQ dK]
             dW_Q, dW_K = dW[:H], dW[H:]
-        db_Q = _bias_grad(dQK[:, :H]) if ctx.has_bq and ctx.needs_input_grad[2] else None
+            db_Q = cs[:H] if need_bq else None
+        elif need_bq:
+            db_Q = _bias_grad(dQK[:, :H])
         return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None
 
 

@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native, linalg
-from .conv import _tn, activation_code
+from .conv import _tn, _weight_and_bias_grad, activation_code
 from .graph import DEFAULT_CHUNK, build_plans_native, build_row_csr
 
 
@@ -214,12 +214,6 @@ def _workspace(plan, H, device):
     return torch.empty((max(n, 1) * H,), device=device, dtype=torch.float32) if n else None
 
 
-def _colsum(G):
-    if G.is_cuda and G.shape[1] % 4 == 0 and G.stride(1) == 1 and G.stride(0) % 4 == 0 and G.data_ptr() % 16 == 0:
-        return _native.col_sum(G)
-    return G.sum(0)
-
-
 class DistSIRConvFunction(torch.autograd.Function):
     """One rank's share of the whole layer, hand-scheduled around the two exchanges.
 
@@ -287,11 +281,9 @@ class DistSIRConvFunction(torch.autograd.Function):
         if agg != "mean":     # overlaps the reverse exchange
             backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, None, partial,
                                      mask)
-        dW_R = _tn(dY, S) if ctx.needs_input_grad[4] else None
-        db_R = _colsum(dY) if ctx.has_br and ctx.needs_input_grad[5] else None
+        dW_R, db_R = _weight_and_bias_grad(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
         dX = linalg.mm_w(dQ, W_Q) if ctx.needs_input_grad[0] else None
-        dW_Q = _tn(dQ, X) if ctx.needs_input_grad[1] else None
-        db_Q = _colsum(dQ) if ctx.has_bq and ctx.needs_input_grad[2] else None
+        dW_Q, db_Q = _weight_and_bias_grad(dQ, X, ctx.needs_input_grad[1], ctx.has_bq and ctx.needs_input_grad[2])
         if work is not None:
             work.wait()
         dK = dK_ext[:n]

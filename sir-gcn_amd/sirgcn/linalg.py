@@ -40,12 +40,14 @@ def mm_w(A, W):
     return torch.mm(A, W)
 
 
-def mm_tn(A, B):
-    """A^T B for tall A [R, M], B [R, N] (the weight gradients)."""
+def mm_tn(A, B, colsum=False):
+    """A^T B for tall A [R, M], B [R, N] (the weight gradients); with ``colsum`` also A.sum(0)
+    (the bias gradient of the same linear), from the same pass: returns (A^T B, colsum)."""
     if (USE_NATIVE and A.is_cuda and B.is_cuda and A.dtype == torch.float32 and B.dtype == torch.float32
             and A.dim() == 2 and B.dim() == 2 and A.stride(1) == 1 and B.stride(1) == 1):
-        return _native.gemm_tn(A, B)
-    return _tn_torch(A, B)
+        return _native.gemm_tn(A, B, colsum=colsum)
+    out = _tn_torch(A, B)
+    return (out, A.sum(0)) if colsum else out
 
 
 def _tn_torch(A, B):

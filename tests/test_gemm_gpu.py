@@ -101,6 +101,24 @@ def test_gemm_tn_vs_fp64(R, M, N):
     _check(C, A.double().t(), B.double(), A.t() @ B, None, f"tn R={R} M={M} N={N}")
 
 
+@pytest.mark.parametrize("R,M,N", [(0, 8, 4), (1, 256, 256), (1000, 512, 256), (70001, 256, 256), (4099, 300, 100)])
+def test_gemm_tn_column_sums(R, M, N):
+    """colsum_a: the bias gradient (sum over rows of A) from the weight-gradient pass, vs fp64 with
+    torch's fp32 column sum as the yardstick; the product must be unchanged by asking for it."""
+    g = torch.Generator(device=DEV).manual_seed(R + M)
+    A = torch.randn(R, M, device=DEV, generator=g)
+    B = torch.randn(R, N, device=DEV, generator=g)
+    C, cs = _native.gemm_tn(A, B, colsum=True)
+    assert torch.equal(C, _native.gemm_tn(A, B))
+    if R == 0:
+        assert torch.all(cs == 0)
+        return
+    ref64 = A.double().sum(0)
+    e_ours, e_torch = _rel(cs.double(), ref64), _rel(A.sum(0).double(), ref64)
+    assert e_ours <= max(2 * e_torch, 1e-6), (e_ours, e_torch)
+    assert torch.equal(cs, _native.gemm_tn(A, B, colsum=True)[1]), "column sums must be deterministic"
+
+
 def test_gemm_tn_dynamic_range_strided_and_deterministic():
     g = torch.Generator(device=DEV).manual_seed(9)
     R = 50000

@@ -76,7 +76,7 @@ def main():
             A, B = v
             C = outs.setdefault((n, s), torch.empty(A.shape[1], B.shape[1], device=dev))
             rc = lib.sir_gemm_tn(P(A), A.stride(0), P(B), B.stride(0), V, A.shape[1], B.shape[1], P(C),
-                                 C.stride(0), P(ws), ws.numel(), st)
+                                 C.stride(0), None, P(ws), ws.numel(), st)
         assert rc == 0, lib.sir_last_error()
 
     times = {(n, s): [] for n, _ in libs for s in shapes}
