@@ -390,6 +390,10 @@ __device__ __forceinline__ float sel_mask(uint64_t m, float t, float slope) {
     else return lane_select(m, t * slope, t);
 }
 
+#ifndef SIR_DQ_VMASK
+#define SIR_DQ_VMASK 1          // dQ pass: mask words by one vector load + v_readlane (1; -9% sum, -19% sym) or scalar loads (0)
+#endif
+
 template <int MODE, int ACT, int AGG, int NV, int UU>
 __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, const int* __restrict__ perm,
                                            const float* __restrict__ G, int64_t ldg,
@@ -410,10 +414,25 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
         }
     }
     uint64_t wd[UU][NW];
+    if constexpr (SIR_DQ_VMASK && MODE == MODE_BWD_DST && UU * NW <= 64) {
+        // the batch's UU*NW words are contiguous: one 8-B vector load per lane, then broadcast
+        // each word to SGPRs (v_readlane) for the lane-mask selects
+        const uint64_t mv = (lane < UU * NW) ? mask[(int64_t)e * NW + lane] : 0ull;
+        const int mlo = (int)(uint32_t)mv, mhi = (int)(uint32_t)(mv >> 32);
+#pragma unroll
+        for (int i = 0; i < UU; ++i)
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(mlo, i * NW + k);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(mhi, i * NW + k);
+                wd[i][k] = ((uint64_t)hi << 32) | lo;
+            }
+    } else {
 #pragma unroll
     for (int i = 0; i < UU; ++i)
 #pragma unroll
         for (int k = 0; k < NW; ++k) wd[i][k] = uniform64(mask[(int64_t)p[i] * NW + k]);
+    }
     float cf[UU];
     if constexpr (AGG == AGG_SYM) {
 #pragma unroll

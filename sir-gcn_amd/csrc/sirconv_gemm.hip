@@ -38,6 +38,9 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 constexpr int KC = 32;          // contraction elements per LDS stage (two k16 MFMA steps)
 
+#ifndef SIR_ABL_TN
+#define SIR_ABL_TN 0            // timing-only ablation: TN loads dropped (zero-record descriptors)
+#endif
 #ifndef SIR_NT_EPI
 #define SIR_NT_EPI 1            // 1: NT epilogue through LDS, full-row stores; 0: fragment stores
 #endif
@@ -376,12 +379,12 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
         const float* src = xbase + vc * ldx;                 // wave-uniform chunk base
         float x[16];
         if (vc + KC <= v_end) {
-            const rsrc_t rs = mk_rsrc(src, (uint32_t)(KC * ldx * 4));
+            const rsrc_t rs = mk_rsrc(src, SIR_ABL_TN ? 0u : (uint32_t)(KC * ldx * 4));
 #pragma unroll
             for (int j = 0; j < 16; ++j)
                 x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, xoff * 4, j * ldx * 4, 0));
         } else {   // tail chunk: rows past v_end fail the range check and read as 0
-            const rsrc_t rs = mk_rsrc(src, (uint32_t)((v_end - vc) * ldx * 4));
+            const rsrc_t rs = mk_rsrc(src, SIR_ABL_TN ? 0u : (uint32_t)((v_end - vc) * ldx * 4));
             int o = xoff * 4;
             asm volatile("" : "+v"(o));      // keep the 16 offsets out of the loop preheader
 #pragma unroll
