@@ -41,6 +41,12 @@ constexpr int KC = 32;          // contraction elements per LDS stage (two k16 M
 #ifndef SIR_ABL_TN
 #define SIR_ABL_TN 0            // timing-only ablation: TN loads dropped (zero-record descriptors)
 #endif
+#ifndef SIR_ABL_NT
+#define SIR_ABL_NT 0            // timing-only ablations: 1 = NT data loads dropped, 2 = NT C stores dropped
+#endif
+#ifndef SIR_NT_PF
+#define SIR_NT_PF 2             // NT chunks in flight in registers ahead of the LDS stage (1 or 2)
+#endif
 #ifndef SIR_NT_EPI
 #define SIR_NT_EPI 1            // 1: NT epilogue through LDS, full-row stores; 0: fragment stores
 #endif
@@ -130,7 +136,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
     // loader role: buffer loads off wave-uniform bases (rows past M read as 0 by the range check)
     const int rho = t / TPR, kp = t % TPR;
     const int64_t rows_here = (M - d0 < BD) ? M - d0 : BD;
-    const rsrc_t arsrc = mk_rsrc(A + d0 * lda, (uint32_t)(rows_here * lda * 4));
+    const rsrc_t arsrc = mk_rsrc(A + d0 * lda, (SIR_ABL_NT & 1) ? 0u : (uint32_t)(rows_here * lda * 4));
     const int aoff = (rho * (int)lda + kp * FPT) * 4;
     const rsrc_t wrsrc = mk_rsrc(Wp, (uint32_t)((int64_t)nc * Npad * 128));
     int woff[WPT];
@@ -146,29 +152,35 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
     const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
     const int d_w = (w / WF) * TDT * 32, f_w = (w % WF) * TFT * 32;
 
-    float4 dv[FPT / 4];
+    // register sets for data chunks in flight: chunk j lands in set j % SIR_NT_PF.  The packed
+    // weights come from L2 (one set, loaded one chunk ahead).
+    float4 dv[2][FPT / 4];
     u4v wv[WPT];
 
-    auto load = [&](int c) {
+    auto load_a = [&](int set, int c) {
 #pragma unroll
         for (int i = 0; i < FPT / 4; ++i) {
             const int k = c * KC + kp * FPT + 4 * i;
             const u4v u = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff + 16 * i, c * KC * 4, 0);
-            dv[i] = (k < K) ? make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
-                                          __uint_as_float(u.w))
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            dv[set][i] = (k < K) ? make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                                               __uint_as_float(u.w))
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+    };
+    auto load_w = [&](int c) {
 #pragma unroll
         for (int i = 0; i < WPT; ++i)
             wv[i] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, woff[i], c * Npad * 128, 0);
     };
+    auto load = [&](int set, int c) { load_a(set, c); load_w(c); };
 
-    // split the loaded chunk into stage `buf`; returns whether this row's scale changed
-    auto store = [&](int buf) -> bool {
+    // split the loaded chunk of register set `set` into stage `buf`; returns whether this row's
+    // scale changed
+    auto store = [&](int set, int buf) -> bool {
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
-        for (int i = 0; i < FPT / 4; ++i) m = fmax4(m, dv[i]);
+        for (int i = 0; i < FPT / 4; ++i) m = fmax4(m, dv[set][i]);
         if (TPR > 1) m = fmaxf(m, __shfl_xor(m, 1));
         if (TPR > 2) m = fmaxf(m, __shfl_xor(m, 2));
         const int e_new = max(e_run, bexp(m));
@@ -180,7 +192,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
         for (int j = 0; j < FPT; j += 8) {
             const int kl = kp * FPT + j, ks = kl >> 4, pos = kl & 15;
             h8 hv, lv;
-            split8(dv[j / 4], dv[j / 4 + 1], s, hv, lv);
+            split8(dv[set][j / 4], dv[set][j / 4 + 1], s, hv, lv);
             *reinterpret_cast<h8*>(st + ((0 * 2 + ks) * BD + rho) * 32 + pos * 2) = hv;
             *reinterpret_cast<h8*>(st + ((1 * 2 + ks) * BD + rho) * 32 + pos * 2) = lv;
         }
@@ -199,14 +211,8 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
 
-    load(0);
-    store(0);
-    int any = 0;
-    __syncthreads();
-    for (int c = 0; c < nc; ++c) {
-        const int buf = c & 1;
-        const bool more = c + 1 < nc;
-        if (more) load(c + 1);
+    // MFMAs of the chunk in stage `buf` (rescaling the rows whose scale rose first)
+    auto compute = [&](int buf, int any) {
         const char* st = lds + buf * STAGE;
         if (any) {
             const float* fac = reinterpret_cast<const float*>(st + D_BYTES + W_BYTES);
@@ -245,10 +251,43 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
                 for (int b = 0; b < TDT; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][1], df[b][0], acc[a][b], 0, 0, 0);
         }
+    };
+
+    load(0, 0);
+    store(0, 0);
+    int any = 0;
+#if SIR_NT_PF == 2
+    // two data chunks in flight: at step c the registers hold chunks c+1 (set (c+1)&1) and c+2
+    // (set c&1); chunk c+1 is split into the free stage, then its set is refilled with chunk c+3
+    if (nc > 1) load_a(1, 1);
+    if (nc > 2) load_a(0, 2);
+    __syncthreads();
+    auto step = [&](int c, int set) {             // set = (c + 1) & 1, static after inlining
+        if (c + 1 < nc) load_w(c + 1);
+        compute(c & 1, any);
         bool changed = false;
-        if (more) changed = store(buf ^ 1);
+        if (c + 1 < nc) {
+            changed = store(set, (c & 1) ^ 1);
+            if (c + 3 < nc) load_a(set, c + 3);
+        }
+        any = __syncthreads_or(changed);
+    };
+    for (int c = 0; c < nc; c += 2) {
+        step(c, 1);
+        if (c + 1 < nc) step(c + 1, 0);
+    }
+#else
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+        const int buf = c & 1;
+        const bool more = c + 1 < nc;
+        if (more) load(0, c + 1);
+        compute(buf, any);
+        bool changed = false;
+        if (more) changed = store(0, buf ^ 1);
         any = __syncthreads_or(changed);
     }
+#endif
 
     // epilogue: C[m][n] = acc * 2^-se(m) * inv_t[n] + bias[n]
 #if SIR_NT_EPI == 1
@@ -295,7 +334,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
             const int64_t m = d0 + (row >> 5) * (TDT * 32) + 32 * b + (row & 31);
             const int n = f0 + c4 * 4;
             const float4 o = *reinterpret_cast<const float4*>(lds + row * PITCH + c4 * 16);
-            if (m < M && n < N) *reinterpret_cast<float4*>(C + m * ldc + n) = o;
+            if (!(SIR_ABL_NT & 2) && m < M && n < N) *reinterpret_cast<float4*>(C + m * ldc + n) = o;
         }
         __syncthreads();
     }
