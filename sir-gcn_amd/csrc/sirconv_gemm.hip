@@ -8,9 +8,10 @@
 // accumulator: three v_mfma_f32_32x32x16_f16 per 32x32x16 step and ~22 significant bits per
 // operand — an error comparable to an fp32 GEMM's own rounding (tests/test_gemm_gpu.py holds
 // it to <= 2x torch fp32's error against fp64).  The scale of a data row is not known before
-// its last k-chunk has been read, so it is a RUNNING maximum: when a chunk raises a row's
-// maximum into a higher binade, the accumulators of that row are multiplied by the (exact,
-// power of two) ratio of the new and old scales before the chunk is added.
+// its last k-chunk has been read, so it is a RUNNING scale: when a chunk's values would leave
+// the fp16 range under the current scale, the scale is reset (with 2^SIR_HR headroom, see
+// next_se) and the accumulators of that row are multiplied by the (exact, power of two) ratio of
+// the new and old scales before the chunk is added.
 //
 // Kernels
 //   k_pack_weight : B[n][k] (= W or W^T) -> fp16 hi/lo in MFMA fragment order + 1/scale per n
@@ -44,6 +45,9 @@ constexpr int KC = 32;          // contraction elements per LDS stage (two k16 M
 #ifndef SIR_ABL_NT
 #define SIR_ABL_NT 0            // timing-only ablations: 1 = NT data loads dropped, 2 = NT C stores dropped
 #endif
+#ifndef SIR_HR
+#define SIR_HR 8                // headroom bits of a reset running scale (see next_se)
+#endif
 #ifndef SIR_NT_PF
 #define SIR_NT_PF 2             // NT chunks in flight in registers ahead of the LDS stage (1 or 2)
 #endif
@@ -55,6 +59,19 @@ constexpr int KC = 32;          // contraction elements per LDS stage (two k16 M
 __device__ inline int bexp(float m) { return (int)((__float_as_uint(m) >> 23) & 255u) - 126; }
 // scale exponent for a running binade e: |x| * 2^(15 - e) < 2^15, clamped to a normal float
 __device__ inline int scale_exp(int e) { int s = 15 - e; return s > 126 ? 126 : s; }
+// Running scale of a data row / column with hysteresis: a chunk whose binade e_c still fits
+// (|x| * 2^se < 2^15) keeps the current scale; otherwise the scale is reset with SIR_HR bits of
+// headroom, so a row's scale changes (and its accumulators are rescaled) only when a chunk
+// exceeds the row's earlier maximum by more than 2^SIR_HR — once per row in practice, at its
+// first chunk.  Scaled values stay in [2^-14, 2^15) over >= 20 binades below the maximum, where
+// the fp16 hi/lo pair is exact to ~22 bits; the split is scale-invariant there, so the result
+// does not depend on which power-of-two scale was in force.
+constexpr int SE_INIT = 127;    // no chunk seen yet
+__device__ inline int next_se(int se_old, int e_c) {
+    if (e_c + se_old <= 15) return se_old;
+    const int s = 15 - SIR_HR - e_c;
+    return s > 126 ? 126 : s;
+}
 __device__ inline float pow2(int e) { e = e < -126 ? -126 : (e > 127 ? 127 : e); return __uint_as_float((uint32_t)(e + 127) << 23); }
 
 // hi/lo fp16 split of 8 floats scaled by s (exact power of two)
@@ -110,7 +127,10 @@ k_pack_weight(const float* __restrict__ W, int64_t ldw, int N, int K, int trans,
 
 // ------------------------------------------------------------------------------------------
 // NT GEMM.  WD x WF waves, each TDT x TFT tiles of 32 data rows x 32 features.
-template <int WD, int WF, int TDT, int TFT>
+// KFULL: K is a multiple of KC, so no column past K is ever loaded (no per-element select: the
+// compiler turns that select into exec-masked branches with a vmcnt(0) inside, draining the
+// prefetch queue every chunk).
+template <int WD, int WF, int TDT, int TFT, bool KFULL>
 __global__ void __launch_bounds__(64 * WD * WF)
 k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
           const u4v* __restrict__ Wp, int Npad, const float* __restrict__ inv_t,
@@ -146,7 +166,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
         const int part = p / (BF * 4), ks = (p / (BF * 2)) & 1, nl = (p >> 1) % BF, q = p & 1;
         woff[i] = (((part * 2 + ks) * Npad + f0 + nl) * 2 + q) * 16;
     }
-    int e_run = -126;                       // running binade of this data row
+    int se_run = SE_INIT;                   // running scale exponent of this data row
 
     // compute role
     const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
@@ -162,7 +182,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
         for (int i = 0; i < FPT / 4; ++i) {
             const int k = c * KC + kp * FPT + 4 * i;
             const u4v u = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff + 16 * i, c * KC * 4, 0);
-            dv[set][i] = (k < K) ? make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+            dv[set][i] = (KFULL || k < K) ? make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
                                                __uint_as_float(u.w))
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -174,18 +194,17 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
     };
     auto load = [&](int set, int c) { load_a(set, c); load_w(c); };
 
-    // split the loaded chunk of register set `set` into stage `buf`; returns whether this row's
-    // scale changed
-    auto store = [&](int set, int buf) -> bool {
+    // split the loaded chunk of register set `set` into stage `buf` (with the row's rescale
+    // factor; 1 for the first chunk, whose accumulators are still zero)
+    auto store = [&](int set, int buf, bool first = false) {
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
         for (int i = 0; i < FPT / 4; ++i) m = fmax4(m, dv[set][i]);
         if (TPR > 1) m = fmaxf(m, __shfl_xor(m, 1));
         if (TPR > 2) m = fmaxf(m, __shfl_xor(m, 2));
-        const int e_new = max(e_run, bexp(m));
-        const int se_old = scale_exp(e_run), se = scale_exp(e_new);
-        e_run = e_new;
+        const int se_old = se_run, se = next_se(se_old, bexp(m));
+        se_run = se;
         const float s = pow2(se);
         // k_local = kp*FPT + j -> ks = k_local / 16, position k_local % 16
 #pragma unroll
@@ -196,11 +215,11 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
             *reinterpret_cast<h8*>(st + ((0 * 2 + ks) * BD + rho) * 32 + pos * 2) = hv;
             *reinterpret_cast<h8*>(st + ((1 * 2 + ks) * BD + rho) * 32 + pos * 2) = lv;
         }
-        if (kp == 0) reinterpret_cast<float*>(st + D_BYTES + W_BYTES)[rho] = pow2(se - se_old);
+        // every loader thread of the row holds the same factor: a branch-free (same-value) store
+        reinterpret_cast<float*>(st + D_BYTES + W_BYTES)[rho] = first ? 1.f : pow2(se - se_old);
 #pragma unroll
         for (int i = 0; i < WPT; ++i)
             *reinterpret_cast<u4v*>(st + D_BYTES + (t + i * NT) * 16) = wv[i];
-        return se != se_old;
     };
 
     f16v acc[TFT][TDT];
@@ -211,18 +230,23 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
 
-    // MFMAs of the chunk in stage `buf` (rescaling the rows whose scale rose first)
-    auto compute = [&](int buf, int any) {
-        const char* st = lds + buf * STAGE;
-        if (any) {
-            const float* fac = reinterpret_cast<const float*>(st + D_BYTES + W_BYTES);
+    // rows whose scale rose with the chunk in stage `buf` carry a factor != 1: each wave checks
+    // its own rows (a ballot, no block-wide reduction) and rescales only when one changed
+    auto rescale = [&](int buf) {
+        const float* fac = reinterpret_cast<const float*>(lds + buf * STAGE + D_BYTES + W_BYTES);
+        float f[TDT];
+        bool ch = false;
 #pragma unroll
-            for (int b = 0; b < TDT; ++b) {
-                const float f = fac[d_w + 32 * b + r];
+        for (int b = 0; b < TDT; ++b) { f[b] = fac[d_w + 32 * b + r]; ch |= f[b] != 1.f; }
+        if (__builtin_amdgcn_ballot_w64(ch) != 0) {
 #pragma unroll
-                for (int a = 0; a < TFT; ++a) acc[a][b] *= f;
-            }
+            for (int b = 0; b < TDT; ++b)
+#pragma unroll
+                for (int a = 0; a < TFT; ++a) acc[a][b] *= f[b];
         }
+    };
+    auto mfma = [&](int buf) {
+        const char* st = lds + buf * STAGE;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             h8 wf[TFT][2], df[TDT][2];
@@ -252,29 +276,90 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][1], df[b][0], acc[a][b], 0, 0, 0);
         }
     };
+    auto compute = [&](int buf) {
+        rescale(buf);
+        mfma(buf);
+    };
 
     load(0, 0);
-    store(0, 0);
-    int any = 0;
+    store(0, 0, true);
 #if SIR_NT_PF == 2
     // two data chunks in flight: at step c the registers hold chunks c+1 (set (c+1)&1) and c+2
-    // (set c&1); chunk c+1 is split into the free stage, then its set is refilled with chunk c+3
-    if (nc > 1) load_a(1, 1);
-    if (nc > 2) load_a(0, 2);
-    __syncthreads();
-    auto step = [&](int c, int set) {             // set = (c + 1) & 1, static after inlining
-        if (c + 1 < nc) load_w(c + 1);
-        compute(c & 1, any);
-        bool changed = false;
+    // (set c&1); chunk c+1 is split into the free stage, then W(c+2) and A(c+3) (into the freed
+    // set) are issued in that order, so that the wait for A(c+1), W(c+1) leaves A(c+2) in flight.
+    // The steady-state steps (and the path into them) carry no conditional loads: a load skipped
+    // on one path makes the compiler's wait-count merge assume the worst and drain the queue
+    // (vmcnt(0)) every step.
+    auto step_full = [&](int c, int set) {        // set = (c + 1) & 1, static; needs c + 3 < nc
+        compute(c & 1);
+        store(set, (c & 1) ^ 1);
+        load_w(c + 2);
+        load_a(set, c + 3);
+        __syncthreads();
+    };
+    auto step_tail = [&](int c, int set) {
+        compute(c & 1);
         if (c + 1 < nc) {
-            changed = store(set, (c & 1) ^ 1);
+            store(set, (c & 1) ^ 1);
+            if (c + 2 < nc) load_w(c + 2);
             if (c + 3 < nc) load_a(set, c + 3);
         }
-        any = __syncthreads_or(changed);
+        __syncthreads();
     };
-    for (int c = 0; c < nc; c += 2) {
-        step(c, 1);
-        if (c + 1 < nc) step(c + 1, 0);
+    int c = 0;
+    if (nc > 4) {
+        load_a(1, 1);
+        load_w(1);
+        load_a(0, 2);
+        __syncthreads();
+        for (; c + 4 < nc; c += 2) {
+            step_full(c, 1);
+            step_full(c + 1, 0);
+        }
+    } else {
+        if (nc > 1) { load_a(1, 1); load_w(1); }
+        if (nc > 2) load_a(0, 2);
+        __syncthreads();
+    }
+    for (; c < nc; c += 2) {
+        step_tail(c, 1);
+        if (c + 1 < nc) step_tail(c + 1, 0);
+    }
+#elif SIR_NT_PF == 3
+    // two data chunks in flight, and the split of chunk c+1 into the free stage happens BEFORE
+    // the MFMAs of chunk c (the free stage was last read before the previous barrier), in one
+    // basic block with them so the scheduler can interleave its VALU/LDS work with the MFMAs.
+    // Issue order per step: W(c+2) then A(c+3), so the next step's wait for A(c+2), W(c+2)
+    // leaves A(c+3) in flight.
+    if (nc > 1) { load_a(1, 1); load_w(1); }
+    if (nc > 2) load_a(0, 2);
+    __syncthreads();
+    auto step_full = [&](int c, int set) {        // requires c + 3 < nc
+        const int buf = c & 1;
+        rescale(buf);
+        store(set, buf ^ 1);
+        load_w(c + 2);
+        load_a(set, c + 3);
+        mfma(buf);
+        __syncthreads();
+    };
+    auto step_tail = [&](int c, int set) {
+        const int buf = c & 1;
+        rescale(buf);
+        if (c + 1 < nc) store(set, buf ^ 1);
+        if (c + 2 < nc) load_w(c + 2);
+        if (c + 3 < nc) load_a(set, c + 3);
+        mfma(buf);
+        __syncthreads();
+    };
+    int c = 0;
+    for (; c + 4 < nc; c += 2) {
+        step_full(c, 1);
+        step_full(c + 1, 0);
+    }
+    for (; c < nc; c += 2) {
+        step_tail(c, 1);
+        if (c + 1 < nc) step_tail(c + 1, 0);
     }
 #else
     __syncthreads();
@@ -282,10 +367,9 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
         const int buf = c & 1;
         const bool more = c + 1 < nc;
         if (more) load(0, c + 1);
-        compute(buf, any);
-        bool changed = false;
-        if (more) changed = store(0, buf ^ 1);
-        any = __syncthreads_or(changed);
+        compute(buf);
+        if (more) store(0, buf ^ 1);
+        __syncthreads();
     }
 #endif
 
@@ -300,7 +384,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
     static_assert(RR * PITCH <= SC_OFF, "epilogue image overlaps the scale row");
     static_assert((RR * BF / 4) % NT == 0, "epilogue copy mapping");
     float* sc = reinterpret_cast<float*>(lds + SC_OFF);
-    if (kp == 0) sc[rho] = pow2(-scale_exp(e_run));
+    if (kp == 0) sc[rho] = pow2(-se_run);
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < TDT; ++b) {
@@ -341,7 +425,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 }
 #else
     float* sc = reinterpret_cast<float*>(lds);
-    if (kp == 0) sc[rho] = pow2(-scale_exp(e_run));
+    if (kp == 0) sc[rho] = pow2(-se_run);
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < TDT; ++b) {
@@ -403,7 +487,7 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     const int ldx = (int)(is_a ? lda : ldb);
     const int xoff = 16 * kse * ldx + (is_a ? m0 : n0) + (col_ok ? cl : 0);   // within a chunk
     const int img = is_a ? 0 : A_BYTES, rows_img = is_a ? BM : BN, fac_off = is_a ? cl : BM + cl;
-    int e_run = -126;
+    int se_run = SE_INIT;
 
     const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
     const int m_w = (w / WN) * TMT * 32, n_w = (w % WN) * TNT * 32;
@@ -438,15 +522,14 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
             xv[j].w = col_ok ? x[4 * j + 3] : 0.f;
         }
     };
-    auto store = [&](int buf) -> bool {
+    auto store = [&](int buf, bool first = false) -> bool {     // first chunk: factor 1 (acc is zero)
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) m = fmax4(m, xv[j]);
         m = fmaxf(m, __shfl_xor(m, 1));
-        const int e_new = max(e_run, bexp(m));
-        const int se_old = scale_exp(e_run), se = scale_exp(e_new);
-        e_run = e_new;
+        const int se_old = se_run, se = next_se(se_old, bexp(m));
+        se_run = se;
         const float s = pow2(se);
         h8 hv[2], lv[2];
         split8(xv[0], xv[1], s, hv[0], lv[0]);
@@ -455,12 +538,12 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
         h8* ld = reinterpret_cast<h8*>(st + img + ((1 * 2 + kse) * rows_img + cl) * 32);
         hd[0] = hv[0]; hd[1] = hv[1];
         ld[0] = lv[0]; ld[1] = lv[1];
-        if (kse == 0) reinterpret_cast<float*>(st + A_BYTES + B_BYTES)[fac_off] = pow2(se - se_old);
+        if (kse == 0) reinterpret_cast<float*>(st + A_BYTES + B_BYTES)[fac_off] = first ? 1.f : pow2(se - se_old);
         if (do_cs) {           // column sums of A from the fp32 values, in row order
 #pragma unroll
             for (int j = 0; j < 4; ++j) { cs += xv[j].x; cs += xv[j].y; cs += xv[j].z; cs += xv[j].w; }
         }
-        return se != se_old;
+        return !first && se != se_old;
     };
 
     f16v acc[TMT][TNT];
@@ -473,7 +556,7 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
 
     if (nc > 0) {
         load(0);
-        store(0);
+        store(0, true);
     }
     int any = 0;
     __syncthreads();
@@ -536,7 +619,7 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
 
     // epilogue: part[p][m][n] = acc * 2^-se_a(m) * 2^-se_b(n)
     float* sc = reinterpret_cast<float*>(lds);
-    if (kse == 0) sc[fac_off] = pow2(-scale_exp(e_run));
+    if (kse == 0) sc[fac_off] = pow2(-se_run);
     __syncthreads();
     float* out = part + (int64_t)p * Mc * Nc;
 #pragma unroll
@@ -591,18 +674,27 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
     const u4v* wp = static_cast<const u4v*>(packed);
     const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
+    const bool kfull = K % KC == 0;
     if (N > 128) {
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;
         const int64_t nblk = (M + BD - 1) / BD * nft;
-        hipLaunchKernelGGL((k_gemm_nt<2, 4, 4, 2>), dim3((unsigned)nblk), dim3(512), 0, st,
-                           A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+        if (kfull)
+            hipLaunchKernelGGL((k_gemm_nt<2, 4, 4, 2, true>), dim3((unsigned)nblk), dim3(512), 0, st,
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+        else
+            hipLaunchKernelGGL((k_gemm_nt<2, 4, 4, 2, false>), dim3((unsigned)nblk), dim3(512), 0, st,
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
     } else {
         constexpr int BD = 256, BF = 128;
         const int nft = (N + BF - 1) / BF;
         const int64_t nblk = (M + BD - 1) / BD * nft;
-        hipLaunchKernelGGL((k_gemm_nt<4, 2, 2, 2>), dim3((unsigned)nblk), dim3(512), 0, st,
-                           A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+        if (kfull)
+            hipLaunchKernelGGL((k_gemm_nt<4, 2, 2, 2, true>), dim3((unsigned)nblk), dim3(512), 0, st,
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+        else
+            hipLaunchKernelGGL((k_gemm_nt<4, 2, 2, 2, false>), dim3((unsigned)nblk), dim3(512), 0, st,
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
     }
     return hipGetLastError();
 }

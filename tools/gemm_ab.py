@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--H", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--only", default=None, help="run only the shapes whose name starts with this")
     a = ap.parse_args()
     V, H = a.V, a.H
     dev = "cuda"
@@ -61,6 +62,8 @@ def main():
         "dWR tn": (X, X),
         "dW  tn": (D2, X),
     }
+    if a.only:
+        shapes = {k: v for k, v in shapes.items() if k.startswith(a.only)}
     packs = {(n, s): pack(lib, v[1], v[2]) for n, lib in libs for s, v in shapes.items() if len(v) == 4}
     outs = {}
     ws = torch.empty(max(lib.sir_gemm_tn_workspace(V, 2 * H, H) for _, lib in libs), dtype=torch.uint8, device=dev)
