@@ -26,8 +26,8 @@
 //                   With csum_part the same pass also sums the columns of A (the bias gradient
 //                   of that linear: db_R = sum dY, db_Q = sum dQ) from the loaded fp32 values.
 //   k_gemm_reduce : C = sum_p part[p] in p order (deterministic).
-// LDS stage image (both kernels): [part hi/lo][k-step 0/1][row][16 halves] — one k-step of 32
-// rows is 1 KiB contiguous, exactly one ds_read_b128 per lane (conflict-free).
+// LDS stage image (both kernels): [part hi/lo][k-step 0/1][rows in fimg order] — one k-step of
+// 32 rows is 1 KiB contiguous, exactly one ds_read_b128 per lane, in lane order (conflict-free).
 #include "sirconv_internal.h"
 
 namespace sir {
@@ -82,6 +82,13 @@ __device__ inline void split8(float4 a, float4 b, float s, h8& hi, h8& lo) {
 }
 #undef SIR_SPLIT1
 
+// Fragment image of one LDS plane (and of the packed weights): the 16 halves of a row's k16
+// step are two 16-byte pieces h = 0, 1; piece (row, h) sits at byte
+//   (row / 32) * 1024 + h * 512 + (row % 32) * 16
+// so the 64 lanes of an MFMA operand read (lane = h * 32 + row % 32) fetch 1 KiB in lane order:
+// every 16-lane group of a ds_read_b128 covers 256 contiguous bytes (no bank conflict).
+__host__ __device__ constexpr int fimg(int row, int h) { return ((row >> 5) << 10) + (h << 9) + ((row & 31) << 4); }
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 // raw buffer resource over [p, p + bytes): out-of-range loads return 0 (gfx9 word3 0x00020000)
 __device__ inline rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
@@ -101,7 +108,7 @@ __device__ inline int xcd_remap(int bid, int nblk) {
 
 // ------------------------------------------------------------------------------------------
 // weight packing: one block of 64 threads per feature n (Npad blocks)
-// out layout: halves [Kc][2 part][2 ks][Npad][16], then float inv_scale[Npad]
+// out layout: halves [Kc][2 part][2 ks][Npad rows in fimg order], then float inv_scale[Npad]
 __global__ void __launch_bounds__(64)
 k_pack_weight(const float* __restrict__ W, int64_t ldw, int N, int K, int trans, int Npad, int Kc,
               _Float16* __restrict__ out, float* __restrict__ inv_scale) {
@@ -119,8 +126,9 @@ k_pack_weight(const float* __restrict__ W, int64_t ldw, int N, int K, int trans,
         const float y = x * s;
         const _Float16 h = (_Float16)y;
         const int kc = k / KC, ks = (k / 16) & 1, j = k & 15;
-        out[((((int64_t)kc * 2 + 0) * 2 + ks) * Npad + n) * 16 + j] = h;
-        out[((((int64_t)kc * 2 + 1) * 2 + ks) * Npad + n) * 16 + j] = (_Float16)(y - (float)h);
+        const int64_t at = fimg(n, j >> 3) / 2 + (j & 7);
+        out[(((int64_t)kc * 2 + 0) * 2 + ks) * Npad * 16 + at] = h;
+        out[(((int64_t)kc * 2 + 1) * 2 + ks) * Npad * 16 + at] = (_Float16)(y - (float)h);
     }
     if (l == 0) inv_scale[n] = (n < N) ? pow2(-se) : 0.f;
 }
@@ -163,8 +171,10 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #pragma unroll
     for (int i = 0; i < WPT; ++i) {
         const int p = t + i * NT;
-        const int part = p / (BF * 4), ks = (p / (BF * 2)) & 1, nl = (p >> 1) % BF, q = p & 1;
-        woff[i] = (((part * 2 + ks) * Npad + f0 + nl) * 2 + q) * 16;
+        // LDS piece p of the stage's weight image: plane p / (2 BF), then fimg order
+        const int plane = p / (BF * 2), rem = p % (BF * 2);
+        const int nl = (rem >> 6) * 32 + (rem & 31), q = (rem >> 5) & 1;
+        woff[i] = plane * Npad * 32 + fimg(f0 + nl, q);
     }
     int se_run = SE_INIT;                   // running scale exponent of this data row
 
@@ -212,8 +222,8 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
             const int kl = kp * FPT + j, ks = kl >> 4, pos = kl & 15;
             h8 hv, lv;
             split8(dv[set][j / 4], dv[set][j / 4 + 1], s, hv, lv);
-            *reinterpret_cast<h8*>(st + ((0 * 2 + ks) * BD + rho) * 32 + pos * 2) = hv;
-            *reinterpret_cast<h8*>(st + ((1 * 2 + ks) * BD + rho) * 32 + pos * 2) = lv;
+            *reinterpret_cast<h8*>(st + (0 * 2 + ks) * BD * 32 + fimg(rho, pos >> 3)) = hv;
+            *reinterpret_cast<h8*>(st + (1 * 2 + ks) * BD * 32 + fimg(rho, pos >> 3)) = lv;
         }
         // every loader thread of the row holds the same factor: a branch-free (same-value) store
         reinterpret_cast<float*>(st + D_BYTES + W_BYTES)[rho] = first ? 1.f : pow2(se - se_old);
@@ -254,10 +264,10 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
             for (int pt = 0; pt < 2; ++pt) {
 #pragma unroll
                 for (int a = 0; a < TFT; ++a)
-                    wf[a][pt] = *reinterpret_cast<const h8*>(st + D_BYTES + ((pt * 2 + ks) * BF + f_w + 32 * a + r) * 32 + h * 16);
+                    wf[a][pt] = *reinterpret_cast<const h8*>(st + D_BYTES + (pt * 2 + ks) * BF * 32 + fimg(f_w + 32 * a + r, h));
 #pragma unroll
                 for (int b = 0; b < TDT; ++b)
-                    df[b][pt] = *reinterpret_cast<const h8*>(st + ((pt * 2 + ks) * BD + d_w + 32 * b + r) * 32 + h * 16);
+                    df[b][pt] = *reinterpret_cast<const h8*>(st + (pt * 2 + ks) * BD * 32 + fimg(d_w + 32 * b + r, h));
             }
 #pragma unroll
             for (int a = 0; a < TFT; ++a)
@@ -534,10 +544,12 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
         h8 hv[2], lv[2];
         split8(xv[0], xv[1], s, hv[0], lv[0]);
         split8(xv[2], xv[3], s, hv[1], lv[1]);
-        h8* hd = reinterpret_cast<h8*>(st + img + ((0 * 2 + kse) * rows_img + cl) * 32);
-        h8* ld = reinterpret_cast<h8*>(st + img + ((1 * 2 + kse) * rows_img + cl) * 32);
-        hd[0] = hv[0]; hd[1] = hv[1];
-        ld[0] = lv[0]; ld[1] = lv[1];
+        char* hd = st + img + (0 * 2 + kse) * rows_img * 32;
+        char* ld = st + img + (1 * 2 + kse) * rows_img * 32;
+        *reinterpret_cast<h8*>(hd + fimg(cl, 0)) = hv[0];
+        *reinterpret_cast<h8*>(hd + fimg(cl, 1)) = hv[1];
+        *reinterpret_cast<h8*>(ld + fimg(cl, 0)) = lv[0];
+        *reinterpret_cast<h8*>(ld + fimg(cl, 1)) = lv[1];
         if (kse == 0) reinterpret_cast<float*>(st + A_BYTES + B_BYTES)[fac_off] = first ? 1.f : pow2(se - se_old);
         if (do_cs) {           // column sums of A from the fp32 values, in row order
 #pragma unroll
@@ -591,10 +603,10 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
             for (int pt = 0; pt < 2; ++pt) {
 #pragma unroll
                 for (int a = 0; a < TMT; ++a)
-                    af[a][pt] = *reinterpret_cast<const h8*>(st + ((pt * 2 + ks) * BM + m_w + 32 * a + r) * 32 + h * 16);
+                    af[a][pt] = *reinterpret_cast<const h8*>(st + (pt * 2 + ks) * BM * 32 + fimg(m_w + 32 * a + r, h));
 #pragma unroll
                 for (int b = 0; b < TNT; ++b)
-                    bf[b][pt] = *reinterpret_cast<const h8*>(st + A_BYTES + ((pt * 2 + ks) * BN + n_w + 32 * b + r) * 32 + h * 16);
+                    bf[b][pt] = *reinterpret_cast<const h8*>(st + A_BYTES + (pt * 2 + ks) * BN * 32 + fimg(n_w + 32 * b + r, h));
             }
 #pragma unroll
             for (int a = 0; a < TMT; ++a)
