@@ -478,7 +478,10 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     static_assert(2 * (BM + BN) == NT, "loader mapping: one column slot per thread");
     constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
     constexpr int STAGE = A_BYTES + B_BYTES + (BM + BN) * 4;
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 16];
+    // per stage: index of the chunk in it if some column's scale changed with that chunk (a
+    // same-value store by every such thread; no reset needed, chunk indices are unique)
+    int* const rescaled = reinterpret_cast<int*>(lds + 2 * STAGE);
 
     const int t = threadIdx.x;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -524,15 +527,13 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
             for (int j = 0; j < 16; ++j)
                 x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + j * ldx * 4, 0, 0));
         }
+        // no zeroing of columns past Mc / Nc (they re-read column 0): such a column only feeds
+        // its own output row / column, which is never stored, under its own scale.  A select
+        // here would make the compiler wait for the loads right after issuing them.
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            xv[j].x = col_ok ? x[4 * j + 0] : 0.f;
-            xv[j].y = col_ok ? x[4 * j + 1] : 0.f;
-            xv[j].z = col_ok ? x[4 * j + 2] : 0.f;
-            xv[j].w = col_ok ? x[4 * j + 3] : 0.f;
-        }
+        for (int j = 0; j < 4; ++j) xv[j] = make_float4(x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]);
     };
-    auto store = [&](int buf, bool first = false) -> bool {     // first chunk: factor 1 (acc is zero)
+    auto store = [&](int buf, int chunk, bool first = false) {   // first chunk: factor 1 (acc is zero)
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
@@ -555,7 +556,7 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
 #pragma unroll
             for (int j = 0; j < 4; ++j) { cs += xv[j].x; cs += xv[j].y; cs += xv[j].z; cs += xv[j].w; }
         }
-        return !first && se != se_old;
+        if (!first && se != se_old) rescaled[buf] = chunk;
     };
 
     f16v acc[TMT][TNT];
@@ -566,18 +567,18 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
 
+    if (t < 2) rescaled[t] = -1;
     if (nc > 0) {
         load(0);
-        store(0, true);
+        store(0, 0, true);
     }
-    int any = 0;
     __syncthreads();
     for (int c = 0; c < nc; ++c) {
         const int buf = c & 1;
         const bool more = c + 1 < nc;
         if (more) load(c + 1);
         const char* st = lds + buf * STAGE;
-        if (any) {
+        if (rescaled[buf] == c) {
             const float* fac = reinterpret_cast<const float*>(st + A_BYTES + B_BYTES);
 #pragma unroll
             for (int a = 0; a < TMT; ++a) {
@@ -624,9 +625,8 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                 for (int b = 0; b < TNT; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][1], bf[b][0], acc[a][b], 0, 0, 0);
         }
-        bool changed = false;
-        if (more) changed = store(buf ^ 1);
-        any = __syncthreads_or(changed);
+        if (more) store(buf ^ 1, c + 1);
+        __syncthreads();
     }
 
     // epilogue: part[p][m][n] = acc * 2^-se_a(m) * 2^-se_b(n)
