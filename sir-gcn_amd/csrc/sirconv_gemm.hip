@@ -500,6 +500,10 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     const int ldx = (int)(is_a ? lda : ldb);
     const int xoff = 16 * kse * ldx + (is_a ? m0 : n0) + (col_ok ? cl : 0);   // within a chunk
     const int img = is_a ? 0 : A_BYTES, rows_img = is_a ? BM : BN, fac_off = is_a ? cl : BM + cl;
+    // this thread's LDS destinations within a stage, folded into two offsets (fewer live VGPRs)
+    const int hi_off = img + kse * rows_img * 32 + fimg(cl, 0);
+    const int lo_delta = 2 * rows_img * 32;
+    const int fac_byte = A_BYTES + B_BYTES + fac_off * 4;
     int se_run = SE_INIT;
 
     const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
@@ -545,13 +549,12 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
         h8 hv[2], lv[2];
         split8(xv[0], xv[1], s, hv[0], lv[0]);
         split8(xv[2], xv[3], s, hv[1], lv[1]);
-        char* hd = st + img + (0 * 2 + kse) * rows_img * 32;
-        char* ld = st + img + (1 * 2 + kse) * rows_img * 32;
-        *reinterpret_cast<h8*>(hd + fimg(cl, 0)) = hv[0];
-        *reinterpret_cast<h8*>(hd + fimg(cl, 1)) = hv[1];
-        *reinterpret_cast<h8*>(ld + fimg(cl, 0)) = lv[0];
-        *reinterpret_cast<h8*>(ld + fimg(cl, 1)) = lv[1];
-        if (kse == 0) reinterpret_cast<float*>(st + A_BYTES + B_BYTES)[fac_off] = first ? 1.f : pow2(se - se_old);
+        char* hd = st + hi_off;               // fimg(cl, 1) = fimg(cl, 0) + 512
+        *reinterpret_cast<h8*>(hd) = hv[0];
+        *reinterpret_cast<h8*>(hd + 512) = hv[1];
+        *reinterpret_cast<h8*>(hd + lo_delta) = lv[0];
+        *reinterpret_cast<h8*>(hd + lo_delta + 512) = lv[1];
+        if (kse == 0) *reinterpret_cast<float*>(st + fac_byte) = first ? 1.f : pow2(se - se_old);
         if (do_cs) {           // column sums of A from the fp32 values, in row order
 #pragma unroll
             for (int j = 0; j < 4; ++j) { cs += xv[j].x; cs += xv[j].y; cs += xv[j].z; cs += xv[j].w; }
