@@ -81,6 +81,9 @@ def test_gemm_nt_wide_dynamic_range_and_running_scale():
     ramp = torch.exp2(torch.linspace(-30, 30, K, device=DEV))
     A[100:300] *= ramp                      # maximum rises chunk after chunk
     A[300:400] *= ramp.flip(0)
+    A[400:420, :96] = 0                     # leading zero chunks, then data: first scale set late
+    A[420:440, :64] = 2.0 ** -130           # subnormal leading chunks, then normal-range data
+    A[440:460, 32:] *= 2.0 ** 20            # a chunk far above the first one's headroom
     W = torch.randn(N, K, device=DEV, generator=g) * torch.exp2(torch.randint(-20, 20, (N, 1), device=DEV,
                                                                                 generator=g).float())
     C = _native.gemm_nt(A, _native.gemm_pack(W))
@@ -127,6 +130,7 @@ def test_gemm_tn_dynamic_range_strided_and_deterministic():
     A *= torch.exp2(torch.randint(-40, 40, (1, 512), device=DEV, generator=g).float())
     B = torch.randn(R, 256, device=DEV, generator=g)
     B[20000:21000] *= 2.0 ** 30                             # a late row block raises the B scales
+    B[:3000, :17] = 0                                       # leading zero rows of some B columns
     C1 = _native.gemm_tn(A, B)
     C2 = _native.gemm_tn(A, B)
     assert torch.equal(C1, C2), "TN GEMM must be run-to-run deterministic"
