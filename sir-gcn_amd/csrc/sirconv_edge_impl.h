@@ -394,12 +394,13 @@ __device__ __forceinline__ float sel_mask(uint64_t m, float t, float slope) {
 #define SIR_DQ_VMASK 1          // dQ pass: mask words by one vector load + v_readlane (1; -9% sum, -19% sym) or scalar loads (0)
 #endif
 
-template <int MODE, int ACT, int AGG, int NV, int UU>
+template <int MODE, int ACT, int AGG, int NV, int UU, bool PRE = false>
 __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, const int* __restrict__ perm,
                                            const float* __restrict__ G, int64_t ldg,
                                            const uint64_t* __restrict__ mask,
                                            const float* __restrict__ norm_col, float nr, float slope,
-                                           int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4]) {
+                                           int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4],
+                                           uint64_t pre = 0, int pre_lane = 0) {
     constexpr int NW = NV * 4;
     int p[UU];
     int v[UU];
@@ -414,7 +415,19 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
         }
     }
     uint64_t wd[UU][NW];
-    if constexpr (SIR_DQ_VMASK && MODE == MODE_BWD_DST && UU * NW <= 64) {
+    if constexpr (PRE) {
+        // words already in registers (one per lane, prefetched by mask_item_dst): edge e's word
+        // k is in lane pre_lane + i*NW + k
+        const int mlo = (int)(uint32_t)pre, mhi = (int)(uint32_t)(pre >> 32);
+#pragma unroll
+        for (int i = 0; i < UU; ++i)
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(mlo, pre_lane + i * NW + k);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(mhi, pre_lane + i * NW + k);
+                wd[i][k] = ((uint64_t)hi << 32) | lo;
+            }
+    } else if constexpr (SIR_DQ_VMASK && MODE == MODE_BWD_DST && UU * NW <= 64) {
         // the batch's UU*NW words are contiguous: one 8-B vector load per lane, then broadcast
         // each word to SGPRs (v_readlane) for the lane-mask selects
         const uint64_t mv = (lane < UU * NW) ? mask[(int64_t)e * NW + lane] : 0ull;
@@ -501,6 +514,44 @@ __device__ __forceinline__ void mask_item(int e0, int e1, const int* __restrict_
         mask_batch<MODE, ACT, AGG, NV, 1>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
 }
 
+#ifndef SIR_DQ_PF
+#define SIR_DQ_PF 1             // dQ pass: next batch's mask words loaded before the current batch is summed
+#endif
+
+// dQ pass (no col/perm reads for sum/mean): the mask words of the NEXT U-edge batch are loaded
+// while the current batch is summed, so a wave no longer waits one memory latency per batch.
+// A full batch is loaded whole; the row's final partial batch (and a row shorter than U) is
+// loaded lane-guarded, so no load leaves the row.  Every batch's words start at lane 0, so the
+// readlane lane indices are compile-time constants (a runtime lane index costs ~20%); the final
+// partial batch is summed edge by edge under uniform guards.
+template <int ACT, int AGG, int NV, int U>
+__device__ __forceinline__ void mask_item_dst(int e0, int e1, const int* __restrict__ col,
+                                              const uint64_t* __restrict__ mask,
+                                              const float* __restrict__ norm_col, float nr, float slope,
+                                              int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4]) {
+    constexpr int NW = NV * 4, BW = U * NW;       // words per edge, per batch (BW <= 64)
+    const int wl = lane % BW;
+    auto load_batch = [&](int eb) -> uint64_t {
+        const int n = e1 - eb;
+        if (n >= U) return mask[(int64_t)eb * NW + wl];
+        return (lane < n * NW) ? mask[(int64_t)eb * NW + lane] : 0ull;
+    };
+    uint64_t cur = load_batch(e0);
+    int e = e0;
+    for (; e + U <= e1; e += U) {
+        const uint64_t nxt = load_batch(e + U);
+        mask_batch<MODE_BWD_DST, ACT, AGG, NV, U, true>(e, col, nullptr, nullptr, 0, mask, norm_col, nr, slope,
+                                                        lane, HC, gv, acc, cur, 0);
+        cur = nxt;
+    }
+    const int r = e1 - e;                         // 0 .. U-1 edges left, their words in cur
+#pragma unroll
+    for (int i = 0; i < U - 1; ++i)
+        if (i < r)
+            mask_batch<MODE_BWD_DST, ACT, AGG, NV, 1, true>(e + i, col, nullptr, nullptr, 0, mask, norm_col, nr,
+                                                            slope, lane, HC, gv, acc, cur, i * NW);
+}
+
 __device__ __forceinline__ int4 uniform_item(const int4* __restrict__ items, int64_t i) {
     int4 it = items[i];
     it.x = __builtin_amdgcn_readfirstlane(it.x);
@@ -555,7 +606,10 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     }
     float nr = 1.f;
     if constexpr (AGG == AGG_SYM) nr = norm_row[row];
-    mask_item<MODE, ACT, AGG, NV, U>(e0, e1, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    if constexpr (SIR_DQ_PF && MODE == MODE_BWD_DST && AGG != AGG_SYM && U * NV * 4 <= 64)
+        mask_item_dst<ACT, AGG, NV, U>(e0, e1, col, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    else
+        mask_item<MODE, ACT, AGG, NV, U>(e0, e1, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
     float* op = (slot < 0) ? out + (int64_t)row * ldo : partial + (int64_t)slot * H;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
