@@ -48,6 +48,9 @@ constexpr int KC = 32;          // contraction elements per LDS stage (two k16 M
 #ifndef SIR_HR
 #define SIR_HR 8                // headroom bits of a reset running scale (see next_se)
 #endif
+#ifndef SIR_TN_CFG
+#define SIR_TN_CFG 2            // TN tiling: 1 = 16 waves 64x64 (4 per SIMD), 2 = 8 waves 128x64 (2 per SIMD)
+#endif
 #ifndef SIR_NT_PF
 #define SIR_NT_PF 2             // NT chunks in flight in registers ahead of the LDS stage (1 or 2)
 #endif
@@ -475,7 +478,11 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
           int n_mtiles, int n_ntiles, int64_t rows_per_split) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BM = 32 * TMT * WM, BN = 32 * TNT * WN;
-    static_assert(2 * (BM + BN) == NT, "loader mapping: one column slot per thread");
+    // loader: one column slot per KSPT threads — KSPT = 1: a thread loads one k-step (16 rows)
+    // of its column, its partner (t ^ 1) the other; KSPT = 2: a thread loads all 32 rows
+    constexpr int KSPT = 2 * (BM + BN) / NT;
+    static_assert(KSPT * NT == 2 * (BM + BN) && (KSPT == 1 || KSPT == 2), "loader mapping");
+    constexpr int XR = 16 * KSPT;            // rows of its column a thread loads per chunk
     constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
     constexpr int STAGE = A_BYTES + B_BYTES + (BM + BN) * 4;
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 16];
@@ -493,8 +500,9 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     const int nc = (int)((v_end - v_begin + KC - 1) / KC);
 
     // loader slot (A or B is wave-uniform: waves [0, BM/32) load A)
-    const bool is_a = __builtin_amdgcn_readfirstlane(t >> 6) < 2 * BM / 64;
-    const int cl = is_a ? (t >> 1) : ((t - 2 * BM) >> 1), kse = t & 1;
+    const int slot = KSPT == 1 ? (t >> 1) : t;
+    const bool is_a = __builtin_amdgcn_readfirstlane(t >> 6) < BM * (2 / KSPT) / 64;
+    const int cl = is_a ? slot : slot - BM, kse = KSPT == 1 ? (t & 1) : 0;
     const bool col_ok = is_a ? (m0 + cl < Mc) : (n0 + cl < Nc);
     const float* xbase = is_a ? A : B;
     const int ldx = (int)(is_a ? lda : ldb);
@@ -509,7 +517,7 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
     const int m_w = (w / WN) * TMT * 32, n_w = (w % WN) * TNT * 32;
 
-    float4 xv[4];
+    float4 xv[XR / 4];
     // bias gradient of the same linear (column sums of A) rides on the A loads: one partial row
     // per split, written by the blocks of the first n-tile
     const bool do_cs = csum_part != nullptr && is_a;
@@ -517,47 +525,50 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     auto load = [&](int c) {
         const int64_t vc = v_begin + (int64_t)c * KC;
         const float* src = xbase + vc * ldx;                 // wave-uniform chunk base
-        float x[16];
+        float x[XR];
         if (vc + KC <= v_end) {
             const rsrc_t rs = mk_rsrc(src, SIR_ABL_TN ? 0u : (uint32_t)(KC * ldx * 4));
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
+            for (int j = 0; j < XR; ++j)
                 x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, xoff * 4, j * ldx * 4, 0));
         } else {   // tail chunk: rows past v_end fail the range check and read as 0
             const rsrc_t rs = mk_rsrc(src, SIR_ABL_TN ? 0u : (uint32_t)((v_end - vc) * ldx * 4));
             int o = xoff * 4;
-            asm volatile("" : "+v"(o));      // keep the 16 offsets out of the loop preheader
+            asm volatile("" : "+v"(o));      // keep the offsets out of the loop preheader
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
+            for (int j = 0; j < XR; ++j)
                 x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + j * ldx * 4, 0, 0));
         }
         // no zeroing of columns past Mc / Nc (they re-read column 0): such a column only feeds
         // its own output row / column, which is never stored, under its own scale.  A select
         // here would make the compiler wait for the loads right after issuing them.
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[j] = make_float4(x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]);
+        for (int j = 0; j < XR / 4; ++j) xv[j] = make_float4(x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]);
     };
     auto store = [&](int buf, int chunk, bool first = false) {   // first chunk: factor 1 (acc is zero)
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) m = fmax4(m, xv[j]);
-        m = fmaxf(m, __shfl_xor(m, 1));
+        for (int j = 0; j < XR / 4; ++j) m = fmax4(m, xv[j]);
+        if (KSPT == 1) m = fmaxf(m, __shfl_xor(m, 1));
         const int se_old = se_run, se = next_se(se_old, bexp(m));
         se_run = se;
         const float s = pow2(se);
-        h8 hv[2], lv[2];
-        split8(xv[0], xv[1], s, hv[0], lv[0]);
-        split8(xv[2], xv[3], s, hv[1], lv[1]);
-        char* hd = st + hi_off;               // fimg(cl, 1) = fimg(cl, 0) + 512
-        *reinterpret_cast<h8*>(hd) = hv[0];
-        *reinterpret_cast<h8*>(hd + 512) = hv[1];
-        *reinterpret_cast<h8*>(hd + lo_delta) = lv[0];
-        *reinterpret_cast<h8*>(hd + lo_delta + 512) = lv[1];
+#pragma unroll
+        for (int q = 0; q < KSPT; ++q) {      // k-step kse + q: rows 16q .. 16q+15 of x
+            h8 hv[2], lv[2];
+            split8(xv[4 * q + 0], xv[4 * q + 1], s, hv[0], lv[0]);
+            split8(xv[4 * q + 2], xv[4 * q + 3], s, hv[1], lv[1]);
+            char* hd = st + hi_off + q * rows_img * 32;    // fimg(cl, 1) = fimg(cl, 0) + 512
+            *reinterpret_cast<h8*>(hd) = hv[0];
+            *reinterpret_cast<h8*>(hd + 512) = hv[1];
+            *reinterpret_cast<h8*>(hd + lo_delta) = lv[0];
+            *reinterpret_cast<h8*>(hd + lo_delta + 512) = lv[1];
+        }
         if (kse == 0) *reinterpret_cast<float*>(st + fac_byte) = first ? 1.f : pow2(se - se_old);
         if (do_cs) {           // column sums of A from the fp32 values, in row order
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { cs += xv[j].x; cs += xv[j].y; cs += xv[j].z; cs += xv[j].w; }
+            for (int j = 0; j < XR / 4; ++j) { cs += xv[j].x; cs += xv[j].y; cs += xv[j].z; cs += xv[j].w; }
         }
         if (!first && se != se_old) rescaled[buf] = chunk;
     };
@@ -653,8 +664,9 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
         }
     }
     if (do_cs && tile % n_ntiles == 0) {
-        const float other = __shfl_xor(cs, 1);          // the partner thread holds rows 16..31 of each chunk
-        if (kse == 0 && col_ok) csum_part[(int64_t)p * Mc + m0 + cl] = cs + other;
+        // KSPT = 1: the partner thread holds rows 16..31 of each chunk
+        const float other = KSPT == 1 ? __shfl_xor(cs, 1) : 0.f;
+        if (kse == 0 && col_ok) csum_part[(int64_t)p * Mc + m0 + cl] = KSPT == 1 ? cs + other : cs;
     }
 }
 
@@ -735,8 +747,14 @@ hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb,
     const int nmt = (Mc + 255) / 256, nnt = (Nc + 255) / 256;
     float* part = static_cast<float*>(workspace);
     float* cpart = colsum != nullptr ? part + (int64_t)P * Mc * Nc : nullptr;
+#if SIR_TN_CFG == 2
+    // 8 waves (2 per SIMD, 256 registers), 128x64 per wave, a thread loads a whole column chunk
+    hipLaunchKernelGGL((k_gemm_tn<2, 4, 4, 2>), dim3((unsigned)(P * nmt * nnt)), dim3(512), 0, st,
+                       A, lda, B, ldb, R, Mc, Nc, part, cpart, nmt, nnt, rps);
+#else
     hipLaunchKernelGGL((k_gemm_tn<4, 4, 2, 2>), dim3((unsigned)(P * nmt * nnt)), dim3(1024), 0, st,
                        A, lda, B, ldb, R, Mc, Nc, part, cpart, nmt, nnt, rps);
+#endif
     const int64_t count = (int64_t)Mc * Nc;
     hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
                        part, P, count, Nc, C, ldc);
