@@ -163,29 +163,35 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
     int u[UU];
 #pragma unroll
     for (int i = 0; i < UU; ++i) u[i] = col[e + i];
-    float cf[UU];
-    if constexpr (AGG == AGG_SYM) {
-#pragma unroll
-        for (int i = 0; i < UU; ++i) cf[i] = norm_col[u[i]] * nr;  // out_norm[u] * in_norm[v]
-    }
     float cv[UU][NV][VW];
     float gc[(MODE == MODE_BWD_SRC) ? UU : 1][NV][VW];
 #pragma unroll
     for (int i = 0; i < UU; ++i) {
+        // gathers are unconditional: lanes past the row (c >= HC) re-read column 0 and their
+        // values are never used.  A guarded load becomes an exec-masked branch whose result the
+        // compiler may copy inside the branch, i.e. wait for right after issuing it — that
+        // serialised the gathers of some instances (sym forward: +50%).
         const float* cp = C + (int64_t)u[i] * ldc;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (c < HC) vload_gather<VW>(cv[i][j], cp + c * VW);
+            vload_gather<VW>(cv[i][j], cp + (c < HC ? c : 0) * VW);
         }
         if constexpr (MODE == MODE_BWD_SRC) {
             const float* gp = G + (int64_t)u[i] * ldg;
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const int c = li + LPR * j;
-                if (c < HC) vload_gather<VW>(gc[i][j], gp + c * VW);
+                vload_gather<VW>(gc[i][j], gp + (c < HC ? c : 0) * VW);
             }
         }
+    }
+    // sym norms after the row gathers are issued: their (scalar) loads then overlap the gathers
+    // instead of the wait for them preceding the gather issue
+    float cf[UU];
+    if constexpr (AGG == AGG_SYM) {
+#pragma unroll
+        for (int i = 0; i < UU; ++i) cf[i] = norm_col[u[i]] * nr;  // out_norm[u] * in_norm[v]
     }
     if constexpr (MASKW) {
         // sign mask of z for the sign-mask backward: word (j*4+w), bit lane = z[(lane+64j)*4+w] > 0.
@@ -459,7 +465,7 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const int c = lane + 64 * j;
-                if (c < HC) vload_gather<4>(gc[i][j], gp + c * 4);
+                vload_gather<4>(gc[i][j], gp + (c < HC ? c : 0) * 4);   // unconditional (see edge_batch)
             }
         }
     }
