@@ -691,7 +691,7 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 #define SIR_UNROLL_FWD 4
 #endif
 #ifndef SIR_UNROLL_DST
-#define SIR_UNROLL_DST 8
+#define SIR_UNROLL_DST 6
 #endif
 #ifndef SIR_UNROLL_SRC
 #define SIR_UNROLL_SRC 8
