@@ -1,26 +1,37 @@
 #!/usr/bin/env python3
-"""bench.py — edges/sec of one SIRConv layer, forward + backward, d_hidden = 256, on MI355X.
+"""bench.py — edges/sec of SIRConv forward + backward on MI355X (BASELINE.json metric).
 
-Metric (BASELINE.json): "edges/sec SIRConv fwd+bwd, d_hidden=256, 1/2/4/8 MI355X".
-Workload (default, BASELINE config 4 / SURVEY §8d): synthetic Chung-Lu power-law graph S2
-(V = 2,000,000, E = 40,000,000, alpha = 0.8; `sirgcn.synth`), d_in = H = d_out = 256 fp32,
-agg = sum, sigma = LeakyReLU(0.2); X ~ N(0,1) (seed 3), nn.Linear default init (seed 4),
-dY ~ N(0,1) (seed 5).  One step = Y = SIRConv(g, X); Y.backward(dY)  (projections, edge
-kernels, all weight/input gradients).  Graph plan (CSR build) is outside the timed region,
-as DGL's cached CSC is.
+Default workload (BASELINE config 4 / SURVEY §8d): synthetic Chung-Lu power-law graph S2
+(V = 2,000,000, E = 40,000,000, alpha = 0.8; ``sirgcn.synth``), ONE SIRConv layer,
+d_in = H = d_out = 256, fp32, agg = sum, sigma = LeakyReLU(0.2); X ~ N(0,1) (seed 3),
+nn.Linear default init (seed 4), dY ~ N(0,1) (seed 5).  One step = Y = SIRConv(g, X);
+Y.backward(dY) (projections, edge kernels, every weight / input gradient).  The graph plan (CSR
+build) is outside the timed region, as DGL's cached CSC is.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--graph S2|S1|S1u|arxiv] [--agg sum]
-  N > 1: launched by torch.distributed.run, one rank per GPU; dst-range edge-cut of the SAME
-  graph (strong scaling) with a sparse RCCL all-to-all of halo K rows fwd and its transpose for dK bwd (sirgcn.dist).
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--graph S2|S1|S1u|arxiv] [--agg sum|mean|sym]
+                  [--dtype f32|bf16|f16] [--workload cfg4|cfg1|cfg2|cfg3|cfg5]
 
-Prints ONE JSON line (rank 0).  `roofline` is for the dominant edge kernel, timed live with
-HIP events on the launching stream; `cpu_baseline` is the reference CPU dataflow restated in
-oracle/ (DGL edge-UDF path: gathers + index_add, torch autograd), on a bounded sample.
+* ``--gpus N`` with N > 1 and no WORLD_SIZE in the environment: this process starts
+  ``torch.distributed.run`` with N ranks (before touching the GPU) and exits with its status;
+  under torchrun (WORLD_SIZE set) it is one rank.  cfg4 at N > 1 = dst-range edge-cut of the SAME
+  graph (strong scaling) with a sparse RCCL all-to-all of halo K rows forward and its transpose
+  for dK backward (``sirgcn.dist``); cfg5 at N > 1 = data parallel (a different 64-molecule batch
+  per rank, DDP gradient all-reduce over RCCL; weak scaling).
+* Without a GPU (``--dist-backend gloo``) the edge-cut plumbing is rehearsed on the CPU with the
+  test-only CPU edge backend: the line is marked ``"rehearsal"`` and measures nothing.
+
+Prints ONE JSON line (rank 0).  ``roofline``: the forward edge-aggregation kernel (the kernel the
+north star names), SURVEY §8(d) algorithmic bytes ÷ its mean launch time from HIP events on the
+launching stream; plus the PMC-counter and unique-bytes views and a streaming-copy rate measured in
+the same process.  ``cpu_baseline``: the reference CPU dataflow restated in ``oracle/`` (DGL
+edge-UDF path: gathers + index_add, torch autograd) on the S1 graph, host cores stated.
 """
 import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,14 +39,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sir-gcn_amd"))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-from torch import nn  # noqa: E402
-
 METRIC = "edges/sec SIRConv fwd+bwd, d_hidden=256, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 FP32_PEAK_TFLOPS = 157.3    # fp32 MFMA = vector peak (no xf32 on gfx950)
 FP16_PEAK_FLOPS = 2.5e15    # dense fp16/bf16 MFMA (MI355X_MICROARCH.md; the 5 PF figure is 2:1 sparse)
+SIZEOF = {"f32": 4, "bf16": 2, "f16": 2}
 
 
 def parse():
@@ -43,14 +51,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--graph", default="S2")
+    ap.add_argument("--workload", default="cfg4", choices=["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+    ap.add_argument("--graph", default="S2", help="cfg4 graph: S2 (default), S1, S1u, arxiv")
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--agg", default="sum", choices=["sum", "mean", "sym"])
+    ap.add_argument("--dtype", default=None, choices=["f32", "bf16", "f16"],
+                    help="feature dtype (16-bit = the autocast path); default f32 (cfg2: bf16)")
     ap.add_argument("--chunk", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-graph", default="S1", help="graph of the reference CPU dataflow baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat CPU baseline steps until this long")
+    ap.add_argument("--no-aux", action="store_true", help="skip the copy-rate and torch-GEMM A/B measurements")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl (= RCCL) for real runs; gloo only to rehearse N ranks on one GPU")
+                    help="nccl (= RCCL) for real runs; gloo to rehearse N ranks (CPU without a GPU)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the edge-cut (sirgcn.dist) code path even at world size 1")
     ap.add_argument("--torch-gemm", action="store_true",
@@ -60,13 +73,32 @@ def parse():
     return ap.parse_args()
 
 
-def edge_pass_bytes(name, V_rows, E, H, agg, masked, s=4, si=4):
-    """Algorithmic HBM bytes of one launch of each edge pass.
+# ------------------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
-    Recompute mode (any sigma): fwd gathers K[u]; dQ pass re-gathers K[u]; dK pass gathers Q[v]
-    and G[v].  Sign-mask mode (ReLU family): fwd also writes H bits/edge; dQ pass reads only the
-    mask; dK pass gathers G[v] + the edge's mask words (+ its permutation index).
-    """
+
+def self_launch(args):
+    """``bench.py --gpus N`` outside torchrun: start N ranks (one per GPU) as a child
+    ``torch.distributed.run`` — before this process initialises any GPU — and return its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------ accounting
+def edge_pass_bytes(name, V_rows, E, H, agg, masked, s=4, si=4):
+    """Bytes one launch of each edge pass moves in THIS design (includes the sign
+    mask of the ReLU-family backward).  Recompute mode (any sigma): fwd gathers K[u]; dQ pass
+    re-gathers K[u]; dK pass gathers Q[v] and G[v].  Sign-mask mode: fwd also writes H bits/edge;
+    dQ pass reads only the mask; dK pass gathers G[v] + the edge's mask words (+ its permutation)."""
     mb = 8 * 4 * ((H + 255) // 256) if masked else 0           # mask bytes per edge
     sym_e = E * (si + 4) if agg == "sym" else 0                 # col + norm_col per edge when c_e needed
     sym_r = V_rows * 4 if agg == "sym" else 0
@@ -84,28 +116,69 @@ def edge_pass_bytes(name, V_rows, E, H, agg, masked, s=4, si=4):
     raise KeyError(name)
 
 
+def fwd_algorithmic_bytes(V, E, H, s=4, si=4):
+    """SURVEY §8(d) B_fwd = E (s_i + H s) + V (2 H s + s_i): col + K[u] per edge, Q read + S write +
+    rowptr per destination (implementation-neutral: no sign mask, no sym norms)."""
+    return E * (si + H * s) + V * (2 * H * s + si)
+
+
+def fwd_unique_bytes(V_src, V, E, H, s=4, si=4):
+    """Lower bound: every K row read ONCE (as if the gathers all hit cache after the first)."""
+    return V_src * H * s + E * si + V * (2 * H * s + si)
+
+
+# ------------------------------------------------------------------------------ baselines
+def copy_rate(dev, nbytes=4 << 30, reps=10):
+    """Streaming-copy GB/s in this process (read + write bytes / time), the achievable HBM rate."""
+    import torch
+    n = nbytes // 4
+    a = torch.empty(n, dtype=torch.float32, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+
 def cpu_baseline(args, H):
-    """Reference CPU dataflow (oracle.reference_cpu_step) on a bounded sample, rank 0 only."""
+    """The reference CPU dataflow (oracle.reference_cpu_step: DGL edge-UDF gathers + index_add,
+    torch autograd) on ``--cpu-graph`` (S1 by default, one step, unchunked), rank 0 only."""
+    import torch
+    from torch import nn
     import oracle
-    from sirgcn.synth import powerlaw_edges
+    from sirgcn.synth import NAMED, powerlaw_edges
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     torch.set_num_threads(cores)
-    Vs, Es = 100_000, 2_000_000
-    src, dst = powerlaw_edges(Vs, Es, 0.8, seed=0)
-    g = torch.Generator().manual_seed(3)
-    X = torch.randn(Vs, H, generator=g)
-    torch.manual_seed(4)
-    m = nn.ModuleList([nn.Linear(H, H), nn.Linear(H, H, bias=False), nn.Linear(H, H)])
-    dY = torch.randn(Vs, H, generator=torch.Generator().manual_seed(5))
-    w = [m[0].weight.data, m[0].bias.data, m[1].weight.data, m[2].weight.data, m[2].bias.data]
-    oracle.reference_cpu_step(src, dst, Vs, X, *w, dY, args.agg, "leaky", 0.2)    # warm-up
+    Vs, Es, alpha = NAMED[args.cpu_graph]
+    agg = args.agg
+
+    def setup(V, E):
+        src, dst = powerlaw_edges(V, E, alpha, seed=0)
+        X = torch.randn(V, H, generator=torch.Generator().manual_seed(3))
+        torch.manual_seed(4)
+        m = nn.ModuleList([nn.Linear(H, H), nn.Linear(H, H, bias=False), nn.Linear(H, H)])
+        dY = torch.randn(V, H, generator=torch.Generator().manual_seed(5))
+        w = [m[0].weight.data, m[0].bias.data, m[1].weight.data, m[2].weight.data, m[2].bias.data]
+        return src, dst, X, w, dY
+
+    src, dst, X, w, dY = setup(Vs // 50, Es // 50)            # warm-up on a 2% sample (allocator, threads)
+    oracle.reference_cpu_step(src, dst, Vs // 50, X, *w, dY, agg, "leaky", 0.2)
+    src, dst, X, w, dY = setup(Vs, Es)
     n, t0 = 0, time.perf_counter()
     while True:
-        oracle.reference_cpu_step(src, dst, Vs, X, *w, dY, args.agg, "leaky", 0.2)
+        oracle.reference_cpu_step(src, dst, Vs, X, *w, dY, agg, "leaky", 0.2)
         n += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or n >= 20:
+        if el >= args.cpu_seconds or n >= 5:
             break
     cpu_model = platform.processor() or "unknown"
     try:
@@ -116,96 +189,16 @@ def cpu_baseline(args, H):
                     break
     except OSError:
         pass
-    return {"value": Es * n / el, "unit": "edges/s", "cores": cores, "kind": "port",
-            "sample": f"Chung-Lu alpha=0.8 V={Vs} E={Es} H={H} {args.agg} LeakyReLU(0.2), "
-                      f"{n} fwd+bwd steps in {el:.1f}s (oracle.reference_cpu_step: DGL edge-UDF dataflow, torch CPU autograd)",
+    return {"value": round(Es * n / el, 1), "unit": "edges/s", "cores": cores, "kind": "port",
+            "sample": f"{args.cpu_graph}: Chung-Lu alpha={alpha} V={Vs} E={Es} H={H} {agg} LeakyReLU(0.2), "
+                      f"{n} full fwd+bwd step(s) in {el:.1f}s, unchunked (oracle.reference_cpu_step: DGL edge-UDF "
+                      f"dataflow, torch CPU autograd)",
             "cpu_model": cpu_model}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", local % max(ndev, 1))     # one rank per GPU (wraps only in rehearsals)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-
-    from sirgcn import SIRConv, _native, linalg
-    if args.torch_gemm:
-        linalg.USE_NATIVE = False
-    from sirgcn.graph import DEFAULT_CHUNK
-    from sirgcn.synth import NAMED, powerlaw_edges
-    H = args.hidden
-    V, E, alpha = NAMED[args.graph]
-    src, dst = powerlaw_edges(V, E, alpha, seed=0)
-
-    torch.manual_seed(4)
-    conv = SIRConv(H, H, H, nn.LeakyReLU(0.2, inplace=True), 0, agg_type=args.agg).to(dev)
-    if args.chunk:
-        conv.chunk = args.chunk
-    gen = torch.Generator().manual_seed(3)
-    X_full = torch.randn(V, H, generator=gen)
-    dY_full = torch.randn(V, H, generator=torch.Generator().manual_seed(5))
-
-    dconv = None
-    if world == 1 and not args.force_dist:
-        from sirgcn import Graph
-        g = Graph(src, dst, V)
-        X = X_full.to(dev).requires_grad_(True)
-        dY = dY_full.to(dev)
-        layer = lambda: conv(g, X)
-        rows_local, edges_local = V, E
-        rows_src = V
-    else:
-        from sirgcn.dist import DistGraph, DistSIRConv
-        dg = DistGraph.from_global(src, dst, V, rank, world, dev, chunk=args.chunk or DEFAULT_CHUNK)
-        dconv = DistSIRConv(conv)
-        r0, r1 = dg.row_begin, dg.row_end
-        X = X_full[r0:r1].to(dev).requires_grad_(True)
-        dY = dY_full[r0:r1].to(dev)
-        layer = lambda: dconv(dg, X)
-        rows_local, edges_local = r1 - r0, dg.num_local_edges
-        rows_src = dg.n_ext
-    del X_full, dY_full
-
-    def step():
-        conv.zero_grad(set_to_none=True)
-        X.grad = None
-        Y = layer()
-        Y.backward(dY)
-        if dconv is not None:
-            dconv.allreduce_grads()
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    timing = _native.enable_timing(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    _native.enable_timing(False)
-    el_t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = el_t.item()
-    ms = 1e3 * el / args.steps
-
-    from sirgcn.conv import EdgeAggregate
-    masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY))
+# ------------------------------------------------------------------------------ timing
+def kernel_table(timing, rows_of, edges, H, agg, masked, s):
+    import torch  # noqa: F401
     kernels, gemm = {}, {}
     for name, evs in timing.items():
         t = sum(a.elapsed_time(b) for a, b, _ in evs) / len(evs)    # ms per launch
@@ -216,58 +209,296 @@ def main():
             gemm[name] = {"ms": round(t, 4), "launches": len(evs), "flops": fl,
                           "TFLOPs": round(fl / (t * 1e-3) / 1e12, 1)}
             continue
-        bytes_ = edge_pass_bytes(name, rows_local if name != "sir_edge_agg_bwd_src" else rows_src, edges_local, H,
-                                 args.agg, masked)
-        kernels[name] = {"ms": round(t, 4), "launches": len(evs), "bytes": bytes_,
-                         "GBps": round(bytes_ / (t * 1e-3) / 1e9, 1)}
-    dom = max(kernels, key=lambda k: kernels[k]["ms"])
-    traffic = None
-    pmc_file = args.pmc_file or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.graph}.json")
-    try:
-        with open(pmc_file) as f:
-            pmc = json.load(f)
-        rec = pmc.get("kernels", {}).get(dom)
-        if (rec and world == 1 and pmc.get("graph") == args.graph and pmc.get("agg") == args.agg
-                and pmc.get("H") == H):
-            traffic = rec["hbm_bytes_per_launch"]      # L2<->fabric bytes (Infinity-Cache hits included)
-    except (OSError, ValueError):
-        pass
-    d = kernels[dom]
-    roofline = {"bound": "hbm", "kernel": dom, "backward_mode": "sign-mask" if masked else "recompute", "achieved": d["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(d["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes": d["bytes"], "ms_per_launch": d["ms"], "all_kernels": kernels}
+        if not name.startswith("sir_edge_agg"):
+            kernels[name] = {"ms": round(t, 4), "launches": len(evs)}
+            continue
+        b = edge_pass_bytes(name, rows_of(name), edges, H, agg, masked, s=s)
+        kernels[name] = {"ms": round(t, 4), "launches": len(evs), "design_bytes": b,
+                         "GBps": round(b / (t * 1e-3) / 1e9, 1)}
+    return kernels, gemm
 
+
+def timed_loop(step, steps, warmup, world, dist, dev):
+    import torch
+    from sirgcn import _native
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    timing = _native.enable_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    _native.enable_timing(False)
+    return el, timing
+
+
+def max_over_ranks(x, world, dist, dev):
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+# ------------------------------------------------------------------------------ main
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
+
+    import torch
+    import torch.distributed as dist
+    from torch import nn
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    rehearsal = not torch.cuda.is_available()
+    if rehearsal:
+        if args.dist_backend != "gloo" or args.workload != "cfg4":
+            raise SystemExit("no GPU: only the cfg4 edge-cut plumbing can be rehearsed (--dist-backend gloo)")
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, min(4, os.cpu_count() // max(world, 1))))
+    else:
+        ndev = torch.cuda.device_count()
+        dev = torch.device("cuda", local % max(ndev, 1))     # one rank per GPU (wraps only in rehearsals)
+        torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    if args.workload == "cfg4":
+        out = run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn)
+    else:
+        out = run_stack(args, world, rank, dev, torch, dist)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
+    from sirgcn import SIRConv, _native, linalg
+    if args.torch_gemm:
+        linalg.USE_NATIVE = False
+    from sirgcn.graph import DEFAULT_CHUNK
+    from sirgcn.synth import NAMED, powerlaw_edges
+    H = args.hidden
+    dtn = args.dtype or "f32"
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[dtn]
+    V, E, alpha = NAMED[args.graph]
+    src, dst = powerlaw_edges(V, E, alpha, seed=0)
+
+    torch.manual_seed(4)
+    conv = SIRConv(H, H, H, nn.LeakyReLU(0.2, inplace=True), 0, agg_type=args.agg).to(dev)
+    if args.chunk:
+        conv.chunk = args.chunk
+    X_full = torch.randn(V, H, generator=torch.Generator().manual_seed(3))
+    dY_full = torch.randn(V, H, generator=torch.Generator().manual_seed(5))
+
+    dconv = None
+    if world == 1 and not args.force_dist and not rehearsal:
+        from sirgcn import Graph
+        g = Graph(src, dst, V)
+        X = X_full.to(dev).requires_grad_(True)
+        dY = dY_full.to(dev)
+        layer = lambda: conv(g, X)
+        rows_local, edges_local, rows_src = V, E, V
+    else:
+        from sirgcn.dist import DistGraph, DistSIRConv
+        backend = None
+        if rehearsal:          # test-only CPU edge passes (tests/cpu_edge_backend.py): plumbing, not a measurement
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import cpu_edge_backend as backend
+        dg = DistGraph.from_global(src, dst, V, rank, world, dev, chunk=args.chunk or DEFAULT_CHUNK)
+        dconv = DistSIRConv(conv, backend=backend)
+        r0, r1 = dg.row_begin, dg.row_end
+        X = X_full[r0:r1].to(dev).requires_grad_(True)
+        dY = dY_full[r0:r1].to(dev)
+        layer = lambda: dconv(dg, X)
+        rows_local, edges_local, rows_src = r1 - r0, dg.num_local_edges, dg.n_ext
+    del X_full, dY_full
+
+    def step():
+        conv.zero_grad(set_to_none=True)
+        X.grad = None
+        if dt != torch.float32:
+            with torch.autocast(dev.type, dtype=dt):
+                Y = layer()
+        else:
+            Y = layer()
+        Y.backward(dY.to(Y.dtype))
+        if dconv is not None:
+            dconv.allreduce_grads()
+
+    if rehearsal:
+        el, timing = rehearsal_loop(step, args.steps, args.warmup, world, dist)
+    else:
+        el, timing = timed_loop(step, args.steps, args.warmup, world, dist, dev)
+    el = max_over_ranks(el, world, dist, dev if args.dist_backend == "nccl" and not rehearsal else "cpu")
+    ms = 1e3 * el / args.steps
     out = {"metric": METRIC, "value": round(E / (el / args.steps), 1), "unit": "edges/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-           "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-           "config": {"workload": f"{args.graph}: Chung-Lu power-law V={V} E={E} alpha={alpha}; 1 SIRConv layer "
-                                  f"d_in=H=d_out={H}, agg={args.agg}, LeakyReLU(0.2); fwd+bwd incl. projections",
+           "scaling": "strong", "vs_baseline": None, "dtype": dtn, "data": "synthetic",
+           "config": {"workload": f"cfg4 {args.graph}: Chung-Lu power-law V={V} E={E} alpha={alpha}; 1 SIRConv layer "
+                                  f"d_in=H=d_out={H}, agg={args.agg}, LeakyReLU(0.2), {dtn}"
+                                  f"{' (autocast)' if dtn != 'f32' else ''}; fwd+bwd incl. projections",
                       "graph": args.graph, "V": V, "E": E, "hidden": H, "agg": args.agg,
                       "parallelism": f"edge-cut dst-range x{world}, sparse halo all-to-all" if world > 1
-                      else "single GPU"},
-           "roofline": roofline}
-    if gemm:   # projections (split-fp16 MFMA): fp32-equivalent flops; raw fp16 MFMA work is 3x that
-        fl = sum(g["flops"] * g["launches"] for g in gemm.values()) / args.steps
-        tg = sum(g["ms"] * g["launches"] for g in gemm.values()) / args.steps
-        out["projections"] = {"bound": "mfma", "ms_per_step": round(tg, 3), "flops_per_step": fl,
-                              "achieved_fp32_equiv_TFLOPs": round(fl / (tg * 1e-3) / 1e12, 1),
-                              "fp16_mfma_util": round(3 * fl / (tg * 1e-3) / FP16_PEAK_FLOPS, 4),
-                              "vs_fp32_peak": round(fl / (tg * 1e-3) / (FP32_PEAK_TFLOPS * 1e12), 3),
-                              "kernels": gemm}
-    if dconv is not None:     # halo exchange volume per rank (rows of H fp32), max over ranks
+                      else "single GPU"}}
+    if rehearsal:
+        out["rehearsal"] = ("CPU gloo rehearsal of the launcher / partition / exchange plumbing; edge passes on "
+                            "the test-only CPU backend: NOT a measurement")
+        out["n_gpus"] = world
+        return out
+
+    from sirgcn.conv import EdgeAggregate
+    s = SIZEOF[dtn]
+    masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY))
+    kernels, gemm = kernel_table(timing, lambda n: rows_src if n == "sir_edge_agg_bwd_src" else rows_local,
+                                 edges_local, H, args.agg, masked, s)
+    out["roofline"] = roofline_fwd(args, kernels, rows_local, edges_local, rows_src, H, s, world)
+    out["roofline"]["all_kernels"] = kernels
+    if gemm:
+        out["projections"] = projections(gemm, args.steps)
+    if dconv is not None:     # halo exchange volume per rank (rows of H), max over ranks
         ex = torch.tensor([dg.n_halo, int(dg.send_idx.numel()), edges_local], dtype=torch.float64,
                           device=dev if args.dist_backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(ex, op=dist.ReduceOp.MAX)
         out["exchange"] = {"halo_rows_max": int(ex[0]), "send_rows_max": int(ex[1]), "local_edges_max": int(ex[2]),
-                           "bytes_per_direction_max": int(ex[0]) * H * 4,
+                           "bytes_per_direction_max": int(ex[0]) * H * s,
                            "dense_allgather_rows": V - min(dg.bounds[i + 1] - dg.bounds[i] for i in range(world))}
+    if world == 1 and not args.no_aux:
+        out["roofline"]["copy_GBps_measured"] = copy_rate(dev)
+        if not args.torch_gemm and dtn == "f32":        # IEEE fp32 projections (torch / hipBLASLt) beside it
+            linalg.USE_NATIVE = False
+            el2, _ = timed_loop(step, max(3, args.steps // 4), 2, 1, dist, dev)
+            linalg.USE_NATIVE = True
+            out["ms_per_step_torch_fp32_gemm"] = round(1e3 * el2 / max(3, args.steps // 4), 3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, H)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    return out
+
+
+def rehearsal_loop(step, steps, warmup, world, dist):
+    for _ in range(warmup):
+        step()
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    return el, {}
+
+
+def roofline_fwd(args, kernels, V, E, V_src, H, s, world):
+    """The forward edge-aggregation kernel against HBM: §8(d) algorithmic bytes / HIP-event time."""
+    k = kernels["sir_edge_agg_fwd"]
+    t = k["ms"] * 1e-3
+    alg = fwd_algorithmic_bytes(V, E, H, s)
+    uniq = fwd_unique_bytes(V_src, V, E, H, s)
+    ach = alg / t / 1e9
+    traffic = None
+    pmc_file = args.pmc_file or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.graph}.json")
+    try:
+        with open(pmc_file) as f:
+            pmc = json.load(f)
+        rec = pmc.get("kernels", {}).get("sir_edge_agg_fwd")
+        if (rec and world == 1 and pmc.get("graph") == args.graph and pmc.get("agg") == args.agg
+                and pmc.get("H") == H and pmc.get("dtype", "f32") == (args.dtype or "f32")):
+            traffic = rec["hbm_bytes_per_launch"]      # L2<->fabric bytes (Infinity-Cache hits included)
+    except (OSError, ValueError):
+        pass
+    frac = ach / HBM_PEAK_GBS
+    if frac > 1.0:   # algorithmic bytes charge every gathered row to HBM; hub rows hit the caches
+        frac_note = "algorithmic rate above the HBM peak: cache-served gathers (see frac_unique / frac_counter)"
+    else:
+        frac_note = None
+    out = {"bound": "hbm", "kernel": "sir_edge_agg_fwd (k_edge<FWD> + k_combine)",
+           "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(min(frac, 1.0), 4),
+           "traffic": traffic, "algorithmic_bytes": alg, "ms_per_launch": k["ms"],
+           "bytes_formula": "SURVEY 8(d): E*(s_i + H*s) + V*(2*H*s + s_i)",
+           "unique_bytes": uniq, "frac_unique": round(uniq / t / 1e9 / HBM_PEAK_GBS, 4),
+           "frac_counter": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None}
+    if frac_note:
+        out["note"] = frac_note
+    return out
+
+
+def projections(gemm, steps):
+    fl = sum(g["flops"] * g["launches"] for g in gemm.values()) / steps
+    tg = sum(g["ms"] * g["launches"] for g in gemm.values()) / steps
+    return {"bound": "mfma", "ms_per_step": round(tg, 3), "flops_per_step": fl,
+            "achieved_fp32_equiv_TFLOPs": round(fl / (tg * 1e-3) / 1e12, 1),
+            "fp16_mfma_util": round(3 * fl / (tg * 1e-3) / FP16_PEAK_FLOPS, 4),
+            "vs_fp32_peak": round(fl / (tg * 1e-3) / (FP32_PEAK_TFLOPS * 1e12), 3),
+            "kernels": gemm}
+
+
+def run_stack(args, world, rank, dev, torch, dist):
+    """BASELINE configs 1/2/3/5: the reference models' layer loops (sirgcn.workloads)."""
+    from sirgcn import GraphNorm, SIRConv, _native
+    from sirgcn.workloads import CONFIGS, DTYPES, make_graph, make_inputs, make_stack
+    name = args.workload
+    c = CONFIGS[name]
+    dtn = args.dtype or c["dtype"]
+    dt = DTYPES[dtn]
+    if world > 1 and name != "cfg5":
+        raise SystemExit(f"{name} is a single-GPU workload (cfg5 is the data-parallel one, cfg4 the edge-cut)")
+    g = make_graph(name, rank=rank)
+    stack = make_stack(name, SIRConv, GraphNorm).to(dev)
+    model = stack
+    if world > 1:           # DP replicas: a different batch per rank, RCCL gradient all-reduce
+        model = torch.nn.parallel.DistributedDataParallel(stack, device_ids=[dev.index])
+    X, dY = make_inputs(name, g.num_nodes(), dev, seed=3 + rank)
+    X.requires_grad_(True)
+
+    def step():
+        model.zero_grad(set_to_none=True)
+        X.grad = None
+        if dt != torch.float32:
+            with torch.autocast("cuda", dtype=dt):
+                Y = model(g, X)
+        else:
+            Y = model(g, X)
+        Y.backward(dY.to(Y.dtype))
+
+    el, timing = timed_loop(step, args.steps, args.warmup, world, dist, dev)
+    el = max_over_ranks(el, world, dist, dev)
+    L, H, E, V = c["layers"], c["hidden"], g.num_edges(), g.num_nodes()
+    tot = torch.tensor([E, V, g.batch_size], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    E_all, V_all, B_all = (int(x) for x in tot.tolist())
+    from sirgcn.conv import EdgeAggregate
+    masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY))
+    kernels, gemm = kernel_table(timing, lambda n: V, E, H, c["agg"], masked, SIZEOF[dtn])
+    out = {"metric": "layer-edges/sec SIRConv stack fwd+bwd (E x layers / step time)",
+           "value": round(E_all * L / (el / args.steps), 1), "unit": "edges/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+           "higher_is_better": True, "scaling": "weak" if name == "cfg5" else "strong", "vs_baseline": None,
+           "dtype": dtn, "data": "synthetic",
+           "config": {"workload": f"{name}: {CONFIGS[name]} V={V} E={E} graphs={g.batch_size}"
+                                  f"{' per rank, DDP over RCCL' if world > 1 else ''}",
+                      "graphs_per_s": round(B_all / (el / args.steps), 1), "V_total": V_all, "E_total": E_all,
+                      "parallelism": f"data-parallel x{world}" if world > 1 else "single GPU"},
+           "kernels": kernels}
+    if gemm:
+        out["projections"] = projections(gemm, args.steps)
+    return out
 
 
 if __name__ == "__main__":

@@ -37,14 +37,20 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 4
+#define SIR_ABI_VERSION 5
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
 /* sigma: the `activation` callable of conv.py:32,45 (ReLU, LeakyReLU(slope), GELU erf / tanh) */
 enum { SIR_ACT_IDENTITY = 0, SIR_ACT_RELU = 1, SIR_ACT_LEAKY_RELU = 2, SIR_ACT_GELU = 3, SIR_ACT_GELU_TANH = 4 };
-/* storage dtype of the gathered node features */
-enum { SIR_DTYPE_F32 = 0, SIR_DTYPE_BF16 = 1 };
+/* Storage dtype of every feature matrix of an edge-pass call (Q, K, G, S, dQ, dK, Gm): fp32, or the
+ * 16-bit types the reference's AMP path produces (torch.amp.autocast, heterophilous-datasets/train.py:75;
+ * fp16 is autocast's CUDA default, bf16 is BASELINE config 2).  16-bit values are widened to fp32 on
+ * load; sigma, sigma', the norm product and the accumulation run in fp32 (the reference promotes its
+ * messages to fp32 before the reduction) and each output is rounded once (RNE).
+ * 16-bit storage needs H % 4 == 0 and leading dimensions that are multiples of 4 (8-B aligned rows).
+ * Norms and the `partial` workspace are fp32 in every mode. */
+enum { SIR_DTYPE_F32 = 0, SIR_DTYPE_BF16 = 1, SIR_DTYPE_F16 = 2 };
 /* error codes */
 enum { SIR_OK = 0, SIR_EINVAL = 1, SIR_EUNSUPPORTED = 2, SIR_ELAUNCH = 3 };
 
@@ -96,13 +102,15 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      const void* Q, int64_t ldq, const void* K, int64_t ldk,
                      const float* norm_row, const float* norm_col,
                      int agg, int act, float slope,
-                     float* S, int64_t lds, uint64_t* mask_out, float* partial, void* stream);
+                     void* S, int64_t lds, uint64_t* mask_out, float* partial, void* stream);
 
 /*
  * Backward, destination pass — the Q half of autograd through conv.py:45,63.
  *   g = G[v] (MEAN: G[v] / max(deg v, 1)),  t_e = g * c_e (SYM) or g,
  *   dQ[v] = sum_{e in row v} sigma'(Q[v] + K[u]) * t_e   (sigma' as torch's backward).
  *   If MEAN and Gm != NULL, the divided rows g are also written to Gm (for the src pass).
+ *   16-bit storage: g is rounded to the storage dtype before use (the values written to Gm), so
+ *   both passes see the same g.
  *   mask != NULL selects the sign-mask mode: sigma'(z) is read from the forward's mask and
  *   Q, K are not touched (may be NULL); results are bit-identical to the recompute mode.
  */
@@ -112,10 +120,10 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
                          int64_t H, int dtype,
                          const void* Q, int64_t ldq, const void* K, int64_t ldk,
                          const uint64_t* mask,
-                         const float* G, int64_t ldg,
+                         const void* G, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
-                         float* dQ, int64_t lddq, float* Gm, int64_t ldgm,
+                         void* dQ, int64_t lddq, void* Gm, int64_t ldgm,
                          float* partial, void* stream);
 
 /*
@@ -133,10 +141,10 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          int64_t H, int dtype,
                          const void* K, int64_t ldk, const void* Q, int64_t ldq,
                          const uint64_t* mask,
-                         const float* Gd, int64_t ldg,
+                         const void* Gd, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
-                         float* dK, int64_t lddk, float* partial, void* stream);
+                         void* dK, int64_t lddk, float* partial, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Edge-materialised path: agg_type='max' (conv.py:46-47 + DGL max reduce) and sigma callables the
@@ -234,6 +242,10 @@ int sir_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int32_t*
  * BLAS to another).  Elements more than 2^29 below their row's maximum lose relative precision
  * (absolute error <= 2^-40 of that maximum).
  * ------------------------------------------------------------------------------------------- */
+
+/* Largest leading dimension (elements) of a GEMM data operand: a 256-row tile is addressed with
+ * 32-bit byte offsets.  Larger strides are rejected with SIR_EINVAL. */
+#define SIR_GEMM_MAX_LD (1 << 20)
 
 /* Weight operand B [N, K] for sir_gemm_nt: B[n][k] = W[n*ldw + k] (trans = 0, an nn.Linear
  * weight used as x W^T) or W[k*ldw + n] (trans = 1, x W).  packed: sir_gemm_pack_bytes(N, K)

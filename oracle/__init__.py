@@ -14,3 +14,4 @@ from .sirconv_oracle import (  # noqa: F401
 )
 from .graphnorm_oracle import graph_norm_fwd, graph_norm_bwd  # noqa: F401
 from .sireconv_oracle import sire_reference_step  # noqa: F401
+from .modules_oracle import SIRConvRef, GraphNormRef  # noqa: F401

@@ -25,7 +25,8 @@ int check_common(const char* fn, const int32_t* rowptr, const int32_t* col, cons
                  int64_t n_items, const int32_t* splits, int64_t n_splits, int64_t H, int dtype,
                  int agg, int act, const float* norm_row, const float* norm_col, const void* out,
                  const float* partial) {
-    if (dtype != SIR_DTYPE_F32) return fail(SIR_EUNSUPPORTED, fn, "only SIR_DTYPE_F32 storage is implemented");
+    if (dtype != SIR_DTYPE_F32 && dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16)
+        return fail(SIR_EINVAL, fn, "dtype must be SIR_DTYPE_F32, _BF16 or _F16");
     if (agg < SIR_AGG_SUM || agg > SIR_AGG_SYM) return fail(SIR_EINVAL, fn, "agg must be SUM, MEAN or SYM");
     if (act < SIR_ACT_IDENTITY || act > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown activation");
     if (H <= 0 || H > 1024) return fail(SIR_EINVAL, fn, "H must be in [1, 1024]");
@@ -99,7 +100,7 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      const void* Q, int64_t ldq, const void* K, int64_t ldk,
                      const float* norm_row, const float* norm_col,
                      int agg, int act, float slope,
-                     float* S, int64_t lds, uint64_t* mask_out, float* partial, void* stream) {
+                     void* S, int64_t lds, uint64_t* mask_out, float* partial, void* stream) {
     const char* fn = "sir_edge_agg_fwd";
     int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, S, partial);
@@ -109,14 +110,14 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
     if (mask_out != nullptr && (rc = check_mask(fn, H, act))) return rc;
     sir::EdgeArgs a{};
     a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items;
-    a.R = static_cast<const float*>(Q); a.ldr = ldq;
-    a.C = static_cast<const float*>(K); a.ldc = ldk;
+    a.R = Q; a.ldr = ldq;
+    a.C = K; a.ldc = ldk;
     a.G = nullptr; a.ldg = H;
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = S; a.ldo = lds; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
     a.mask_out = mask_out;
     const char* why = nullptr;
-    hipError_t err = sir::run_edge(sir::MODE_FWD, a, agg, act, splits, n_splits, S, lds,
+    hipError_t err = sir::run_edge(sir::MODE_FWD, dtype, a, agg, act, splits, n_splits, S, lds,
                                    agg == SIR_AGG_MEAN, static_cast<hipStream_t>(stream), &why);
     return finish(fn, err, why);
 }
@@ -127,10 +128,10 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
                          int64_t H, int dtype,
                          const void* Q, int64_t ldq, const void* K, int64_t ldk,
                          const uint64_t* mask,
-                         const float* G, int64_t ldg,
+                         const void* G, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
-                         float* dQ, int64_t lddq, float* Gm, int64_t ldgm,
+                         void* dQ, int64_t lddq, void* Gm, int64_t ldgm,
                          float* partial, void* stream) {
     const char* fn = "sir_edge_agg_bwd_dst";
     int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
@@ -147,15 +148,15 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
     }
     sir::EdgeArgs a{};
     a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items;
-    a.R = static_cast<const float*>(Q); a.ldr = mask ? H : ldq;
-    a.C = static_cast<const float*>(K); a.ldc = mask ? H : ldk;
+    a.R = Q; a.ldr = mask ? H : ldq;
+    a.C = K; a.ldc = mask ? H : ldk;
     a.G = G; a.ldg = ldg;
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = dQ; a.ldo = lddq; a.partial = partial;
     a.Gm = (agg == SIR_AGG_MEAN) ? Gm : nullptr; a.ldgm = Gm ? ldgm : H;
     a.mask_in = mask;
     const char* why = nullptr;
-    hipError_t err = sir::run_edge(sir::MODE_BWD_DST, a, agg, act, splits, n_splits, dQ, lddq, false,
+    hipError_t err = sir::run_edge(sir::MODE_BWD_DST, dtype, a, agg, act, splits, n_splits, dQ, lddq, false,
                                    static_cast<hipStream_t>(stream), &why);
     return finish(fn, err, why);
 }
@@ -166,10 +167,10 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          int64_t H, int dtype,
                          const void* K, int64_t ldk, const void* Q, int64_t ldq,
                          const uint64_t* mask,
-                         const float* Gd, int64_t ldg,
+                         const void* Gd, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
-                         float* dK, int64_t lddk, float* partial, void* stream) {
+                         void* dK, int64_t lddk, float* partial, void* stream) {
     const char* fn = "sir_edge_agg_bwd_src";
     int rc = check_common(fn, rowptr_s, col_s, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, dK, partial);
@@ -185,14 +186,14 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
     }
     sir::EdgeArgs a{};
     a.rowptr = rowptr_s; a.col = col_s; a.items = items; a.n_items = n_items;
-    a.R = static_cast<const float*>(K); a.ldr = mask ? H : ldk;
-    a.C = static_cast<const float*>(Q); a.ldc = mask ? H : ldq;
+    a.R = K; a.ldr = mask ? H : ldk;
+    a.C = Q; a.ldc = mask ? H : ldq;
     a.G = Gd; a.ldg = ldg;
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = dK; a.ldo = lddk; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
     a.mask_in = mask; a.perm = perm_s;
     const char* why = nullptr;
-    hipError_t err = sir::run_edge(sir::MODE_BWD_SRC, a, agg, act, splits, n_splits, dK, lddk, false,
+    hipError_t err = sir::run_edge(sir::MODE_BWD_SRC, dtype, a, agg, act, splits, n_splits, dK, lddk, false,
                                    static_cast<hipStream_t>(stream), &why);
     return finish(fn, err, why);
 }
@@ -364,6 +365,8 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
     if ((M + 255) / 256 * ((N + 127) / 128) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
     if (K % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldc % 4 != 0 || lda < K || ldc < N)
         return fail(SIR_EINVAL, fn, "K, N, lda, ldc must be multiples of 4 (lda >= K, ldc >= N)");
+    // a 256-row tile of A is addressed by one buffer resource with 32-bit signed byte offsets
+    if (lda > SIR_GEMM_MAX_LD) return fail(SIR_EINVAL, fn, "lda too large (256 rows must span < 2^31 bytes)");
     if (M > 0 && (A == nullptr || C == nullptr || packed == nullptr)) return fail(SIR_EINVAL, fn, "NULL buffer");
     if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(bias) |
           reinterpret_cast<uintptr_t>(packed)) & 15u) != 0)
@@ -382,6 +385,8 @@ int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_
     const char* fn = "sir_gemm_tn";
     if (R < 0 || M <= 0 || N <= 0 || M > 65536 || N > 65536) return fail(SIR_EINVAL, fn, "bad shape");
     if (lda < M || ldb < N || ldc < N) return fail(SIR_EINVAL, fn, "leading dimension too small");
+    if (lda > SIR_GEMM_MAX_LD || ldb > SIR_GEMM_MAX_LD)
+        return fail(SIR_EINVAL, fn, "lda/ldb too large (a 32-row chunk must span < 2^31 bytes)");
     if (C == nullptr || workspace == nullptr || (R > 0 && (A == nullptr || B == nullptr)))
         return fail(SIR_EINVAL, fn, "NULL buffer");
     if (workspace_bytes < sir::gemm_tn_workspace(R, M, N)) return fail(SIR_EINVAL, fn, "workspace too small");

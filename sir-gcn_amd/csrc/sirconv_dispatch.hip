@@ -102,17 +102,33 @@ hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, fl
     return hipGetLastError();
 }
 
-template <bool MEAN_DIV>
+template <int ST, bool MEAN_DIV>
 static hipError_t launch_combine(const int32_t* splits, int64_t n, const float* partial, int H,
-                                 float* out, int64_t ldo, int vw, hipStream_t st) {
+                                 void* out, int64_t ldo, int vw, hipStream_t st) {
     if (n == 0) return hipSuccess;
+    TP<ST>* o = static_cast<TP<ST>*>(out);
     if (vw == 4)
-        hipLaunchKernelGGL((k_combine<MEAN_DIV, 4>), dim3((unsigned)n), dim3(1024), 0, st,
-                           reinterpret_cast<const int4*>(splits), partial, H, out, ldo);
+        hipLaunchKernelGGL((k_combine<ST, MEAN_DIV, 4>), dim3((unsigned)n), dim3(1024), 0, st,
+                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo);
     else
-        hipLaunchKernelGGL((k_combine<MEAN_DIV, 1>), dim3((unsigned)n), dim3(1024), 0, st,
-                           reinterpret_cast<const int4*>(splits), partial, H, out, ldo);
+        hipLaunchKernelGGL((k_combine<ST, MEAN_DIV, 1>), dim3((unsigned)n), dim3(1024), 0, st,
+                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo);
     return hipGetLastError();
+}
+
+template <int ST>
+static hipError_t run_edge_t(int mode, const EdgeArgs& a, int agg, int act, Shape s,
+                             const int32_t* splits, int64_t n_splits, void* out_final, int64_t ld_final,
+                             bool mean_div, hipStream_t st) {
+    hipError_t err;
+    switch (mode) {
+        case MODE_FWD: err = launch_edge_pass<ST, MODE_FWD>(a, agg, act, s, st); break;
+        case MODE_BWD_DST: err = launch_edge_pass<ST, MODE_BWD_DST>(a, agg, act, s, st); break;
+        default: err = launch_edge_pass<ST, MODE_BWD_SRC>(a, agg, act, s, st); break;
+    }
+    if (err != hipSuccess || n_splits == 0) return err;
+    return mean_div ? launch_combine<ST, true>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st)
+                    : launch_combine<ST, false>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st);
 }
 
 hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
@@ -123,7 +139,7 @@ hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowpt
     return hipGetLastError();
 }
 
-static bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+static bool aligned_to(const void* p, uintptr_t b) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & (b - 1)) == 0; }
 
 // Vector width 4 needs every row start 16-B aligned.
 bool pick_shape(int H, bool vec4_ok, Shape* s) {
@@ -146,11 +162,13 @@ bool pick_shape(int H, bool vec4_ok, Shape* s) {
     return s->nv <= 4;
 }
 
-hipError_t run_edge(int mode, const EdgeArgs& a, int agg, int act,
-                    const int32_t* splits, int64_t n_splits, float* out_final, int64_t ld_final,
+hipError_t run_edge(int mode, int dtype, const EdgeArgs& a, int agg, int act,
+                    const int32_t* splits, int64_t n_splits, void* out_final, int64_t ld_final,
                     bool mean_div, hipStream_t st, const char** why) {
-    const bool v4 = aligned16(a.R) && aligned16(a.C) && aligned16(a.G) && aligned16(a.out) &&
-                    aligned16(a.partial) && aligned16(a.Gm) &&
+    // 4-wide vectors need every feature row start aligned to 4 elements (16 B fp32, 8 B 16-bit)
+    const uintptr_t vb = (dtype == ST_F32) ? 16 : 8;
+    const bool v4 = aligned_to(a.R, vb) && aligned_to(a.C, vb) && aligned_to(a.G, vb) && aligned_to(a.out, vb) &&
+                    aligned_to(a.partial, 16) && aligned_to(a.Gm, vb) &&
                     (a.ldr % 4 == 0) && (a.ldc % 4 == 0) && (a.ldg % 4 == 0) && (a.ldo % 4 == 0) &&
                     (a.ldgm % 4 == 0);
     Shape s;
@@ -158,18 +176,15 @@ hipError_t run_edge(int mode, const EdgeArgs& a, int agg, int act,
         *why = "unsupported hidden size (H must be <= 1024 with H%4==0 and 16-B aligned rows, else <= 256)";
         return hipErrorInvalidValue;
     }
-    hipError_t err;
-    switch (mode) {
-        case MODE_FWD: err = launch_mode_fwd(a, agg, act, s, st); break;
-        case MODE_BWD_DST: err = launch_mode_bwd_dst(a, agg, act, s, st); break;
-        default: err = launch_mode_bwd_src(a, agg, act, s, st); break;
+    if (dtype != ST_F32 && s.vw != 4) {
+        *why = "bf16/fp16 storage needs H % 4 == 0 and 8-B aligned rows (leading dimensions multiples of 4)";
+        return hipErrorInvalidValue;
     }
-    if (err != hipSuccess) return err;
-    if (n_splits > 0) {
-        err = mean_div ? launch_combine<true>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st)
-                       : launch_combine<false>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st);
+    switch (dtype) {
+        case ST_BF16: return run_edge_t<ST_BF16>(mode, a, agg, act, s, splits, n_splits, out_final, ld_final, mean_div, st);
+        case ST_F16: return run_edge_t<ST_F16>(mode, a, agg, act, s, splits, n_splits, out_final, ld_final, mean_div, st);
+        default: return run_edge_t<ST_F32>(mode, a, agg, act, s, splits, n_splits, out_final, ld_final, mean_div, st);
     }
-    return err;
 }
 
 }  // namespace sir

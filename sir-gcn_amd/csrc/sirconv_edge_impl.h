@@ -77,6 +77,35 @@ __device__ __forceinline__ float dsig(float z, float t, float slope) {
     }
 }
 
+// ------------------------------------------------------------------------------ storage dtype
+// Feature rows (Q, K, G, S, dQ, dK, Gm) are stored as fp32, bf16 or fp16 (SIR_DTYPE_*; the AMP
+// path of the reference, heterophilous-datasets/train.py:75, runs the layer under autocast).  Every
+// value is converted to fp32 on load; sigma, sigma', the norm product and the accumulation run in
+// fp32 (the reference accumulates its promoted fp32 messages), and results are
+// rounded once (RNE) on store.  Partial rows of split items stay fp32.
+template <int ST> struct Stor { typedef float T; };
+template <> struct Stor<ST_BF16> { typedef __bf16 T; };
+template <> struct Stor<ST_F16> { typedef _Float16 T; };
+
+typedef unsigned int sir_u2 __attribute__((ext_vector_type(2)));
+
+template <int ST>
+__device__ __forceinline__ float h2f(uint32_t bits16) {
+    if constexpr (ST == ST_BF16) return __uint_as_float(bits16 << 16);
+    else return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+}
+template <int ST>
+__device__ __forceinline__ uint32_t f2h(float x) {
+    if constexpr (ST == ST_BF16) return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x);
+    else return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x);
+}
+// fp32 value rounded to the storage precision (what a store + reload yields)
+template <int ST>
+__device__ __forceinline__ float round_st(float x) {
+    if constexpr (ST == ST_F32) return x;
+    else return h2f<ST>(f2h<ST>(x));
+}
+
 // ------------------------------------------------------------------------------ vectors
 // Cache-policy experiment knobs (tools/edge_ab.py builds them as separate libraries):
 //   SIR_NT_STREAM = 1: non-temporal loads/stores for the once-touched row-side streams
@@ -121,13 +150,49 @@ __device__ __forceinline__ void vstore_p(float* __restrict__ p, const float (&s)
     }
 }
 
+// typed loads / stores: fp32 as above; 16-bit storage as one 8-B access per 4 values
+template <int ST, int VW, bool NT>
+__device__ __forceinline__ void tload_p(float (&d)[VW], const typename Stor<ST>::T* __restrict__ p) {
+    if constexpr (ST == ST_F32) {
+        vload_p<VW, NT>(d, p);
+    } else if constexpr (VW == 4) {
+        const sir_u2* q = reinterpret_cast<const sir_u2*>(p);
+        const sir_u2 t = NT ? __builtin_nontemporal_load(q) : *q;
+        d[0] = h2f<ST>(t.x & 0xffffu); d[1] = h2f<ST>(t.x >> 16);
+        d[2] = h2f<ST>(t.y & 0xffffu); d[3] = h2f<ST>(t.y >> 16);
+    } else {
+        const uint16_t* q = reinterpret_cast<const uint16_t*>(p);
+#pragma unroll
+        for (int w = 0; w < VW; ++w) d[w] = h2f<ST>(q[w]);
+    }
+}
+
+template <int ST, int VW, bool NT>
+__device__ __forceinline__ void tstore_p(typename Stor<ST>::T* __restrict__ p, const float (&s)[VW]) {
+    if constexpr (ST == ST_F32) {
+        vstore_p<VW, NT>(p, s);
+    } else if constexpr (VW == 4) {
+        sir_u2 t;
+        t.x = f2h<ST>(s[0]) | (f2h<ST>(s[1]) << 16);
+        t.y = f2h<ST>(s[2]) | (f2h<ST>(s[3]) << 16);
+        if constexpr (NT) __builtin_nontemporal_store(t, reinterpret_cast<sir_u2*>(p));
+        else *reinterpret_cast<sir_u2*>(p) = t;
+    } else {
+        uint16_t* q = reinterpret_cast<uint16_t*>(p);
+#pragma unroll
+        for (int w = 0; w < VW; ++w) q[w] = (uint16_t)f2h<ST>(s[w]);
+    }
+}
+
 // row-side streams (read or written once) and gathered rows
+template <int ST, int VW>
+__device__ __forceinline__ void vload_row(float (&d)[VW], const typename Stor<ST>::T* __restrict__ p) { tload_p<ST, VW, SIR_NT_STREAM>(d, p); }
+template <int ST, int VW>
+__device__ __forceinline__ void vstore_row(typename Stor<ST>::T* __restrict__ p, const float (&s)[VW]) { tstore_p<ST, VW, SIR_NT_STREAM>(p, s); }
 template <int VW>
-__device__ __forceinline__ void vload_row(float (&d)[VW], const float* __restrict__ p) { vload_p<VW, SIR_NT_STREAM>(d, p); }
-template <int VW>
-__device__ __forceinline__ void vstore_row(float* __restrict__ p, const float (&s)[VW]) { vstore_p<VW, SIR_NT_STREAM>(p, s); }
-template <int VW>
-__device__ __forceinline__ void vload_gather(float (&d)[VW], const float* __restrict__ p) { vload_p<VW, SIR_NT_GATHER>(d, p); }
+__device__ __forceinline__ void vstore_part(float* __restrict__ p, const float (&s)[VW]) { vstore_p<VW, SIR_NT_STREAM>(p, s); }
+template <int ST, int VW>
+__device__ __forceinline__ void vload_gather(float (&d)[VW], const typename Stor<ST>::T* __restrict__ p) { tload_p<ST, VW, SIR_NT_GATHER>(d, p); }
 
 template <int VW>
 __device__ __forceinline__ void vload(float (&d)[VW], const float* __restrict__ p) {
@@ -152,10 +217,10 @@ __device__ __forceinline__ void vstore(float* __restrict__ p, const float (&s)[V
 
 // ------------------------------------------------------------------------------ edge batch
 // Processes UU consecutive edges [e, e+UU) of one row: all gathers issued before any use.
-template <int MODE, int ACT, int AGG, int LPR, int NV, int VW, int UU, bool MASKW>
+template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int UU, bool MASKW>
 __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
-                                           const float* __restrict__ C, int64_t ldc,
-                                           const float* __restrict__ G, int64_t ldg,
+                                           const typename Stor<ST>::T* __restrict__ C, int64_t ldc,
+                                           const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
                                            const float* __restrict__ norm_col, float nr, float slope,
                                            int li, int HC,
                                            const float (&rv)[NV][VW], const float (&gv)[NV][VW],
@@ -171,18 +236,18 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
         // values are never used.  A guarded load becomes an exec-masked branch whose result the
         // compiler may copy inside the branch, i.e. wait for right after issuing it — that
         // serialised the gathers of some instances (sym forward: +50%).
-        const float* cp = C + (int64_t)u[i] * ldc;
+        const auto* cp = C + (int64_t)u[i] * ldc;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            vload_gather<VW>(cv[i][j], cp + (c < HC ? c : 0) * VW);
+            vload_gather<ST, VW>(cv[i][j], cp + (c < HC ? c : 0) * VW);
         }
         if constexpr (MODE == MODE_BWD_SRC) {
-            const float* gp = G + (int64_t)u[i] * ldg;
+            const auto* gp = G + (int64_t)u[i] * ldg;
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const int c = li + LPR * j;
-                vload_gather<VW>(gc[i][j], gp + (c < HC ? c : 0) * VW);
+                vload_gather<ST, VW>(gc[i][j], gp + (c < HC ? c : 0) * VW);
             }
         }
     }
@@ -252,17 +317,17 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 // MODE_FWD:     R = Q (rows = dst), C = K (gathered by src), out = S
 // MODE_BWD_DST: R = Q, C = K, G = dS rows (row-side), out = dQ, optional Gm = G/deg (MEAN)
 // MODE_BWD_SRC: R = K (rows = src), C = Q (gathered by dst), G = Gd (gathered), out = dK
-template <int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U, bool MASKW>
+template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U, bool MASKW>
 __global__ void __launch_bounds__(256)
 k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
        const int4* __restrict__ items, int64_t n_items,
-       const float* __restrict__ R, int64_t ldr,
-       const float* __restrict__ C, int64_t ldc,
-       const float* __restrict__ G, int64_t ldg,
+       const typename Stor<ST>::T* __restrict__ R, int64_t ldr,
+       const typename Stor<ST>::T* __restrict__ C, int64_t ldc,
+       const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
        const float* __restrict__ norm_row, const float* __restrict__ norm_col,
        float slope, int H,
-       float* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-       float* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask) {
+       typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
+       typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LPR;
@@ -284,16 +349,16 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
     float rv[NV][VW];
     float gv[NV][VW];
     float acc[NV][VW];
-    const float* rp = R + (int64_t)row * ldr;
+    const auto* rp = R + (int64_t)row * ldr;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const int c = li + LPR * j;
 #pragma unroll
         for (int w = 0; w < VW; ++w) { acc[j][w] = 0.f; rv[j][w] = 0.f; gv[j][w] = 0.f; }
-        if (c < HC) vload_row<VW>(rv[j], rp + c * VW);
+        if (c < HC) vload_row<ST, VW>(rv[j], rp + c * VW);
     }
     if constexpr (MODE == MODE_BWD_DST) {
-        const float* gp = G + (int64_t)row * ldg;
+        const auto* gp = G + (int64_t)row * ldg;
         float degf = 1.f;
         bool first = true;
         if constexpr (AGG == AGG_MEAN) {
@@ -306,11 +371,12 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
             if (c < HC) {
-                vload_row<VW>(gv[j], gp + c * VW);
+                vload_row<ST, VW>(gv[j], gp + c * VW);
                 if constexpr (AGG == AGG_MEAN) {
+                    // DivBackward: grad / deg (16-bit storage: rounded like the Gm copy the src pass reads)
 #pragma unroll
-                    for (int w = 0; w < VW; ++w) gv[j][w] = gv[j][w] / degf;   // DivBackward: grad / deg
-                    if (Gm != nullptr && first) vstore_row<VW>(Gm + (int64_t)row * ldgm + c * VW, gv[j]);
+                    for (int w = 0; w < VW; ++w) gv[j][w] = round_st<ST>(gv[j][w] / degf);
+                    if (Gm != nullptr && first) vstore_row<ST, VW>(Gm + (int64_t)row * ldgm + c * VW, gv[j]);
                 }
             }
         }
@@ -320,27 +386,27 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 
     int e = e0;
     for (; e + U <= e1; e += U)
-        edge_batch<MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+        edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
     if constexpr (U > 8) {
         if (e + 8 <= e1) {
-            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 8, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 8, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
             e += 8;
         }
     }
     if constexpr (U > 4) {
         if (e + 4 <= e1) {
-            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 4, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 4, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
             e += 4;
         }
     }
     if constexpr (U > 2) {
         if (e + 2 <= e1) {
-            edge_batch<MODE, ACT, AGG, LPR, NV, VW, 2, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 2, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
             e += 2;
         }
     }
     if (e < e1)
-        edge_batch<MODE, ACT, AGG, LPR, NV, VW, 1, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+        edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 1, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
 
     if (slot < 0) {
         if constexpr (MODE == MODE_FWD && AGG == AGG_MEAN) {
@@ -351,18 +417,18 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 #pragma unroll
                 for (int w = 0; w < VW; ++w) acc[j][w] = acc[j][w] / degf;
         }
-        float* op = out + (int64_t)row * ldo;
+        auto* op = out + (int64_t)row * ldo;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (c < HC) vstore_row<VW>(op + c * VW, acc[j]);
+            if (c < HC) vstore_row<ST, VW>(op + c * VW, acc[j]);
         }
     } else {
         float* pp = partial + (int64_t)slot * H;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
-            if (c < HC) vstore_row<VW>(pp + c * VW, acc[j]);
+            if (c < HC) vstore_part<VW>(pp + c * VW, acc[j]);
         }
     }
 }
@@ -400,9 +466,9 @@ __device__ __forceinline__ float sel_mask(uint64_t m, float t, float slope) {
 #define SIR_DQ_VMASK 1          // dQ pass: mask words by one vector load + v_readlane (1; -9% sum, -19% sym) or scalar loads (0)
 #endif
 
-template <int MODE, int ACT, int AGG, int NV, int UU, bool PRE = false>
+template <int ST, int MODE, int ACT, int AGG, int NV, int UU, bool PRE = false>
 __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, const int* __restrict__ perm,
-                                           const float* __restrict__ G, int64_t ldg,
+                                           const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
                                            const uint64_t* __restrict__ mask,
                                            const float* __restrict__ norm_col, float nr, float slope,
                                            int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4],
@@ -461,11 +527,11 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
     if constexpr (MODE == MODE_BWD_SRC) {
 #pragma unroll
         for (int i = 0; i < UU; ++i) {
-            const float* gp = G + (int64_t)v[i] * ldg;
+            const auto* gp = G + (int64_t)v[i] * ldg;
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 const int c = lane + 64 * j;
-                vload_gather<4>(gc[i][j], gp + (c < HC ? c : 0) * 4);   // unconditional (see edge_batch)
+                vload_gather<ST, 4>(gc[i][j], gp + (c < HC ? c : 0) * 4);   // unconditional (see edge_batch)
             }
         }
     }
@@ -489,35 +555,35 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
 }
 
 // The edge loop of one item (UNROLL-edge batches, then a binary tail).
-template <int MODE, int ACT, int AGG, int NV, int U>
+template <int ST, int MODE, int ACT, int AGG, int NV, int U>
 __device__ __forceinline__ void mask_item(int e0, int e1, const int* __restrict__ col, const int* __restrict__ perm,
-                                          const float* __restrict__ G, int64_t ldg,
+                                          const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
                                           const uint64_t* __restrict__ mask,
                                           const float* __restrict__ norm_col, float nr, float slope,
                                           int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4]) {
     int e = e0;
     for (; e + U <= e1; e += U)
-        mask_batch<MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+        mask_batch<ST, MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
     if constexpr (U > 8) {
         if (e + 8 <= e1) {
-            mask_batch<MODE, ACT, AGG, NV, 8>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            mask_batch<ST, MODE, ACT, AGG, NV, 8>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
             e += 8;
         }
     }
     if constexpr (U > 4) {
         if (e + 4 <= e1) {
-            mask_batch<MODE, ACT, AGG, NV, 4>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            mask_batch<ST, MODE, ACT, AGG, NV, 4>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
             e += 4;
         }
     }
     if constexpr (U > 2) {
         if (e + 2 <= e1) {
-            mask_batch<MODE, ACT, AGG, NV, 2>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+            mask_batch<ST, MODE, ACT, AGG, NV, 2>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
             e += 2;
         }
     }
     if (e < e1)
-        mask_batch<MODE, ACT, AGG, NV, 1>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+        mask_batch<ST, MODE, ACT, AGG, NV, 1>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
 }
 
 #ifndef SIR_DQ_PF
@@ -530,7 +596,7 @@ __device__ __forceinline__ void mask_item(int e0, int e1, const int* __restrict_
 // loaded lane-guarded, so no load leaves the row.  Every batch's words start at lane 0, so the
 // readlane lane indices are compile-time constants (a runtime lane index costs ~20%); the final
 // partial batch is summed edge by edge under uniform guards.
-template <int ACT, int AGG, int NV, int U>
+template <int ST, int ACT, int AGG, int NV, int U>
 __device__ __forceinline__ void mask_item_dst(int e0, int e1, const int* __restrict__ col,
                                               const uint64_t* __restrict__ mask,
                                               const float* __restrict__ norm_col, float nr, float slope,
@@ -546,7 +612,7 @@ __device__ __forceinline__ void mask_item_dst(int e0, int e1, const int* __restr
     int e = e0;
     for (; e + U <= e1; e += U) {
         const uint64_t nxt = load_batch(e + U);
-        mask_batch<MODE_BWD_DST, ACT, AGG, NV, U, true>(e, col, nullptr, nullptr, 0, mask, norm_col, nr, slope,
+        mask_batch<ST, MODE_BWD_DST, ACT, AGG, NV, U, true>(e, col, nullptr, nullptr, 0, mask, norm_col, nr, slope,
                                                         lane, HC, gv, acc, cur, 0);
         cur = nxt;
     }
@@ -554,7 +620,7 @@ __device__ __forceinline__ void mask_item_dst(int e0, int e1, const int* __restr
 #pragma unroll
     for (int i = 0; i < U - 1; ++i)
         if (i < r)
-            mask_batch<MODE_BWD_DST, ACT, AGG, NV, 1, true>(e + i, col, nullptr, nullptr, 0, mask, norm_col, nr,
+            mask_batch<ST, MODE_BWD_DST, ACT, AGG, NV, 1, true>(e + i, col, nullptr, nullptr, 0, mask, norm_col, nr,
                                                             slope, lane, HC, gv, acc, cur, i * NW);
 }
 
@@ -567,14 +633,14 @@ __device__ __forceinline__ int4 uniform_item(const int4* __restrict__ items, int
     return it;
 }
 
-template <int MODE, int ACT, int AGG, int NV, int U>
+template <int ST, int MODE, int ACT, int AGG, int NV, int U>
 __global__ void __launch_bounds__(256)
 k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
             const int4* __restrict__ items, int64_t n_items,
-            const float* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
+            const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
             const float* __restrict__ norm_row, const float* __restrict__ norm_col,
-            float slope, int H, float* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-            float* __restrict__ Gm, int64_t ldgm) {
+            float slope, int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
+            typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     if (wave >= n_items) return;
@@ -588,7 +654,7 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
 #pragma unroll
         for (int w = 0; w < 4; ++w) { acc[j][w] = 0.f; gv[j][w] = 0.f; }
     if constexpr (MODE == MODE_BWD_DST) {
-        const float* gp = G + (int64_t)row * ldg;
+        const auto* gp = G + (int64_t)row * ldg;
         float degf = 1.f;
         bool first = true;
         if constexpr (AGG == AGG_MEAN) {
@@ -601,11 +667,11 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
         for (int j = 0; j < NV; ++j) {
             const int c = lane + 64 * j;
             if (c < HC) {
-                vload_row<4>(gv[j], gp + c * 4);
+                vload_row<ST, 4>(gv[j], gp + c * 4);
                 if constexpr (AGG == AGG_MEAN) {
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) gv[j][w] = gv[j][w] / degf;
-                    if (Gm != nullptr && first) vstore_row<4>(Gm + (int64_t)row * ldgm + c * 4, gv[j]);
+                    for (int w = 0; w < 4; ++w) gv[j][w] = round_st<ST>(gv[j][w] / degf);
+                    if (Gm != nullptr && first) vstore_row<ST, 4>(Gm + (int64_t)row * ldgm + c * 4, gv[j]);
                 }
             }
         }
@@ -613,14 +679,23 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     float nr = 1.f;
     if constexpr (AGG == AGG_SYM) nr = norm_row[row];
     if constexpr (SIR_DQ_PF && MODE == MODE_BWD_DST && AGG != AGG_SYM && U * NV * 4 <= 64)
-        mask_item_dst<ACT, AGG, NV, U>(e0, e1, col, mask, norm_col, nr, slope, lane, HC, gv, acc);
+        mask_item_dst<ST, ACT, AGG, NV, U>(e0, e1, col, mask, norm_col, nr, slope, lane, HC, gv, acc);
     else
-        mask_item<MODE, ACT, AGG, NV, U>(e0, e1, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
-    float* op = (slot < 0) ? out + (int64_t)row * ldo : partial + (int64_t)slot * H;
+        mask_item<ST, MODE, ACT, AGG, NV, U>(e0, e1, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    if (slot < 0) {
+        auto* op = out + (int64_t)row * ldo;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-        const int c = lane + 64 * j;
-        if (c < HC) vstore_row<4>(op + c * 4, acc[j]);
+        for (int j = 0; j < NV; ++j) {
+            const int c = lane + 64 * j;
+            if (c < HC) vstore_row<ST, 4>(op + c * 4, acc[j]);
+        }
+    } else {
+        float* op = partial + (int64_t)slot * H;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int c = lane + 64 * j;
+            if (c < HC) vstore_part<4>(op + c * 4, acc[j]);
+        }
     }
 }
 
@@ -628,10 +703,10 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
 // per split row: threads cover the row's columns (VW floats each); the remaining thread
 // dimension takes slices of the partial slots (slot s -> slice s % nslice, 4 loads in
 // flight); the slices are added in slice order through LDS.  MEAN_DIV divides by the degree.
-template <bool MEAN_DIV, int VW>
+template <int ST, bool MEAN_DIV, int VW>
 __global__ void __launch_bounds__(1024)
 k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
-          int H, float* __restrict__ out, int64_t ldo) {
+          int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo) {
     __shared__ float red[1024 * VW];
     const int4 sp = splits[blockIdx.x];
     const int HC = H / VW;
@@ -678,7 +753,7 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 #pragma unroll
                 for (int w = 0; w < VW; ++w) r[w] = r[w] / degf;
             }
-            vstore<VW>(out + (int64_t)sp.x * ldo + c * VW, r);
+            tstore_p<ST, VW, false>(out + (int64_t)sp.x * ldo + c * VW, r);
         }
         __syncthreads();
     }
@@ -704,7 +779,11 @@ constexpr int unroll_of() {
     return MODE == MODE_FWD ? SIR_UNROLL_FWD : (MODE == MODE_BWD_DST ? SIR_UNROLL_DST : SIR_UNROLL_SRC);
 }
 
-template <int MODE, int ACT, int AGG, int LPR, int NV, int VW>
+template <int ST> using TP = typename Stor<ST>::T;
+template <int ST> __host__ inline const TP<ST>* cp_(const void* p) { return static_cast<const TP<ST>*>(p); }
+template <int ST> __host__ inline TP<ST>* mp_(void* p) { return static_cast<TP<ST>*>(p); }
+
+template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW>
 static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     constexpr int U = (NV == 1) ? unroll_of<MODE>() : 4;
     constexpr int RPW = 64 / LPR;
@@ -715,90 +794,94 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
                                (ACT == ACT_RELU || ACT == ACT_LEAKY);
     if constexpr (kMaskable) {
         if (a.mask_out != nullptr) {
-            hipLaunchKernelGGL((k_edge<MODE, ACT, AGG, LPR, NV, VW, U, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+            hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, true>), dim3((unsigned)blocks), dim3(256), 0, st,
                                a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
-                               a.R, a.ldr, a.C, a.ldc, a.G, a.ldg, a.norm_row, a.norm_col, a.slope, a.H,
-                               a.out, a.ldo, a.partial, a.Gm, a.ldgm, a.mask_out);
+                               cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
+                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out);
             return hipGetLastError();
         }
     } else {
         if (a.mask_out != nullptr) return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL((k_edge<MODE, ACT, AGG, LPR, NV, VW, U, false>), dim3((unsigned)blocks), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, false>), dim3((unsigned)blocks), dim3(256), 0, st,
                        a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
-                       a.R, a.ldr, a.C, a.ldc, a.G, a.ldg, a.norm_row, a.norm_col, a.slope, a.H,
-                       a.out, a.ldo, a.partial, a.Gm, a.ldgm, nullptr);
+                       cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
+                       a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr);
     return hipGetLastError();
 }
 
-template <int MODE, int ACT, int AGG, int NV>
+template <int ST, int MODE, int ACT, int AGG, int NV>
 static hipError_t launch_mask_t(const EdgeArgs& a, hipStream_t st) {
     constexpr int U = (NV == 1) ? unroll_of<MODE>() : (NV == 2 ? 4 : 2);
     const int64_t blocks = (a.n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_edge_mask<MODE, ACT, AGG, NV, U>), dim3((unsigned)blocks), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_edge_mask<ST, MODE, ACT, AGG, NV, U>), dim3((unsigned)blocks), dim3(256), 0, st,
                        a.rowptr, a.col, a.perm, reinterpret_cast<const int4*>(a.items), a.n_items,
-                       a.G, a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H,
-                       a.out, a.ldo, a.partial, a.Gm, a.ldgm);
+                       cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H,
+                       mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm);
     return hipGetLastError();
 }
 
-template <int MODE, int ACT, int AGG>
+template <int ST, int MODE, int ACT, int AGG>
 static hipError_t launch_mask_shape(const EdgeArgs& a, Shape s, hipStream_t st) {
     switch (s.nv) {
-        case 1: return launch_mask_t<MODE, ACT, AGG, 1>(a, st);
-        case 2: return launch_mask_t<MODE, ACT, AGG, 2>(a, st);
-        case 3: return launch_mask_t<MODE, ACT, AGG, 3>(a, st);
-        default: return launch_mask_t<MODE, ACT, AGG, 4>(a, st);
+        case 1: return launch_mask_t<ST, MODE, ACT, AGG, 1>(a, st);
+        case 2: return launch_mask_t<ST, MODE, ACT, AGG, 2>(a, st);
+        case 3: return launch_mask_t<ST, MODE, ACT, AGG, 3>(a, st);
+        default: return launch_mask_t<ST, MODE, ACT, AGG, 4>(a, st);
     }
 }
 
-template <int MODE, int ACT, int AGG>
+template <int ST, int MODE, int ACT, int AGG>
 static hipError_t launch_edge_shape(const EdgeArgs& a, Shape s, hipStream_t st) {
     if constexpr (MODE != MODE_FWD && (ACT == ACT_RELU || ACT == ACT_LEAKY)) {
         if (a.mask_in != nullptr) {
             if (s.vw != 4 || s.lpr != 64) return hipErrorInvalidValue;
-            return launch_mask_shape<MODE, ACT, AGG>(a, s, st);
+            return launch_mask_shape<ST, MODE, ACT, AGG>(a, s, st);
         }
     } else if constexpr (MODE != MODE_FWD) {
         if (a.mask_in != nullptr) return hipErrorInvalidValue;
     }
     if (s.vw == 4) {
-        if (s.lpr == 4) return launch_edge_t<MODE, ACT, AGG, 4, 1, 4>(a, st);
-        if (s.lpr == 8) return launch_edge_t<MODE, ACT, AGG, 8, 1, 4>(a, st);
-        if (s.lpr == 16) return launch_edge_t<MODE, ACT, AGG, 16, 1, 4>(a, st);
-        if (s.lpr == 32) return launch_edge_t<MODE, ACT, AGG, 32, 1, 4>(a, st);
+        if (s.lpr == 4) return launch_edge_t<ST, MODE, ACT, AGG, 4, 1, 4>(a, st);
+        if (s.lpr == 8) return launch_edge_t<ST, MODE, ACT, AGG, 8, 1, 4>(a, st);
+        if (s.lpr == 16) return launch_edge_t<ST, MODE, ACT, AGG, 16, 1, 4>(a, st);
+        if (s.lpr == 32) return launch_edge_t<ST, MODE, ACT, AGG, 32, 1, 4>(a, st);
         switch (s.nv) {
-            case 1: return launch_edge_t<MODE, ACT, AGG, 64, 1, 4>(a, st);
-            case 2: return launch_edge_t<MODE, ACT, AGG, 64, 2, 4>(a, st);
-            case 3: return launch_edge_t<MODE, ACT, AGG, 64, 3, 4>(a, st);
-            default: return launch_edge_t<MODE, ACT, AGG, 64, 4, 4>(a, st);
+            case 1: return launch_edge_t<ST, MODE, ACT, AGG, 64, 1, 4>(a, st);
+            case 2: return launch_edge_t<ST, MODE, ACT, AGG, 64, 2, 4>(a, st);
+            case 3: return launch_edge_t<ST, MODE, ACT, AGG, 64, 3, 4>(a, st);
+            default: return launch_edge_t<ST, MODE, ACT, AGG, 64, 4, 4>(a, st);
         }
     }
-    switch (s.nv) {
-        case 1: return launch_edge_t<MODE, ACT, AGG, 64, 1, 1>(a, st);
-        case 2: return launch_edge_t<MODE, ACT, AGG, 64, 2, 1>(a, st);
-        default: return launch_edge_t<MODE, ACT, AGG, 64, 4, 1>(a, st);
+    if constexpr (ST != ST_F32) {
+        return hipErrorInvalidValue;        // 16-bit storage: H % 4 == 0 and 8-B aligned rows only
+    } else {
+        switch (s.nv) {
+            case 1: return launch_edge_t<ST, MODE, ACT, AGG, 64, 1, 1>(a, st);
+            case 2: return launch_edge_t<ST, MODE, ACT, AGG, 64, 2, 1>(a, st);
+            default: return launch_edge_t<ST, MODE, ACT, AGG, 64, 4, 1>(a, st);
+        }
     }
 }
 
-template <int MODE, int ACT>
+template <int ST, int MODE, int ACT>
 static hipError_t launch_edge_agg(const EdgeArgs& a, int agg, Shape s, hipStream_t st) {
     switch (agg) {
-        case AGG_SUM: return launch_edge_shape<MODE, ACT, AGG_SUM>(a, s, st);
-        case AGG_MEAN: return launch_edge_shape<MODE, ACT, AGG_MEAN>(a, s, st);
-        default: return launch_edge_shape<MODE, ACT, AGG_SYM>(a, s, st);
+        case AGG_SUM: return launch_edge_shape<ST, MODE, ACT, AGG_SUM>(a, s, st);
+        case AGG_MEAN: return launch_edge_shape<ST, MODE, ACT, AGG_MEAN>(a, s, st);
+        default: return launch_edge_shape<ST, MODE, ACT, AGG_SYM>(a, s, st);
     }
 }
 
-template <int MODE>
+template <int ST, int MODE>
 static hipError_t launch_edge_mode(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st) {
     switch (act) {
-        case ACT_IDENTITY: return launch_edge_agg<MODE, ACT_IDENTITY>(a, agg, s, st);
-        case ACT_RELU: return launch_edge_agg<MODE, ACT_RELU>(a, agg, s, st);
-        case ACT_LEAKY: return launch_edge_agg<MODE, ACT_LEAKY>(a, agg, s, st);
-        case ACT_GELU: return launch_edge_agg<MODE, ACT_GELU>(a, agg, s, st);
-        default: return launch_edge_agg<MODE, ACT_GELU_TANH>(a, agg, s, st);
+        case ACT_IDENTITY: return launch_edge_agg<ST, MODE, ACT_IDENTITY>(a, agg, s, st);
+        case ACT_RELU: return launch_edge_agg<ST, MODE, ACT_RELU>(a, agg, s, st);
+        case ACT_LEAKY: return launch_edge_agg<ST, MODE, ACT_LEAKY>(a, agg, s, st);
+        case ACT_GELU: return launch_edge_agg<ST, MODE, ACT_GELU>(a, agg, s, st);
+        default: return launch_edge_agg<ST, MODE, ACT_GELU_TANH>(a, agg, s, st);
     }
 }
 

@@ -1,0 +1,10 @@
+// sirconv_fwd_bf16.hip — instantiates the MODE_FWD edge kernels for bf16 feature storage (one TU per
+// pass and dtype: parallel builds).
+#include "sirconv_edge_impl.h"
+
+namespace sir {
+template <>
+hipError_t launch_edge_pass<ST_BF16, MODE_FWD>(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st) {
+    return launch_edge_mode<ST_BF16, MODE_FWD>(a, agg, act, s, st);
+}
+}  // namespace sir

@@ -8,22 +8,24 @@ namespace sir {
 enum { AGG_SUM = 0, AGG_MEAN = 1, AGG_SYM = 2 };
 enum { ACT_IDENTITY = 0, ACT_RELU = 1, ACT_LEAKY = 2, ACT_GELU = 3, ACT_GELU_TANH = 4 };
 enum { MODE_FWD = 0, MODE_BWD_DST = 1, MODE_BWD_SRC = 2 };
+enum { ST_F32 = 0, ST_BF16 = 1, ST_F16 = 2 };     // feature storage dtype (SIR_DTYPE_*)
 
+// Feature pointers carry the storage dtype of the call (ST_*); norms and partial rows are fp32.
 struct EdgeArgs {
     const int* rowptr;
     const int* col;
     const int32_t* items;
     int64_t n_items;
-    const float* R;  int64_t ldr;     // row-side features
-    const float* C;  int64_t ldc;     // gathered (col-side) features
-    const float* G;  int64_t ldg;     // gradient rows (row-side for BWD_DST, gathered for BWD_SRC)
+    const void* R;  int64_t ldr;      // row-side features
+    const void* C;  int64_t ldc;      // gathered (col-side) features
+    const void* G;  int64_t ldg;      // gradient rows (row-side for BWD_DST, gathered for BWD_SRC)
     const float* norm_row;
     const float* norm_col;
     float slope;
     int H;
-    float* out;  int64_t ldo;
+    void* out;  int64_t ldo;
     float* partial;
-    float* Gm;  int64_t ldgm;
+    void* Gm;  int64_t ldgm;
     uint64_t* mask_out;          // forward: write the sign mask (ReLU family, full-wave rows)
     const uint64_t* mask_in;     // backward: sign-mask mode (Q/K not read)
     const int* perm;             // BWD_SRC mask mode: src-CSR position -> dst-CSR position
@@ -33,9 +35,15 @@ struct Shape {
     int lpr, nv, vw;   // lanes per row, float-vectors per lane, floats per vector
 };
 
-hipError_t launch_mode_fwd(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
-hipError_t launch_mode_bwd_dst(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
-hipError_t launch_mode_bwd_src(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
+// one TU per (pass, storage dtype) instantiates these (parallel builds)
+template <int ST, int MODE>
+hipError_t launch_edge_pass(const EdgeArgs& a, int agg, int act, Shape s, hipStream_t st);
+#define SIR_DECL_PASS(ST_, MODE_) \
+    template <> hipError_t launch_edge_pass<ST_, MODE_>(const EdgeArgs&, int, int, Shape, hipStream_t);
+SIR_DECL_PASS(ST_F32, MODE_FWD) SIR_DECL_PASS(ST_F32, MODE_BWD_DST) SIR_DECL_PASS(ST_F32, MODE_BWD_SRC)
+SIR_DECL_PASS(ST_BF16, MODE_FWD) SIR_DECL_PASS(ST_BF16, MODE_BWD_DST) SIR_DECL_PASS(ST_BF16, MODE_BWD_SRC)
+SIR_DECL_PASS(ST_F16, MODE_FWD) SIR_DECL_PASS(ST_F16, MODE_BWD_DST) SIR_DECL_PASS(ST_F16, MODE_BWD_SRC)
+#undef SIR_DECL_PASS
 
 // edge-materialised (generic) path, sirconv_generic.hip
 struct GenericArgs {
@@ -78,8 +86,8 @@ hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowpt
 hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, float* out,
                       float* workspace, int nb, hipStream_t st);
 
-hipError_t run_edge(int mode, const EdgeArgs& a, int agg, int act,
-                    const int32_t* splits, int64_t n_splits, float* out_final, int64_t ld_final,
+hipError_t run_edge(int mode, int dtype, const EdgeArgs& a, int agg, int act,
+                    const int32_t* splits, int64_t n_splits, void* out_final, int64_t ld_final,
                     bool mean_div, hipStream_t st, const char** why);
 
 int64_t csr_build_workspace(int64_t n_rows, int64_t E);

@@ -14,8 +14,9 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
-DTYPE_F32, DTYPE_BF16 = 0, 1
-ABI_VERSION = 4
+DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
+ABI_VERSION = 5
+STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
 _P, _I64, _I, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
@@ -154,13 +155,21 @@ def _ldx(t, H):
     return H if t is None else _ld(t, H)
 
 
+def _storage(*ts):
+    """SIR_DTYPE_* of the feature matrices of one edge-pass call (all must share one dtype)."""
+    dts = {t.dtype for t in ts if t is not None}
+    if len(dts) != 1 or next(iter(dts)) not in STORAGE:
+        raise RuntimeError(f"edge pass: feature tensors must share one of fp32/bf16/fp16, got {dts}")
+    return STORAGE[dts.pop()]
+
+
 def edge_agg_fwd(csr, Q, K, norm_row, norm_col, agg, act, slope, S, partial, mask_out=None):
     lib = load()
     H = S.shape[1]
     with _Timed("sir_edge_agg_fwd", S.device):
         rc = lib.sir_edge_agg_fwd(
             _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
-            H, DTYPE_F32, _ptr(Q), _ld(Q, H), _ptr(K), _ld(K, H), _ptr(norm_row), _ptr(norm_col),
+            H, _storage(Q, K, S), _ptr(Q), _ld(Q, H), _ptr(K), _ld(K, H), _ptr(norm_row), _ptr(norm_col),
             AGG[agg], act, float(slope), _ptr(S), _ld(S, H), _ptr(mask_out), _ptr(partial), _stream(S.device))
     _check(rc, lib)
 
@@ -171,7 +180,7 @@ def edge_agg_bwd_dst(csr, Q, K, G, norm_row, norm_col, agg, act, slope, dQ, Gm, 
     with _Timed("sir_edge_agg_bwd_dst", dQ.device):
         rc = lib.sir_edge_agg_bwd_dst(
             _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
-            H, DTYPE_F32, _ptr(Q), _ldx(Q, H), _ptr(K), _ldx(K, H), _ptr(mask), _ptr(G), _ld(G, H),
+            H, _storage(Q, K, G, dQ, Gm), _ptr(Q), _ldx(Q, H), _ptr(K), _ldx(K, H), _ptr(mask), _ptr(G), _ld(G, H),
             _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
             _ptr(dQ), _ld(dQ, H), _ptr(Gm), _ldx(Gm, H), _ptr(partial), _stream(dQ.device))
     _check(rc, lib)
@@ -183,7 +192,7 @@ def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, p
     with _Timed("sir_edge_agg_bwd_src", dK.device):
         rc = lib.sir_edge_agg_bwd_src(
             _ptr(csr_s.rowptr), _ptr(csr_s.col), _ptr(csr_s.perm if mask is not None else None),
-            _ptr(csr_s.items), csr_s.n_items, _ptr(csr_s.splits), csr_s.n_splits, H, DTYPE_F32,
+            _ptr(csr_s.items), csr_s.n_items, _ptr(csr_s.splits), csr_s.n_splits, H, _storage(K, Q, Gd, dK),
             _ptr(K), _ldx(K, H), _ptr(Q), _ldx(Q, H), _ptr(mask), _ptr(Gd), _ld(Gd, H),
             _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
             _ptr(dK), _ld(dK, H), _ptr(partial), _stream(dK.device))

@@ -44,8 +44,22 @@ def activation_code(act):
         f"SIRConv: activation {act!r} has no native kernel (supported: ReLU, LeakyReLU, GELU, Identity)")
 
 
+def _storage_dtype(dtype, H):
+    """Feature storage of the edge kernels for a QK of ``dtype``: the autocast dtypes run natively
+    as 16-bit rows (fp32 math inside), everything else as fp32."""
+    if dtype in (torch.bfloat16, torch.float16) and H % 4 == 0:
+        return dtype
+    return torch.float32
+
+
 class EdgeAggregate(torch.autograd.Function):
     """S = update_all(message_func, agg) of ``conv.py:63`` on packed ``QK = [Q | K]`` ([V, 2H]).
+
+    Under autocast (the reference's AMP path, ``heterophilous-datasets/train.py:75``) Q and K
+    arrive as bf16/fp16: the kernels gather those 16-bit rows directly (half the bytes), compute
+    z, sigma and the fp32 sum the reference's promoted messages get, and
+    return S in the same 16-bit dtype — the cast ``linear_relation`` applies to the reference's
+    fp32 S anyway.  The backward reads dS and writes dQ/dK in that dtype as well.
 
     Backward returns dQK written by the dst pass (dQ half) and the src pass (dK half).
     For sigma in {ReLU, LeakyReLU} (and 128 < H <= 1024) the forward also stores the sign of
@@ -55,21 +69,20 @@ class EdgeAggregate(torch.autograd.Function):
     use_mask = True
 
     @staticmethod
-    def forward(ctx, QK, plan, H, agg, act, slope):
+    def forward(ctx, QK, plan, H, agg, act, slope, grad_on=True):
         if QK.device.type != "cuda":
             raise RuntimeError("SIRConv native path needs a ROCm GPU tensor (no CPU fallback)")
         ctx.in_dtype = QK.dtype
-        QK = QK.contiguous()
-        if QK.dtype != torch.float32:
-            QK = QK.float()          # fp32 storage kernels (bf16 storage: DESIGN.md next steps)
+        st = _storage_dtype(QK.dtype, H)
+        QK = QK.contiguous().to(st)
         V = QK.shape[0]
         Q, K = QK[:, :H], QK[:, H:]
         in_norm, out_norm = plan.norms(agg)
-        S = torch.empty((V, H), device=QK.device, dtype=torch.float32)
+        S = torch.empty((V, H), device=QK.device, dtype=st)
         partial = _partial(plan, H, QK.device)
         nw = _native.mask_words(H, act) if EdgeAggregate.use_mask else 0
         mask = None
-        if nw and QK.requires_grad:
+        if nw and grad_on and QK.requires_grad:     # (inference: no mask; Function.forward runs under no_grad)
             mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=QK.device, dtype=torch.int64)
         _native.edge_agg_fwd(plan.dst, Q, K, in_norm, out_norm, agg, act, slope, S, partial, mask)
         if mask is not None:
@@ -77,18 +90,18 @@ class EdgeAggregate(torch.autograd.Function):
         else:
             ctx.save_for_backward(QK)
         ctx.masked = mask is not None
-        ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.V = plan, H, agg, act, slope, V
+        ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.V, ctx.st = plan, H, agg, act, slope, V, st
         return S
 
     @staticmethod
     def backward(ctx, dS):
         (saved,) = ctx.saved_tensors
-        plan, H, agg, act, slope, V = ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.V
-        G = dS.contiguous().float()
-        dQK = torch.empty((V, 2 * H), device=G.device, dtype=torch.float32)
+        plan, H, agg, act, slope, V, st = ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.V, ctx.st
+        G = dS.contiguous().to(st)
+        dQK = torch.empty((V, 2 * H), device=G.device, dtype=st)
         in_norm, out_norm = plan.norms(agg)
         partial = _partial(plan, H, G.device)
-        Gm = torch.empty((V, H), device=G.device, dtype=torch.float32) if agg == "mean" else None
+        Gm = torch.empty((V, H), device=G.device, dtype=st) if agg == "mean" else None
         if ctx.masked:
             Q = K = None
             mask = saved
@@ -99,7 +112,7 @@ class EdgeAggregate(torch.autograd.Function):
                                  dQK[:, :H], Gm, partial, mask)
         _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
                                  agg, act, slope, dQK[:, H:], partial, mask)
-        return dQK.to(ctx.in_dtype), None, None, None, None, None
+        return dQK.to(ctx.in_dtype), None, None, None, None, None, None
 
 
 def _partial(plan, H, device):
@@ -137,7 +150,7 @@ class SIRConvFunction(torch.autograd.Function):
     Used when dropout is inactive and inputs are fp32 (the modular path covers the rest)."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on=True):
         H = W_Q.shape[0]
         X = X.contiguous()
         W_cat = torch.cat([W_Q, W_K], 0)
@@ -146,7 +159,9 @@ class SIRConvFunction(torch.autograd.Function):
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=torch.float32)
         partial = _partial(plan, H, X.device)
-        training = any(ctx.needs_input_grad[:6])
+        # needs_input_grad mirrors requires_grad even under torch.no_grad(): the caller passes the
+        # grad mode, so inference forwards never write the per-edge sign mask
+        training = grad_on and any(ctx.needs_input_grad[:6])
         nw = _native.mask_words(H, act) if (EdgeAggregate.use_mask and training) else 0
         mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=X.device, dtype=torch.int64) if nw else None
         _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, act, slope, S, partial, mask)
@@ -189,7 +204,7 @@ class SIRConvFunction(torch.autograd.Function):
             db_Q = cs[:H] if need_bq else None
         elif need_bq:
             db_Q = _bias_grad(dQK[:, :H])
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None
 
 
 class SIRConv(nn.Module):
@@ -258,9 +273,10 @@ class SIRConv(nn.Module):
         if fused:
             return SIRConvFunction.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
                                          self.linear_key.weight, self.linear_relation.weight,
-                                         self.linear_relation.bias, plan, self._agg_type, act, slope)
+                                         self.linear_relation.bias, plan, self._agg_type, act, slope,
+                                         torch.is_grad_enabled())
         QK = self._project(feat_key, feat_query)
-        S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope)
+        S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope, torch.is_grad_enabled())
         return self.linear_relation(S)
 
     def extra_repr(self):

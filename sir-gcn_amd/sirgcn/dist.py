@@ -45,8 +45,7 @@ def all_to_all_rows(out, inp, out_splits, in_splits, group=None, async_op=False)
     """``out`` ← rows of every peer's ``inp`` (RCCL alltoallv).  Returns a waitable or None.
     ``group`` may also be an in-process communicator with the same method (tests)."""
     if hasattr(group, "all_to_all_rows"):
-        group.all_to_all_rows(out, inp, out_splits, in_splits)
-        return None
+        return group.all_to_all_rows(out, inp, out_splits, in_splits, async_op=async_op)
     if _host_staged(group, inp):
         o = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
@@ -224,7 +223,7 @@ class DistSIRConvFunction(torch.autograd.Function):
               dX += dK W_K, dW_K.  Weight gradients are this rank's partial sums."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on=True):
         H = W_Q.shape[0]
         n = dg.n_rows
         dev = X.device
@@ -238,7 +237,7 @@ class DistSIRConvFunction(torch.autograd.Function):
         in_norm, out_norm = dg.norms(agg)
         S = torch.empty((n, H), device=dev, dtype=torch.float32)
         partial = _workspace(dg, H, dev)
-        training = any(ctx.needs_input_grad[:6])
+        training = grad_on and any(ctx.needs_input_grad[:6])     # grad mode passed in (see conv.py)
         nw = _native.mask_words(H, act) if (use_mask and training and backend is _native) else 0
         mask = torch.empty((max(dg.dst.col.numel(), 1) * nw,), device=dev, dtype=torch.int64) if nw else None
         backend.edge_agg_fwd(dg.dst, Q, K_ext, in_norm, out_norm, agg, act, slope, S, partial, mask)
@@ -292,7 +291,7 @@ class DistSIRConvFunction(torch.autograd.Function):
         if dX is not None:
             dX += linalg.mm_w(dK, W_K)
         dW_K = _tn(dK, X) if ctx.needs_input_grad[3] else None
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None
 
 
 class DistEdgeAggregate(torch.autograd.Function):
@@ -300,7 +299,7 @@ class DistEdgeAggregate(torch.autograd.Function):
     from Q (own rows) and K (own rows); the halo exchange runs inside."""
 
     @staticmethod
-    def forward(ctx, Q, K_local, dg, H, agg, act, slope, backend, use_mask):
+    def forward(ctx, Q, K_local, dg, H, agg, act, slope, backend, use_mask, grad_on=True):
         dev = Q.device
         n = dg.n_rows
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
@@ -311,7 +310,7 @@ class DistEdgeAggregate(torch.autograd.Function):
         partial = _workspace(dg, H, dev)
         nw = _native.mask_words(H, act) if (use_mask and backend is _native) else 0
         mask = None
-        if nw and (Q.requires_grad or K_local.requires_grad):
+        if nw and grad_on and (Q.requires_grad or K_local.requires_grad):
             mask = torch.empty((max(dg.dst.col.numel(), 1) * nw,), device=dev, dtype=torch.int64)
         Qc = Q.contiguous().float()
         backend.edge_agg_fwd(dg.dst, Qc, K_ext, in_norm, out_norm, agg, act, slope, S, partial, mask)
@@ -348,7 +347,7 @@ class DistEdgeAggregate(torch.autograd.Function):
             recv = torch.empty((dg.send_idx.numel(), H), device=dev, dtype=torch.float32)
             dg.scatter_halo(dK_ext[n:], recv)
             dg.add_received(dK, recv)
-        return dQ, dK, None, None, None, None, None, None, None
+        return dQ, dK, None, None, None, None, None, None, None, None
 
 
 class DistSIRConv(torch.nn.Module):
@@ -378,10 +377,12 @@ class DistSIRConv(torch.nn.Module):
         if fused:
             return DistSIRConvFunction.apply(feat, c.linear_query.weight, c.linear_query.bias, c.linear_key.weight,
                                              c.linear_relation.weight, c.linear_relation.bias, dgraph,
-                                             c._agg_type, act, slope, self.backend, self.use_mask)
+                                             c._agg_type, act, slope, self.backend, self.use_mask,
+                                             torch.is_grad_enabled())
         Q = c.dropout(c.linear_query(feat))
         K = c.dropout(c.linear_key(feat))
-        S = DistEdgeAggregate.apply(Q, K, dgraph, H, c._agg_type, act, slope, self.backend, self.use_mask)
+        S = DistEdgeAggregate.apply(Q, K, dgraph, H, c._agg_type, act, slope, self.backend, self.use_mask,
+                                    torch.is_grad_enabled())
         return c.linear_relation(S)
 
     def allreduce_grads(self, group=None):

@@ -13,16 +13,23 @@ import torch
 from . import _native
 
 USE_NATIVE = True
+MAX_DIM = 65536          # N, K (and M, N of the TN GEMM) limit of the native kernels
+MAX_LD = 1 << 20         # SIR_GEMM_MAX_LD (include/sirconv.h)
 
 
 def _ok(t):
     return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
-            and t.stride(0) % 4 == 0 and t.shape[1] % 4 == 0 and t.data_ptr() % 16 == 0)
+            and t.stride(0) % 4 == 0 and t.shape[1] % 4 == 0 and t.data_ptr() % 16 == 0
+            and t.shape[1] <= MAX_DIM and t.stride(0) <= MAX_LD)
+
+
+def _w_ok(W, n_out):
+    return W.is_cuda and W.dtype == torch.float32 and n_out % 4 == 0 and n_out <= MAX_DIM
 
 
 def mm_wt(A, W, bias=None, out=None):
     """A W^T + bias (nn.Linear); W [N, K]."""
-    if (USE_NATIVE and _ok(A) and W.is_cuda and W.dtype == torch.float32 and W.shape[0] % 4 == 0
+    if (USE_NATIVE and _ok(A) and _w_ok(W, W.shape[0])
             and (bias is None or (bias.is_contiguous() and bias.data_ptr() % 16 == 0))
             and (out is None or _ok(out))):
         return _native.gemm_nt(A, _native.gemm_pack(W.contiguous()), bias, out)
@@ -35,16 +42,20 @@ def mm_wt(A, W, bias=None, out=None):
 
 def mm_w(A, W):
     """A W; W [K, N]."""
-    if USE_NATIVE and _ok(A) and W.is_cuda and W.dtype == torch.float32 and W.shape[1] % 4 == 0:
+    if USE_NATIVE and _ok(A) and _w_ok(W, W.shape[1]):
         return _native.gemm_nt(A, _native.gemm_pack(W.contiguous(), trans=True))
     return torch.mm(A, W)
+
+
+def _tn_ok(t):
+    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+            and 0 < t.shape[1] <= MAX_DIM and t.stride(0) <= MAX_LD)
 
 
 def mm_tn(A, B, colsum=False):
     """A^T B for tall A [R, M], B [R, N] (the weight gradients); with ``colsum`` also A.sum(0)
     (the bias gradient of the same linear), from the same pass: returns (A^T B, colsum)."""
-    if (USE_NATIVE and A.is_cuda and B.is_cuda and A.dtype == torch.float32 and B.dtype == torch.float32
-            and A.dim() == 2 and B.dim() == 2 and A.stride(1) == 1 and B.stride(1) == 1):
+    if USE_NATIVE and _tn_ok(A) and _tn_ok(B):
         return _native.gemm_tn(A, B, colsum=colsum)
     out = _tn_torch(A, B)
     return (out, A.sum(0)) if colsum else out

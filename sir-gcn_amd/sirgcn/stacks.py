@@ -1,0 +1,49 @@
+"""Multi-layer SIRConv stacks: the layer loops of the reference's models, i.e. the callers of the
+hot path for BASELINE configs 1, 2, 3 and 5.
+
+The reference models wrap SIRConv in embeddings, readouts and pooling (out of scope);
+what reaches the hot path is their per-layer loop, restated here with the conv / norm classes as
+parameters so that the SAME loop runs on the reference's own ``models/conv.py`` / ``models/norm.py``
+(``tests/golden/make_golden.py`` builds the stack fixtures that way) and on this package's
+MI355X modules (tests, ``bench.py --workload``):
+
+* ``order="arxiv"`` — ``ogbn-arxiv/model.py:65-73`` and ``ogbg-molhiv/model.py:76-84``:
+  ``resid = h; h = conv(g, h); h = norm(g, h); h = act(h); h = h + resid``;
+* ``order="zinc"`` — ``zinc/model.py:50-56`` (identity residual): ``h = conv(g, h) + h;
+  h = norm(g, h); h = act(h)``;
+* ``order="plain"`` — ``dictionary-lookup/model.py:30-32``: ``h = conv(g, h)`` (the
+  ``Sequential`` sigma lives inside the conv).
+
+``norm_cls`` (e.g. GraphNorm, ``models/norm.py:7-29``) is called as ``norm(graph, feats)``.
+"""
+from torch import nn
+
+
+class SIRStack(nn.Module):
+    def __init__(self, conv_cls, hidden, num_layers, activation, agg_type="sum", order="arxiv",
+                 norm_cls=None, conv_activation=None):
+        super().__init__()
+        if order not in ("arxiv", "zinc", "plain"):
+            raise ValueError(order)
+        self.order = order
+        self.activation = activation
+        sigma = conv_activation if conv_activation is not None else activation
+        self.convs = nn.ModuleList([conv_cls(hidden, hidden, hidden, sigma, 0, agg_type=agg_type)
+                                    for _ in range(num_layers)])
+        self.norms = nn.ModuleList([norm_cls(hidden) for _ in range(num_layers)]) if norm_cls else None
+
+    def forward(self, graph, feats):
+        for i, conv in enumerate(self.convs):
+            if self.order == "plain":
+                feats = conv(graph, feats)
+                continue
+            resid = feats
+            feats = conv(graph, feats)
+            if self.order == "zinc":
+                feats = feats + resid
+            if self.norms is not None:
+                feats = self.norms[i](graph, feats)
+            feats = self.activation(feats)
+            if self.order == "arxiv":
+                feats = feats + resid
+        return feats

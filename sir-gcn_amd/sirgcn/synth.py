@@ -8,7 +8,7 @@ multi-edges kept (DGL allows both).
 """
 import torch
 
-from .graph import Graph
+from .graph import Graph, batch
 
 NAMED = {
     # name: (V, E, alpha)
@@ -44,3 +44,47 @@ def powerlaw_graph(V, E, alpha=0.8, seed=0):
 def named_graph(name, seed=0):
     V, E, alpha = NAMED[name]
     return powerlaw_graph(V, E, alpha, seed)
+
+
+def molecule_graph(n, rings, gen):
+    """A molecule-shaped graph: a random tree over n atoms plus ``rings`` ring-closing bonds,
+    every bond as two directed edges (OGB / benchmarking-GNNs molecules are bidirected)."""
+    parent = [int(torch.randint(0, i, (1,), generator=gen)) for i in range(1, n)]
+    u = list(range(1, n))
+    v = parent
+    for _ in range(rings if n > 4 else 0):
+        a = int(torch.randint(0, n, (1,), generator=gen))
+        b = int(torch.randint(0, n, (1,), generator=gen))
+        if a != b:
+            u.append(a)
+            v.append(b)
+    src = torch.tensor(u + v, dtype=torch.int64)
+    dst = torch.tensor(v + u, dtype=torch.int64)
+    return Graph(src, dst, n)
+
+
+def molecule_batch(num_graphs, mean_nodes, seed=0, min_nodes=6, ring_closures=3):
+    """``dgl.batch`` of molecule-shaped graphs with ~``mean_nodes`` atoms and ~``ring_closures``
+    ring-closing bonds each: ZINC (~23.2 atoms, ~49.8 directed edges: ``molecule_batch(B, 23)``)
+    and ogbg-molhiv (~25.5, ~55: ``molecule_batch(B, 25)``) statistics (the real
+    datasets need network)."""
+    gen = torch.Generator().manual_seed(seed)
+    lo, hi = min_nodes, 2 * mean_nodes - min_nodes
+    graphs = []
+    for _ in range(num_graphs):
+        n = int(torch.randint(lo, hi + 1, (1,), generator=gen))
+        rings = int(torch.randint(0, 2 * ring_closures + 1, (1,), generator=gen))
+        graphs.append(molecule_graph(n, rings, gen))
+    return batch(graphs)
+
+
+def dictionary_lookup_batch(n, num_graphs):
+    """``synthetic-datasets/dictionary-lookup/data.py:27-31``: per graph 2n nodes, key nodes
+    0..n-1, value nodes n..2n-1, the n^2 edges of the complete bipartite value->key graph
+    (``itertools.product(val, key)`` order), batched ``num_graphs`` times."""
+    key = torch.arange(n)
+    val = torch.arange(n, 2 * n)
+    src = val.repeat_interleave(n)
+    dst = key.repeat(n)
+    g = Graph(src, dst, 2 * n)
+    return batch([g] * num_graphs)

@@ -58,28 +58,51 @@ def assert_close(actual, ref, rel=1e-5, what=""):
     assert torch.allclose(a, r, rtol=rel, atol=atol), f"{what}: allclose failed (max abs diff {(a - r).abs().max().item():.3e})"
 
 
-def assert_parity(actual, ref32, truth64, rel=1e-5, what=""):
+PARITY_FALLBACKS = []      # (what, relL2 vs ref32, relL2 vs fp64, ref32's own relL2 vs fp64)
+
+
+def assert_parity(actual, ref32, truth64, rel=1e-5, what="", strict=False, factor=2.0):
     """Accuracy-aware parity against the reference.
 
     ``ref32`` is the reference's own fp32 output (golden fixture / CPU oracle), ``truth64`` the
     same algorithm evaluated in fp64 (oracle).  Passes when the native result is within ``rel``
-    of the reference, or — where the reference's own fp32 rounding (long hub sums) is already
-    of that order — no worse than twice the reference's own error against fp64:
+    of the reference (relative L2 and elementwise), or — where the reference's own fp32 rounding
+    (long hub sums) is already of that order — no worse than twice the reference's own error
+    against fp64:
       per tensor : relL2(actual, truth) <= max(rel, 2 * relL2(ref32, truth))
       elementwise: |actual - truth| <= rel*|truth| + 1e-6*max|truth| + 4*max|ref32 - truth|
+    Every case that passes only through that second criterion is recorded in PARITY_FALLBACKS and
+    listed in the session summary.  ``strict=True`` (layer outputs h*, the north-star bar "within
+    1e-5 rel"): relL2 to the reference <= ``rel`` is REQUIRED, and elements must lie inside the fp64
+    envelope above (near-zero elements of a long fp32 sum are ill-posed for a pure rtol).
+    ``factor`` (default 2) scales the envelope for multi-layer stacks, where rounding differences
+    of every layer compound.
     """
     import torch
     a = torch.as_tensor(actual).double().cpu()
     r = torch.as_tensor(ref32).double().cpu()
     t = torch.as_tensor(truth64).double().cpu()
     assert a.shape == t.shape == r.shape, (what, a.shape, r.shape, t.shape)
-    if rel_err(a, r) <= rel and torch.allclose(a, r, rtol=rel, atol=1e-6 * (r.abs().max().item() if r.numel() else 0)):
+    e_r = rel_err(a, r)
+    if e_r <= rel and torch.allclose(a, r, rtol=rel, atol=1e-6 * (r.abs().max().item() if r.numel() else 0)):
         return
+    assert not strict or e_r <= rel, f"{what}: relL2 vs the reference {e_r:.3e} > {rel:.0e} (strict)"
     e_ref = rel_err(r, t)
     e_act = rel_err(a, t)
-    assert e_act <= max(rel, 2 * e_ref), f"{what}: relL2 vs fp64 {e_act:.3e} > max({rel:.0e}, 2*ref {e_ref:.3e})"
+    assert strict or e_act <= max(rel, factor * e_ref), \
+        f"{what}: relL2 vs fp64 {e_act:.3e} > max({rel:.0e}, {factor:g}*ref {e_ref:.3e})"
     ref_abs = (r - t).abs().max().item() if r.numel() else 0.0
     tmax = t.abs().max().item() if t.numel() else 0.0
     bound = rel * t.abs() + 1e-6 * tmax + 4 * ref_abs
     bad = ((a - t).abs() > bound)
     assert not bad.any(), f"{what}: {int(bad.sum())} elements beyond the reference's own error envelope"
+    PARITY_FALLBACKS.append((what + (" [strict: relL2 ok, elementwise via envelope]" if strict else ""),
+                             e_r, e_act, e_ref))
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    if PARITY_FALLBACKS:
+        terminalreporter.write_line(f"assert_parity: {len(PARITY_FALLBACKS)} tensor(s) passed through the fp64 "
+                                    "envelope (relL2 vs ref32 / vs fp64 / ref32's own vs fp64):")
+        for what, e_r, e_a, e_ref in PARITY_FALLBACKS:
+            terminalreporter.write_line(f"  {what}: {e_r:.2e} / {e_a:.2e} / {e_ref:.2e}")

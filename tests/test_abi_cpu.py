@@ -43,9 +43,11 @@ def _fwd(lib, rowptr, col, items, n_items, H, dtype, Q, ldq, K, ldk, nr, nc, agg
 def test_argument_checks_are_synchronous_and_reported():
     lib = _native.load()
     n = _null()
-    # unsupported dtype
-    assert _fwd(lib, n, n, n, 0, 256, 7, n, 256, n, 256, n, n, 0, 2, n, 256) == 2
+    # unknown dtype (F32 = 0, BF16 = 1, F16 = 2 are the storage dtypes)
+    assert _fwd(lib, n, n, n, 0, 256, 7, n, 256, n, 256, n, n, 0, 2, n, 256) == 1
     assert b"F32" in lib.sir_last_error()
+    for dt in (1, 2):       # 16-bit storage: empty work is a no-op like fp32
+        assert _fwd(lib, n, n, n, 0, 256, dt, n, 256, n, 256, n, n, 0, 2, n, 256) == 0
     # bad agg
     assert _fwd(lib, n, n, n, 0, 256, 0, n, 256, n, 256, n, n, 9, 2, n, 256) == 1
     assert b"agg" in lib.sir_last_error()

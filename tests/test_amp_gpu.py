@@ -1,0 +1,180 @@
+"""16-bit storage (SIR_DTYPE_BF16 / SIR_DTYPE_F16) edge kernels and the autocast path.
+
+Kernel level: Q, K, dS are rounded to the storage dtype, the oracle evaluates the same rounded
+values in fp64, and the kernels (fp32 math inside, one RNE rounding per output) must land within
+two units of the storage dtype's roundoff u (bf16 2^-8, fp16 2^-11) of that truth, elementwise.
+Layer level: SIRConv under ``torch.autocast`` (the reference's AMP path,
+``heterophilous-datasets/train.py:75,92,106``) against the fp32 golden fixtures of the reference:
+relative L2 within 2e-2 (bf16) / 1e-2 (fp16), or no worse than the reference's own AMP
+dataflow (``oracle.SIRConvRef`` under the same autocast) — whose half-precision gathers, sigma and
+index_add backward are less accurate than the fp32-internal kernels here.
+"""
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+import oracle
+from conftest import golden_manifest, load_case, rel_err
+
+from sirgcn import _native
+from sirgcn.conv import EdgeAggregate, SIRConv, activation_code
+from sirgcn.graph import Graph, GraphPlan
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DT = {"bf16": torch.bfloat16, "f16": torch.float16}
+U = {"bf16": 2.0 ** -8, "f16": 2.0 ** -11}
+ACTS = {"relu": nn.ReLU(), "leaky": nn.LeakyReLU(0.2), "gelu": nn.GELU()}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X box"
+    _native.load()
+
+
+def _within(got, truth, u, what):
+    g = got.double().cpu()
+    t = truth.double().cpu()
+    bound = 2 * u * t.abs() + 1e-5 * t.abs().max()
+    bad = (g - t).abs() > bound
+    assert not bad.any(), f"{what}: {int(bad.sum())} elements off by more than 2u (max {(g - t).abs().max():.3e})"
+    assert rel_err(g, t) <= 2 * u, (what, rel_err(g, t))
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("agg", ["sum", "mean", "sym"])
+@pytest.mark.parametrize("H,act", [(256, "leaky"), (128, "relu"), (64, "gelu"), (300, "leaky"), (16, "leaky")])
+def test_16bit_storage_kernels_vs_fp64(dt, agg, H, act):
+    gen = torch.Generator().manual_seed(H + 3 * len(agg) + len(dt))
+    V, E = 300, 2500
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V - 20, (E,), generator=gen)
+    dst[:400] = 5                                            # a split row at chunk 256
+    Q, K, dS = (torch.randn(V, H, generator=gen).to(DT[dt]) for _ in range(3))
+    slope = 0.2 if act == "leaky" else 0.01
+    S64 = oracle.edge_agg_fwd(src, dst, V, Q.double(), K.double(), agg, act, slope)
+    if agg == "mean":
+        # kernel contract (include/sirconv.h): in 16-bit storage the mean's g = G / deg is rounded to the
+        # storage dtype (the Gm rows the src pass gathers; the reference likewise casts dm to half for
+        # sigma's backward), so the truth is the plain sum over those rounded rows
+        deg = torch.bincount(dst, minlength=V).clamp(min=1).float().unsqueeze(1)
+        g = (dS.float() / deg).to(DT[dt]).double()
+        dQ64, dK64 = oracle.edge_agg_bwd(src, dst, V, Q.double(), K.double(), g, "sum", act, slope)
+    else:
+        dQ64, dK64 = oracle.edge_agg_bwd(src, dst, V, Q.double(), K.double(), dS.double(), agg, act, slope)
+    plan = GraphPlan(src, dst, V, DEV)
+    code, sl = activation_code(ACTS[act])
+    QK = torch.cat([Q, K], 1).to(DEV).requires_grad_(True)
+    S = EdgeAggregate.apply(QK, plan, H, agg, code, sl)
+    assert S.dtype == DT[dt]
+    S.backward(dS.to(DEV))
+    assert QK.grad.dtype == DT[dt]
+    _within(S, S64, U[dt], "S")
+    _within(QK.grad[:, :H], dQ64, U[dt], "dQ")
+    _within(QK.grad[:, H:], dK64, U[dt], "dK")
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("agg", ["sum", "sym", "mean"])
+def test_16bit_sign_mask_backward_bit_identical_to_recompute(dt, agg):
+    gen = torch.Generator().manual_seed(7)
+    V, E, H = 400, 6000, 256
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V, (E,), generator=gen)
+    dst[:700] = 11
+    QK = torch.randn(V, 2 * H, generator=gen).to(DEV, DT[dt])
+    dS = torch.randn(V, H, generator=gen).to(DEV, DT[dt])
+    plan = GraphPlan(src, dst, V, DEV)
+    outs = []
+    for use_mask in (True, False):
+        EdgeAggregate.use_mask = use_mask
+        try:
+            x = QK.clone().requires_grad_(True)
+            S = EdgeAggregate.apply(x, plan, H, agg, _native.ACT_LEAKY, 0.2)
+            S.backward(dS)
+            outs.append((S.detach(), x.grad))
+        finally:
+            EdgeAggregate.use_mask = True
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+CASES = [c for c in golden_manifest() if c["agg"] in ("sum", "mean", "sym") and c["dtype"] == "float32"
+         and c["act"] in ("relu", "leaky", "gelu") and c["H"] % 4 == 0 and c["E"] > 0]
+
+
+@pytest.mark.parametrize("dt,tol", [("bf16", 2e-2), ("f16", 1e-2)])
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_sirconv_autocast_vs_reference_fp32_golden(case, dt, tol):
+    z = load_case(case["name"])
+    m = SIRConv(case["d"], case["H"], case["O"], ACTS[case["act"]], 0, agg_type=case["agg"]).to(DEV)
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(z[k])).to(DEV)
+    with torch.no_grad():
+        m.linear_query.weight.copy_(t("W_Q")); m.linear_query.bias.copy_(t("b_Q"))
+        m.linear_key.weight.copy_(t("W_K"))
+        m.linear_relation.weight.copy_(t("W_R")); m.linear_relation.bias.copy_(t("b_R"))
+    g = Graph(torch.from_numpy(z["src"]), torch.from_numpy(z["dst"]), case["V"])
+    X = t("X").requires_grad_(True)
+    with torch.autocast("cuda", dtype=DT[dt]):
+        Y = m(g, X)
+    assert Y.dtype == DT[dt]                      # conv.py:65 under autocast: a half-precision linear
+    Y.float().backward(t("dY"))
+    got = {"Y": Y, "dX": X.grad, "dW_Q": m.linear_query.weight.grad, "db_Q": m.linear_query.bias.grad,
+           "dW_K": m.linear_key.weight.grad, "dW_R": m.linear_relation.weight.grad,
+           "db_R": m.linear_relation.bias.grad}
+    amp = _reference_amp(case, z, DT[dt])
+    for k, v in got.items():       # no worse than the reference's own AMP dataflow, or within tol
+        e, e_amp = rel_err(v.detach().float().cpu(), z[k]), rel_err(amp[k], z[k])
+        assert e <= max(tol, e_amp), f"{case['name']} {k}: relL2 {e:.3e} vs fp32 (reference AMP {e_amp:.3e})"
+
+
+def _reference_amp(case, z, dt):
+    """The reference's dataflow (oracle.SIRConvRef: gathers in half, sigma in half, fp32-promoted
+    messages, index_add backward in half) under the same autocast, on the GPU (checker only)."""
+    m = oracle.SIRConvRef(case["d"], case["H"], case["O"], ACTS[case["act"]], 0, agg_type=case["agg"]).to(DEV)
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(z[k])).to(DEV)
+    with torch.no_grad():
+        m.linear_query.weight.copy_(t("W_Q")); m.linear_query.bias.copy_(t("b_Q"))
+        m.linear_key.weight.copy_(t("W_K"))
+        m.linear_relation.weight.copy_(t("W_R")); m.linear_relation.bias.copy_(t("b_R"))
+    g = Graph(torch.from_numpy(z["src"]), torch.from_numpy(z["dst"]), case["V"])
+    X = t("X").requires_grad_(True)
+    with torch.autocast("cuda", dtype=dt):
+        Y = m(g, X)
+    Y.float().backward(t("dY"))
+    out = {"Y": Y, "dX": X.grad, "dW_Q": m.linear_query.weight.grad, "db_Q": m.linear_query.bias.grad,
+           "dW_K": m.linear_key.weight.grad, "dW_R": m.linear_relation.weight.grad,
+           "db_R": m.linear_relation.bias.grad}
+    return {k: v.detach().float().cpu() for k, v in out.items()}
+
+
+def test_amp_training_step_with_grad_scaler():
+    """The heterophilous-datasets training step (train.py:75,92,106): fp16 autocast forward,
+    GradScaler-scaled backward, unscale, step — gradients finite and close to fp32."""
+    z = load_case("wide_sym_leaky_h256_f32")
+    torch.manual_seed(0)
+    m = SIRConv(64, 256, 64, nn.LeakyReLU(0.2), 0, agg_type="sym").to(DEV)
+    m32 = SIRConv(64, 256, 64, nn.LeakyReLU(0.2), 0, agg_type="sym").to(DEV)
+    m32.load_state_dict(m.state_dict())
+    g = Graph(torch.from_numpy(z["src"]), torch.from_numpy(z["dst"]), 96)
+    X = torch.from_numpy(z["X"]).to(DEV)
+    dY = torch.from_numpy(z["dY"]).to(DEV)
+    opt = torch.optim.SGD(m.parameters(), lr=0.0)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 12)
+    with torch.amp.autocast(device_type="cuda", enabled=True):
+        loss = (m(g, X).float() * dY).sum()
+    scaler.scale(loss).backward()
+    scaler.unscale_(opt)
+    (m32(g, X) * dY).sum().backward()
+    mr = oracle.SIRConvRef(64, 256, 64, nn.LeakyReLU(0.2), 0, agg_type="sym").to(DEV)
+    mr.load_state_dict(m32.state_dict())
+    with torch.amp.autocast(device_type="cuda", enabled=True):      # the reference's AMP dataflow
+        lr = (mr(g, X).float() * dY).sum()
+    lr.backward()
+    for (n, p), p32, pr in zip(m.named_parameters(), m32.parameters(), mr.parameters()):
+        assert torch.isfinite(p.grad).all(), n
+        e, e_ref = rel_err(p.grad.cpu(), p32.grad.cpu()), rel_err(pr.grad.cpu(), p32.grad.cpu())
+        assert e <= max(1e-2, e_ref), (n, e, e_ref)
+    scaler.step(opt)
+    scaler.update()

@@ -151,7 +151,7 @@ def test_edge_cut_fused_function_threads(world, agg):
 
     def fn(r):
         dg = DistGraph(src, dst, V, bounds, r, world, "cpu", chunk=64, group=comms[r])
-        ctx = FakeCtx((True,) * 6 + (False,) * 6)
+        ctx = FakeCtx((True,) * 6 + (False,) * 7)
         Y = DistSIRConvFunction.forward(ctx, X[dg.row_begin:dg.row_end], *w, dg, agg, _native.ACT_LEAKY, 0.2,
                                         cpu_edge_backend, True)
         return dg.n_halo, Y, DistSIRConvFunction.backward(ctx, dY[dg.row_begin:dg.row_end])
@@ -166,3 +166,44 @@ def test_edge_cut_fused_function_threads(world, agg):
     assert_parity(dX, r["dX"], t["dX"], 1e-5, "dX")
     for i, k in enumerate(("dW_Q", "db_Q", "dW_K", "dW_R", "db_R")):
         assert_parity(sum(o[2][i + 1] for o in outs), r[k], t[k], 1e-5, k)
+
+
+@pytest.mark.parametrize("agg", ["sum", "mean"])
+def test_edge_cut_async_exchange_waits_before_use(agg):
+    """The async all-to-all path of DistSIRConvFunction (async_op=True, work.wait()) with a group
+    whose rows arrive only at wait() (NaN before): the assembled result must still match the oracle."""
+    import cpu_edge_backend
+    import oracle
+    from torch import nn
+    from conftest import assert_parity
+    from sirgcn import SIRConv, _native
+    from sirgcn.dist import DistGraph, DistSIRConvFunction, partition_rows
+    from sirgcn.synth import powerlaw_edges
+    from thread_comm import DeferredComm, FakeCtx, run_ranks
+    world, V, E, H = 3, 500, 7000, 16
+    src, dst = powerlaw_edges(V, E, 0.8, seed=9)
+    X = torch.randn(V, 12, generator=torch.Generator().manual_seed(1))
+    dY = torch.randn(V, 8, generator=torch.Generator().manual_seed(2))
+    torch.manual_seed(3)
+    conv = SIRConv(12, H, 8, nn.LeakyReLU(0.2), 0, agg_type=agg)
+    w = [p.detach() for p in (conv.linear_query.weight, conv.linear_query.bias, conv.linear_key.weight,
+                              conv.linear_relation.weight, conv.linear_relation.bias)]
+    comms = DeferredComm.make(world)
+    bounds = partition_rows(torch.bincount(dst, minlength=V), world)
+
+    def fn(r):
+        dg = DistGraph(src, dst, V, bounds, r, world, "cpu", chunk=64, group=comms[r])
+        ctx = FakeCtx((True,) * 6 + (False,) * 7)
+        Y = DistSIRConvFunction.forward(ctx, X[dg.row_begin:dg.row_end], *w, dg, agg, _native.ACT_LEAKY, 0.2,
+                                        cpu_edge_backend, True)
+        return Y, DistSIRConvFunction.backward(ctx, dY[dg.row_begin:dg.row_end]), comms[r].works
+
+    outs = run_ranks(world, fn)
+    assert all(o[2] == 2 for o in outs)          # one async exchange forward, one backward, per rank
+    Y = torch.cat([o[0] for o in outs])
+    dX = torch.cat([o[1][0] for o in outs])
+    assert torch.isfinite(Y).all() and torch.isfinite(dX).all()
+    t = oracle.layer_fwd_bwd(src, dst, V, X.double(), *[x.double() for x in w], dY.double(), agg, "leaky", 0.2)
+    r = oracle.reference_cpu_step(src, dst, V, X, *w, dY, agg, "leaky", 0.2)
+    assert_parity(Y, r["Y"], t["Y"], 1e-5, "Y")
+    assert_parity(dX, r["dX"], t["dX"], 1e-5, "dX")

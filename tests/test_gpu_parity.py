@@ -110,8 +110,8 @@ def test_sirconv_layer_vs_reference_golden(case, fused):
     d = lambda k: torch.from_numpy(z[k]).double()
     truth = oracle.layer_fwd_bwd(z["src"], z["dst"], case["V"], *[d(k) for k in ("X", "W_Q", "b_Q", "W_K", "W_R", "b_R", "dY")],
                                  case["agg"], case["act"], case["slope"])
-    for k, v in got.items():
-        assert_parity(v.detach().cpu(), z[k], truth[k], 1e-5, f"{case['name']} {k}")
+    for k, v in got.items():      # Y (h*) on the strict 1e-5 bar of the north star
+        assert_parity(v.detach().cpu(), z[k], truth[k], 1e-5, f"{case['name']} {k}", strict=(k == "Y"))
 
 
 def test_state_dict_keys_match_reference_layout():
@@ -318,7 +318,7 @@ def test_edge_cut_halo_exchange_on_device(world, agg):
 
     def rank_fn(r):
         dg = DistGraph(src, dst, V, bounds, r, world, DEV, group=comms[r])
-        ctx = FakeCtx((True,) * 6 + (False,) * 6)
+        ctx = FakeCtx((True,) * 6 + (False,) * 7)
         x = X[dg.row_begin:dg.row_end]
         with torch.no_grad():
             Y = DistSIRConvFunction.forward(ctx, x, w[0], w[1], w[2], w[3], w[4], dg, agg, _native.ACT_LEAKY, 0.2,

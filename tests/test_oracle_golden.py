@@ -161,3 +161,62 @@ def test_sire_oracle_matches_reference(case):
     tol = 1e-12 if case["dtype"] == "float64" else 1e-5
     for key in ("Y", "dX", "defeat", "dW_Q", "db_Q", "dW_K", "dW_E", "dW_R", "db_R"):
         assert_close(ref[key], z[key], tol, f"{case['name']} {key}")
+
+
+# ------------------------------------------------------------------ differentiable oracle modules
+def _oracle_act_module(case, z, dtype):
+    from torch import nn
+    a = _act_from_case(case, z, dtype)
+    if not isinstance(a, str):
+        return a
+    return {"relu": nn.ReLU(), "leaky": nn.LeakyReLU(0.2), "gelu": nn.GELU()}[a]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_oracle_conv_module_matches_reference(case):
+    """oracle.SIRConvRef (the chainable restatement used by the stack tests) vs every fixture."""
+    from sirgcn.graph import Graph
+    z = load_case(case["name"])
+    dt = torch.float64 if case["dtype"] == "float64" else torch.float32
+    m = oracle.SIRConvRef(case["d"], case["H"], case["O"], _oracle_act_module(case, z, dt), 0,
+                          agg_type=case["agg"]).to(dt)
+    with torch.no_grad():
+        for mod, wk, bk in ((m.linear_query, "W_Q", "b_Q"), (m.linear_key, "W_K", None),
+                            (m.linear_relation, "W_R", "b_R")):
+            mod.weight.copy_(_t(z[wk]))
+            if bk:
+                mod.bias.copy_(_t(z[bk]))
+    X = _t(z["X"]).requires_grad_(True)
+    Y = m(Graph(_t(z["src"]).long(), _t(z["dst"]).long(), case["V"]), X)
+    Y.backward(_t(z["dY"]))
+    tol = 1e-12 if dt == torch.float64 else 1e-5
+    if dt == torch.float64 and case["agg"] == "sym":
+        tol = 1e-6
+    assert_close(Y.detach(), z["Y"], tol, f"{case['name']} Y")
+    if case["agg"] == "max" and not case["name"].startswith("nodup"):
+        return      # tie gradients: see test_generic_layer_matches_reference
+    for key, got in (("dX", X.grad), ("dW_Q", m.linear_query.weight.grad), ("db_Q", m.linear_query.bias.grad),
+                     ("dW_K", m.linear_key.weight.grad), ("dW_R", m.linear_relation.weight.grad),
+                     ("db_R", m.linear_relation.bias.grad)):
+        assert_close(got, z[key], tol, f"{case['name']} {key}")
+
+
+@pytest.mark.parametrize("case", GN, ids=[c["name"] for c in GN])
+def test_oracle_graphnorm_module_matches_reference(case):
+    from sirgcn.graph import Graph
+    z = load_case(case["name"])
+    n = int(z["batch_num_nodes"].sum())
+    g = Graph(torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64), n, z["batch_num_nodes"])
+    gn = oracle.GraphNormRef(case["F"], bias=case["bias"], mean_scale=case["mean_scale"])
+    with torch.no_grad():
+        gn.weight.copy_(_t(z["weight"]))
+        if case["bias"]:
+            gn.bias.copy_(_t(z["bias"]))
+        if case["mean_scale"]:
+            gn.mean_scale.copy_(_t(z["mean_scale"]))
+    X = _t(z["X"]).requires_grad_(True)
+    Y = gn(g, X)
+    Y.backward(_t(z["dY"]))
+    assert_close(Y.detach(), z["Y"], 1e-6, "Y")
+    assert_close(X.grad, z["dX"], 1e-5, "dX")
+    assert_close(gn.weight.grad, z["dweight"], 1e-5, "dweight")

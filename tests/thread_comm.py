@@ -31,7 +31,7 @@ class ThreadComm:
             torch.cuda.synchronize(t.device)
         self.s.barrier.wait()
 
-    def all_to_all_rows(self, out, inp, out_splits, in_splits):
+    def all_to_all_rows(self, out, inp, out_splits, in_splits, async_op=False):
         self.s.slots[self.rank] = (inp, list(in_splits))
         self._sync(inp)
         off = 0
@@ -75,3 +75,32 @@ def run_ranks(world, fn):
     if errs:
         raise errs[0]
     return out
+
+
+class _Deferred:
+    def __init__(self, fn):
+        self._fn, self.done = fn, False
+
+    def wait(self):
+        if not self.done:
+            self._fn()
+            self.done = True
+
+
+class DeferredComm(ThreadComm):
+    """Like ThreadComm, but ``async_op=True`` calls return a work object and the rows land only at
+    ``wait()`` — until then the destination holds NaN, so a consumer that reads the halo before
+    waiting (the stream-ordering bug an async RCCL all-to-all allows) produces NaN."""
+
+    @staticmethod
+    def make(world):
+        sh = _Shared(world)
+        return [DeferredComm(sh, r) for r in range(world)]
+
+    def all_to_all_rows(self, out, inp, out_splits, in_splits, async_op=False):
+        if not async_op:
+            return super().all_to_all_rows(out, inp, out_splits, in_splits)
+        snap = inp.clone()
+        out.fill_(float("nan"))
+        self.works = getattr(self, "works", 0) + 1
+        return _Deferred(lambda: ThreadComm.all_to_all_rows(self, out, snap, out_splits, in_splits))

@@ -19,9 +19,20 @@ import json
 import os
 from collections import defaultdict
 
-PASS_OF = [("k_edge_mask<1,", "sir_edge_agg_bwd_dst"), ("k_edge_mask<2,", "sir_edge_agg_bwd_src"),
-           ("k_edge<0,", "sir_edge_agg_fwd"), ("k_edge<1,", "sir_edge_agg_bwd_dst"),
-           ("k_edge<2,", "sir_edge_agg_bwd_src")]
+PASSES = {0: "sir_edge_agg_fwd", 1: "sir_edge_agg_bwd_dst", 2: "sir_edge_agg_bwd_src"}
+
+
+def pass_of(short):
+    """ABI call of an edge kernel: k_edge<ST, MODE, ...> / k_edge_mask<ST, MODE, ...> (MODE 0 fwd,
+    1 dst pass, 2 src pass); None for other kernels."""
+    for pre in ("k_edge_mask<", "k_edge<"):
+        if short.startswith(pre):
+            args = short[len(pre):].split(">", 1)[0].split(",")
+            try:
+                return PASSES[int(args[1])]
+            except (IndexError, ValueError, KeyError):
+                return None
+    return None
 
 
 def load(d, counter):
@@ -45,7 +56,7 @@ def by_pass(rows):
     cur = None
     for name, val in rows:
         short = name.split("sir::", 1)[-1] if "sir::" in name else name
-        hit = next((p for pre, p in PASS_OF if short.startswith(pre)), None)
+        hit = pass_of(short)
         if hit is not None:
             cur = [hit, val]
             out[hit].append(cur)
