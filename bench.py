@@ -66,6 +66,8 @@ def parse():
                     help="nccl (= RCCL) for real runs; gloo to rehearse N ranks (CPU without a GPU)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the edge-cut (sirgcn.dist) code path even at world size 1")
+    ap.add_argument("--no-dual", action="store_true",
+                    help="A/B only: the two backward edge passes as two launches instead of one")
     ap.add_argument("--torch-gemm", action="store_true",
                     help="A/B only: projections on torch fp32 GEMMs instead of the native MFMA kernels")
     ap.add_argument("--pmc-file", default=None,
@@ -212,7 +214,11 @@ def kernel_table(timing, rows_of, edges, H, agg, masked, s):
         if not name.startswith("sir_edge_agg"):
             kernels[name] = {"ms": round(t, 4), "launches": len(evs)}
             continue
-        b = edge_pass_bytes(name, rows_of(name), edges, H, agg, masked, s=s)
+        if name == "sir_edge_agg_bwd":         # both backward passes in one launch
+            b = sum(edge_pass_bytes(n, rows_of(n), edges, H, agg, masked, s=s)
+                    for n in ("sir_edge_agg_bwd_dst", "sir_edge_agg_bwd_src"))
+        else:
+            b = edge_pass_bytes(name, rows_of(name), edges, H, agg, masked, s=s)
         kernels[name] = {"ms": round(t, 4), "launches": len(evs), "design_bytes": b,
                          "GBps": round(b / (t * 1e-3) / 1e9, 1)}
     return kernels, gemm
@@ -288,8 +294,11 @@ def main():
 
 def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
     from sirgcn import SIRConv, _native, linalg
+    from sirgcn.conv import EdgeAggregate
     if args.torch_gemm:
         linalg.USE_NATIVE = False
+    if args.no_dual:
+        EdgeAggregate.dual = False
     from sirgcn.graph import DEFAULT_CHUNK
     from sirgcn.synth import NAMED, powerlaw_edges
     H = args.hidden

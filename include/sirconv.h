@@ -146,6 +146,24 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          int agg, int act, float slope,
                          void* dK, int64_t lddk, float* partial, void* stream);
 
+/*
+ * Both backward passes in ONE launch — sign-mask mode, SUM or SYM (MEAN's source pass needs the
+ * destination pass's Gm first: use the two calls above).  Same results, bit for bit, as
+ * sir_edge_agg_bwd_dst followed by sir_edge_agg_bwd_src with the same arguments; the destination
+ * pass (VALU-bound) and the source pass (HBM-bound) share the CUs instead of running one after the
+ * other.  in_norm / out_norm: the SYM degree norms (NULL otherwise).  The two passes write their
+ * split rows' partial sums to separate workspaces: partial (destination plan's slots * H floats)
+ * and partial_s (source plan's slots * H floats).
+ */
+int sir_edge_agg_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                     const int32_t* splits, int64_t n_splits,
+                     const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
+                     const int32_t* items_s, int64_t n_items_s, const int32_t* splits_s, int64_t n_splits_s,
+                     int64_t H, int dtype, const uint64_t* mask, const void* G, int64_t ldg,
+                     const float* in_norm, const float* out_norm, int agg, int act, float slope,
+                     void* dQ, int64_t lddq, void* dK, int64_t lddk, float* partial, float* partial_s,
+                     void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Edge-materialised path: agg_type='max' (conv.py:46-47 + DGL max reduce) and sigma callables the
  * fused kernels do not cover (e.g. Sequential(ReLU, Linear, ReLU), dictionary-lookup/model.py:17).

@@ -198,6 +198,44 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
     return finish(fn, err, why);
 }
 
+int sir_edge_agg_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                     const int32_t* splits, int64_t n_splits,
+                     const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
+                     const int32_t* items_s, int64_t n_items_s, const int32_t* splits_s, int64_t n_splits_s,
+                     int64_t H, int dtype, const uint64_t* mask, const void* G, int64_t ldg,
+                     const float* in_norm, const float* out_norm, int agg, int act, float slope,
+                     void* dQ, int64_t lddq, void* dK, int64_t lddk, float* partial, float* partial_s,
+                     void* stream) {
+    const char* fn = "sir_edge_agg_bwd";
+    int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act, in_norm, out_norm,
+                          dQ, partial);
+    if (rc) return rc;
+    rc = check_common(fn, rowptr_s, col_s, items_s, n_items_s, splits_s, n_splits_s, H, dtype, agg, act, out_norm,
+                      in_norm, dK, partial_s);
+    if (rc) return rc;
+    if (agg == SIR_AGG_MEAN)
+        return fail(SIR_EUNSUPPORTED, fn, "MEAN: the source pass needs the destination pass's Gm (two calls)");
+    if (mask == nullptr) return fail(SIR_EINVAL, fn, "the one-launch backward is the sign-mask mode: mask required");
+    if ((rc = check_mask(fn, H, act))) return rc;
+    if (ldg < H || lddq < H || lddk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
+    if ((n_items > 0 || n_items_s > 0) && G == nullptr) return fail(SIR_EINVAL, fn, "G must be non-NULL");
+    if (n_items_s > 0 && perm_s == nullptr) return fail(SIR_EINVAL, fn, "sign-mask mode needs perm_s");
+    if (n_items > INT32_MAX || n_items_s > INT32_MAX || n_items + n_items_s > (int64_t)INT32_MAX)
+        return fail(SIR_EINVAL, fn, "too many work items for one launch");
+    sir::EdgeArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items;
+    a.G = G; a.ldg = ldg; a.norm_row = in_norm; a.norm_col = out_norm; a.slope = slope; a.H = (int)H;
+    a.out = dQ; a.ldo = lddq; a.partial = partial; a.mask_in = mask; a.ldr = H; a.ldc = H; a.ldgm = H;
+    sir::EdgeArgs b{};
+    b.rowptr = rowptr_s; b.col = col_s; b.perm = perm_s; b.items = items_s; b.n_items = n_items_s;
+    b.G = G; b.ldg = ldg; b.norm_row = out_norm; b.norm_col = in_norm; b.slope = slope; b.H = (int)H;
+    b.out = dK; b.ldo = lddk; b.partial = partial_s; b.mask_in = mask; b.ldr = H; b.ldc = H; b.ldgm = H;
+    const char* why = nullptr;
+    hipError_t err = sir::run_edge_dual(dtype, a, splits, n_splits, b, splits_s, n_splits_s, agg, act,
+                                        static_cast<hipStream_t>(stream), &why);
+    return finish(fn, err, why);
+}
+
 // ------------------------------------------------------------------------------ generic path
 static int check_generic(const char* fn, int64_t n_items, int64_t F, const int32_t* items) {
     if (F <= 0 || F > 1024) return fail(SIR_EINVAL, fn, "F must be in [1, 1024]");

@@ -1,0 +1,10 @@
+// sirconv_bwd_dual_bf16.hip — instantiates the one-launch sign-mask backward (dQ pass || dK pass)
+// for bf16 feature storage.
+#include "sirconv_edge_impl.h"
+
+namespace sir {
+template <>
+hipError_t launch_edge_dual<ST_BF16>(const EdgeArgs& a, const EdgeArgs& b, int agg, int act, Shape s, hipStream_t st) {
+    return launch_edge_dual_st<ST_BF16>(a, b, agg, act, s, st);
+}
+}  // namespace sir

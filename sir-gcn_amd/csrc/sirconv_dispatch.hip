@@ -187,4 +187,38 @@ hipError_t run_edge(int mode, int dtype, const EdgeArgs& a, int agg, int act,
     }
 }
 
+hipError_t run_edge_dual(int dtype, const EdgeArgs& a, const int32_t* splits, int64_t n_splits,
+                         const EdgeArgs& b, const int32_t* splits_s, int64_t n_splits_s,
+                         int agg, int act, hipStream_t st, const char** why) {
+    const uintptr_t vb = (dtype == ST_F32) ? 16 : 8;
+    const bool v4 = aligned_to(a.G, vb) && aligned_to(a.out, vb) && aligned_to(b.out, vb) &&
+                    aligned_to(a.partial, 16) && aligned_to(b.partial, 16) &&
+                    (a.ldg % 4 == 0) && (a.ldo % 4 == 0) && (b.ldo % 4 == 0);
+    Shape s;
+    if (!pick_shape(a.H, v4, &s) || s.vw != 4 || s.lpr != 64) {
+        *why = "the one-launch backward needs the sign-mask layout (H % 4 == 0, 128 < H <= 1024, aligned rows)";
+        return hipErrorInvalidValue;
+    }
+    hipError_t err;
+    switch (dtype) {
+        case ST_BF16: err = launch_edge_dual<ST_BF16>(a, b, agg, act, s, st); break;
+        case ST_F16: err = launch_edge_dual<ST_F16>(a, b, agg, act, s, st); break;
+        default: err = launch_edge_dual<ST_F32>(a, b, agg, act, s, st); break;
+    }
+    if (err != hipSuccess) {
+        if (err == hipErrorInvalidValue) *why = "the one-launch backward covers SUM/SYM with ReLU/LeakyReLU only";
+        return err;
+    }
+    auto combine = [&](const int32_t* sp, int64_t n, const EdgeArgs& x) -> hipError_t {
+        if (n == 0) return hipSuccess;
+        switch (dtype) {
+            case ST_BF16: return launch_combine<ST_BF16, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st);
+            case ST_F16: return launch_combine<ST_F16, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st);
+            default: return launch_combine<ST_F32, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st);
+        }
+    };
+    if ((err = combine(splits, n_splits, a)) != hipSuccess) return err;
+    return combine(splits_s, n_splits_s, b);
+}
+
 }  // namespace sir

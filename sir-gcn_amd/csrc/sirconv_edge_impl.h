@@ -633,17 +633,16 @@ __device__ __forceinline__ int4 uniform_item(const int4* __restrict__ items, int
     return it;
 }
 
+// One work item of a sign-mask backward pass (one wave).
 template <int ST, int MODE, int ACT, int AGG, int NV, int U>
-__global__ void __launch_bounds__(256)
-k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
-            const int4* __restrict__ items, int64_t n_items,
-            const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
-            const float* __restrict__ norm_row, const float* __restrict__ norm_col,
-            float slope, int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-            typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm) {
+__device__ __forceinline__ void
+mask_pass_item(int64_t wave, const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
+               const int4* __restrict__ items,
+               const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
+               const float* __restrict__ norm_row, const float* __restrict__ norm_col,
+               float slope, int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
+               typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm) {
     const int lane = threadIdx.x & 63;
-    const int64_t wave = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
-    if (wave >= n_items) return;
     const int4 it = uniform_item(items, wave);
     const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
     const int HC = H / 4;
@@ -697,6 +696,56 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
             if (c < HC) vstore_part<4>(op + c * 4, acc[j]);
         }
     }
+}
+
+template <int ST, int MODE, int ACT, int AGG, int NV, int U>
+__global__ void __launch_bounds__(256)
+k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
+            const int4* __restrict__ items, int64_t n_items,
+            const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
+            const float* __restrict__ norm_row, const float* __restrict__ norm_col,
+            float slope, int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
+            typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm) {
+    const int64_t wave = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    if (wave >= n_items) return;
+    mask_pass_item<ST, MODE, ACT, AGG, NV, U>(wave, rowptr, col, perm, items, G, ldg, mask, norm_row, norm_col, slope, H,
+                                              out, ldo, partial, Gm, ldgm);
+}
+
+// Both sign-mask backward passes in ONE launch (SUM / SYM: the dK pass does not need the dQ pass's
+// Gm).  The dQ pass is VALU-bound (v_readlane + select + add per element and edge) and reads 32 B
+// per edge; the dK pass is HBM-bound (one gathered G row per edge).  Interleaving their waves
+// (even waves dQ items, odd waves dK items, then the rest of the larger set) puts both kinds on
+// every CU at once, so the dQ pass's VALU work hides under the dK pass's memory time instead of
+// running as a separate launch.  Each wave still runs exactly the single-pass code, so results are
+// bit-identical to the two launches.
+template <int ST, int ACT, int AGG, int NV, int UD, int US>
+__global__ void __launch_bounds__(256)
+k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
+                 int64_t n_items, float* __restrict__ partial, typename Stor<ST>::T* __restrict__ dQ, int64_t lddq,
+                 const int* __restrict__ rowptr_s, const int* __restrict__ col_s, const int* __restrict__ perm_s,
+                 const int4* __restrict__ items_s, int64_t n_items_s, float* __restrict__ partial_s,
+                 typename Stor<ST>::T* __restrict__ dK, int64_t lddk,
+                 const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
+                 const float* __restrict__ in_norm, const float* __restrict__ out_norm, float slope, int H) {
+    const int64_t w = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int64_t nmin = n_items < n_items_s ? n_items : n_items_s;
+    bool dst;
+    int64_t idx;
+    if (w < 2 * nmin) {
+        dst = (w & 1) == 0;
+        idx = w >> 1;
+    } else {
+        dst = n_items > n_items_s;
+        idx = nmin + (w - 2 * nmin);
+        if (idx >= (dst ? n_items : n_items_s)) return;
+    }
+    if (dst)
+        mask_pass_item<ST, MODE_BWD_DST, ACT, AGG, NV, UD>(idx, rowptr, col, nullptr, items, G, ldg, mask, in_norm,
+                                                           out_norm, slope, H, dQ, lddq, partial, nullptr, H);
+    else
+        mask_pass_item<ST, MODE_BWD_SRC, ACT, AGG, NV, US>(idx, rowptr_s, col_s, perm_s, items_s, G, ldg, mask,
+                                                           out_norm, in_norm, slope, H, dK, lddk, partial_s, nullptr, H);
 }
 
 // Combine the partial rows of split rows (deterministic, no atomics).  One 1024-thread block
@@ -771,12 +820,27 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 #ifndef SIR_UNROLL_SRC
 #define SIR_UNROLL_SRC 8
 #endif
-#if SIR_UNROLL_FWD > 16 || SIR_UNROLL_DST > 16 || SIR_UNROLL_SRC > 16
+// 16-bit storage (A/B on MI355X, profiles/r02_ab_dq_smem_unroll.txt: twice the rows in flight per
+// wave made the bf16 passes 17-40% slower, like fp32 UNROLL 8 in round 1)
+#ifndef SIR_UNROLL_FWD_H
+#define SIR_UNROLL_FWD_H 4
+#endif
+#ifndef SIR_UNROLL_DST_H
+#define SIR_UNROLL_DST_H 6
+#endif
+#ifndef SIR_UNROLL_SRC_H
+#define SIR_UNROLL_SRC_H 8
+#endif
+#if SIR_UNROLL_FWD > 16 || SIR_UNROLL_DST > 16 || SIR_UNROLL_SRC > 16 || SIR_UNROLL_FWD_H > 16 || \
+    SIR_UNROLL_DST_H > 16 || SIR_UNROLL_SRC_H > 16
 #error "unroll must be <= 16 (the tail covers < 16 edges)"
 #endif
-template <int MODE>
+template <int MODE, int ST>
 constexpr int unroll_of() {
-    return MODE == MODE_FWD ? SIR_UNROLL_FWD : (MODE == MODE_BWD_DST ? SIR_UNROLL_DST : SIR_UNROLL_SRC);
+    if constexpr (ST == ST_F32)
+        return MODE == MODE_FWD ? SIR_UNROLL_FWD : (MODE == MODE_BWD_DST ? SIR_UNROLL_DST : SIR_UNROLL_SRC);
+    else
+        return MODE == MODE_FWD ? SIR_UNROLL_FWD_H : (MODE == MODE_BWD_DST ? SIR_UNROLL_DST_H : SIR_UNROLL_SRC_H);
 }
 
 template <int ST> using TP = typename Stor<ST>::T;
@@ -785,7 +849,7 @@ template <int ST> __host__ inline TP<ST>* mp_(void* p) { return static_cast<TP<S
 
 template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW>
 static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
-    constexpr int U = (NV == 1) ? unroll_of<MODE>() : 4;
+    constexpr int U = (NV == 1) ? unroll_of<MODE, ST>() : 4;
     constexpr int RPW = 64 / LPR;
     const int64_t waves = (a.n_items + RPW - 1) / RPW;
     const int64_t blocks = (waves + 3) / 4;
@@ -812,7 +876,7 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
 
 template <int ST, int MODE, int ACT, int AGG, int NV>
 static hipError_t launch_mask_t(const EdgeArgs& a, hipStream_t st) {
-    constexpr int U = (NV == 1) ? unroll_of<MODE>() : (NV == 2 ? 4 : 2);
+    constexpr int U = (NV == 1) ? unroll_of<MODE, ST>() : (NV == 2 ? 4 : 2);
     const int64_t blocks = (a.n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL((k_edge_mask<ST, MODE, ACT, AGG, NV, U>), dim3((unsigned)blocks), dim3(256), 0, st,
@@ -820,6 +884,42 @@ static hipError_t launch_mask_t(const EdgeArgs& a, hipStream_t st) {
                        cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H,
                        mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm);
     return hipGetLastError();
+}
+
+// a: the destination pass (dQ), b: the source pass (dK); mask mode, SUM / SYM
+template <int ST, int ACT, int AGG, int NV>
+static hipError_t launch_dual_t(const EdgeArgs& a, const EdgeArgs& b, hipStream_t st) {
+    constexpr int UD = (NV == 1) ? unroll_of<MODE_BWD_DST, ST>() : (NV == 2 ? 4 : 2);
+    constexpr int US = (NV == 1) ? unroll_of<MODE_BWD_SRC, ST>() : (NV == 2 ? 4 : 2);
+    const int64_t blocks = (a.n_items + b.n_items + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_edge_mask_dual<ST, ACT, AGG, NV, UD, US>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items, a.partial,
+                       mp_<ST>(a.out), a.ldo,
+                       b.rowptr, b.col, b.perm, reinterpret_cast<const int4*>(b.items), b.n_items, b.partial,
+                       mp_<ST>(b.out), b.ldo, cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H);
+    return hipGetLastError();
+}
+
+template <int ST, int ACT, int AGG>
+static hipError_t launch_dual_shape(const EdgeArgs& a, const EdgeArgs& b, Shape s, hipStream_t st) {
+    switch (s.nv) {
+        case 1: return launch_dual_t<ST, ACT, AGG, 1>(a, b, st);
+        case 2: return launch_dual_t<ST, ACT, AGG, 2>(a, b, st);
+        case 3: return launch_dual_t<ST, ACT, AGG, 3>(a, b, st);
+        default: return launch_dual_t<ST, ACT, AGG, 4>(a, b, st);
+    }
+}
+
+template <int ST>
+static hipError_t launch_edge_dual_st(const EdgeArgs& a, const EdgeArgs& b, int agg, int act, Shape s, hipStream_t st) {
+    if (s.vw != 4 || s.lpr != 64 || (agg != AGG_SUM && agg != AGG_SYM) || (act != ACT_RELU && act != ACT_LEAKY))
+        return hipErrorInvalidValue;
+    if (act == ACT_RELU)
+        return agg == AGG_SUM ? launch_dual_shape<ST, ACT_RELU, AGG_SUM>(a, b, s, st)
+                              : launch_dual_shape<ST, ACT_RELU, AGG_SYM>(a, b, s, st);
+    return agg == AGG_SUM ? launch_dual_shape<ST, ACT_LEAKY, AGG_SUM>(a, b, s, st)
+                          : launch_dual_shape<ST, ACT_LEAKY, AGG_SYM>(a, b, s, st);
 }
 
 template <int ST, int MODE, int ACT, int AGG>

@@ -44,6 +44,15 @@ SIR_DECL_PASS(ST_F32, MODE_FWD) SIR_DECL_PASS(ST_F32, MODE_BWD_DST) SIR_DECL_PAS
 SIR_DECL_PASS(ST_BF16, MODE_FWD) SIR_DECL_PASS(ST_BF16, MODE_BWD_DST) SIR_DECL_PASS(ST_BF16, MODE_BWD_SRC)
 SIR_DECL_PASS(ST_F16, MODE_FWD) SIR_DECL_PASS(ST_F16, MODE_BWD_DST) SIR_DECL_PASS(ST_F16, MODE_BWD_SRC)
 #undef SIR_DECL_PASS
+// both sign-mask backward passes in one launch (a = destination pass, b = source pass)
+template <int ST>
+hipError_t launch_edge_dual(const EdgeArgs& a, const EdgeArgs& b, int agg, int act, Shape s, hipStream_t st);
+template <> hipError_t launch_edge_dual<ST_F32>(const EdgeArgs&, const EdgeArgs&, int, int, Shape, hipStream_t);
+template <> hipError_t launch_edge_dual<ST_BF16>(const EdgeArgs&, const EdgeArgs&, int, int, Shape, hipStream_t);
+template <> hipError_t launch_edge_dual<ST_F16>(const EdgeArgs&, const EdgeArgs&, int, int, Shape, hipStream_t);
+hipError_t run_edge_dual(int dtype, const EdgeArgs& a, const int32_t* splits, int64_t n_splits,
+                         const EdgeArgs& b, const int32_t* splits_s, int64_t n_splits_s,
+                         int agg, int act, hipStream_t st, const char** why);
 
 // edge-materialised (generic) path, sirconv_generic.hip
 struct GenericArgs {

@@ -49,6 +49,8 @@ SIGNATURES = {
                                             _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P]),
     "sir_edge_agg_bwd_src": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
                                             _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _P]),
+    "sir_edge_agg_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _P, _I64, _I64, _I, _P,
+                                        _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P, _P]),
 }
 
 _lib = None
@@ -196,6 +198,21 @@ def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, p
             _ptr(K), _ldx(K, H), _ptr(Q), _ldx(Q, H), _ptr(mask), _ptr(Gd), _ld(Gd, H),
             _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
             _ptr(dK), _ld(dK, H), _ptr(partial), _stream(dK.device))
+    _check(rc, lib)
+
+
+def edge_agg_bwd(csr, csr_s, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK, partial, partial_s):
+    """Both sign-mask backward passes in one launch (SUM / SYM); bit-identical to
+    edge_agg_bwd_dst + edge_agg_bwd_src."""
+    lib = load()
+    H = dQ.shape[1]
+    with _Timed("sir_edge_agg_bwd", dQ.device):
+        rc = lib.sir_edge_agg_bwd(
+            _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
+            _ptr(csr_s.rowptr), _ptr(csr_s.col), _ptr(csr_s.perm), _ptr(csr_s.items), csr_s.n_items,
+            _ptr(csr_s.splits), csr_s.n_splits, H, _storage(G, dQ, dK), _ptr(mask), _ptr(G), _ld(G, H),
+            _ptr(in_norm), _ptr(out_norm), AGG[agg], act, float(slope), _ptr(dQ), _ld(dQ, H), _ptr(dK), _ld(dK, H),
+            _ptr(partial), _ptr(partial_s), _stream(dQ.device))
     _check(rc, lib)
 
 

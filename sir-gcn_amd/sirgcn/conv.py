@@ -67,6 +67,7 @@ class EdgeAggregate(torch.autograd.Function):
     re-gather, QK not kept alive; results are bit-identical to the recompute mode."""
 
     use_mask = True
+    dual = True          # one-launch backward (sir_edge_agg_bwd) where it applies
 
     @staticmethod
     def forward(ctx, QK, plan, H, agg, act, slope, grad_on=True):
@@ -99,25 +100,39 @@ class EdgeAggregate(torch.autograd.Function):
         plan, H, agg, act, slope, V, st = ctx.plan, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.V, ctx.st
         G = dS.contiguous().to(st)
         dQK = torch.empty((V, 2 * H), device=G.device, dtype=st)
-        in_norm, out_norm = plan.norms(agg)
-        partial = _partial(plan, H, G.device)
-        Gm = torch.empty((V, H), device=G.device, dtype=st) if agg == "mean" else None
         if ctx.masked:
             Q = K = None
             mask = saved
         else:
             Q, K = saved[:, :H], saved[:, H:]
             mask = None
-        _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope,
-                                 dQK[:, :H], Gm, partial, mask)
-        _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
-                                 agg, act, slope, dQK[:, H:], partial, mask)
+        edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK)
         return dQK.to(ctx.in_dtype), None, None, None, None, None, None
 
 
 def _partial(plan, H, device):
     n = max(plan.dst.n_slots, plan.src.n_slots)
     return torch.empty((max(n, 1) * H,), device=device, dtype=torch.float32) if n else None
+
+
+def _slots(csr, H, device):
+    return torch.empty((csr.n_slots * H,), device=device, dtype=torch.float32) if csr.n_slots else None
+
+
+def edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK):
+    """dQ -> dQK[:, :H], dK -> dQK[:, H:] (the backward of ``update_all``, conv.py:45,63).  Sign-mask
+    mode with SUM / SYM runs both passes in one launch (``sir_edge_agg_bwd``); MEAN (the source
+    pass reads the destination pass's G / deg) and recompute mode run them one after the other."""
+    in_norm, out_norm = plan.norms(agg)
+    if mask is not None and agg != "mean" and EdgeAggregate.dual:
+        _native.edge_agg_bwd(plan.dst, plan.src, G, mask, in_norm, out_norm, agg, act, slope, dQK[:, :H],
+                             dQK[:, H:], _slots(plan.dst, H, G.device), _slots(plan.src, H, G.device))
+        return
+    partial = _partial(plan, H, G.device)
+    Gm = torch.empty((G.shape[0], H), device=G.device, dtype=G.dtype) if agg == "mean" else None
+    _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope, dQK[:, :H], Gm, partial, mask)
+    _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
+                             agg, act, slope, dQK[:, H:], partial, mask)
 
 
 _tn = linalg.mm_tn
@@ -181,9 +196,6 @@ class SIRConvFunction(torch.autograd.Function):
         dY = dY.contiguous()
         G = linalg.mm_w(dY, W_R)
         dW_R, db_R = _weight_and_bias_grad(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
-        in_norm, out_norm = plan.norms(agg)
-        partial = _partial(plan, H, X.device)
-        Gm = torch.empty((V, H), device=X.device, dtype=torch.float32) if agg == "mean" else None
         if ctx.masked:
             Q = K = None
             mask = saved
@@ -191,10 +203,7 @@ class SIRConvFunction(torch.autograd.Function):
             Q, K = saved[:, :H], saved[:, H:]
             mask = None
         dQK = torch.empty((V, 2 * H), device=X.device, dtype=torch.float32)
-        _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope,
-                                 dQK[:, :H], Gm, partial, mask)
-        _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
-                                 agg, act, slope, dQK[:, H:], partial, mask)
+        edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK)
         dX = linalg.mm_w(dQK, W_cat) if ctx.needs_input_grad[0] else None
         dW_Q = dW_K = db_Q = None
         need_bq = ctx.has_bq and ctx.needs_input_grad[2]

@@ -643,3 +643,38 @@ def test_native_plan_build_batched_molecules_speed():
     td, tsr, tperm = torch_plans()
     assert torch.equal(nd.items, td.items) and torch.equal(ns.perm, tperm)
     assert ts["native"] <= ts["torch"] * 1.5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("agg", ["sum", "sym"])
+@pytest.mark.parametrize("chunk", [256, 4])
+def test_one_launch_backward_bit_identical_to_two_passes(agg, dtype, chunk):
+    """sir_edge_agg_bwd (dQ pass || dK pass in one launch) == sir_edge_agg_bwd_dst + _src, bit for bit."""
+    from sirgcn.conv import edge_backward
+    gen = torch.Generator().manual_seed(21)
+    V, E, H = 3000, 60000, 256
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V, (E,), generator=gen)
+    dst[:3000] = 17                                       # hub rows: split items on both plans
+    src[3000:5000] = 5
+    plan = GraphPlan(src, dst, V, DEV, chunk=chunk)
+    assert plan.dst.n_splits > 0 and plan.src.n_splits > 0
+    QK = torch.randn(V, 2 * H, generator=gen).to(DEV, dtype)
+    G = torch.randn(V, H, generator=gen).to(DEV, dtype)
+    in_norm, out_norm = plan.norms(agg)
+    S = torch.empty(V, H, device=DEV, dtype=dtype)
+    mask = torch.empty(E * 4, device=DEV, dtype=torch.int64)
+    part = torch.empty(max(plan.dst.n_slots, plan.src.n_slots) * H, device=DEV)
+    _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, _native.ACT_LEAKY, 0.2, S, part, mask)
+    outs = []
+    for dual in (True, False):
+        EdgeAggregate.dual = dual
+        try:
+            dQK = torch.full((V, 2 * H), float("nan"), device=DEV, dtype=dtype)
+            edge_backward(plan, H, agg, _native.ACT_LEAKY, 0.2, G, None, None, mask, dQK)
+            outs.append(dQK)
+        finally:
+            EdgeAggregate.dual = True
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.isfinite(outs[0]).all()

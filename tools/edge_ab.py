@@ -37,15 +37,18 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--chunk", type=int, default=256)
     ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16", "f16"])
     a = ap.parse_args()
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[a.dtype]
+    dcode = _native.STORAGE[tdt]
     V, E, alpha = NAMED[a.graph]
     src, dst = powerlaw_edges(V, E, alpha, seed=0)
     dev = "cuda"
     plan = GraphPlan(src, dst, V, dev, chunk=a.chunk)
     H = a.H
     g = torch.Generator(device=dev).manual_seed(0)
-    QK = torch.randn(V, 2 * H, device=dev, generator=g)
-    G = torch.randn(V, H, device=dev, generator=g)
+    QK = torch.randn(V, 2 * H, device=dev, generator=g).to(tdt)
+    G = torch.randn(V, H, device=dev, generator=g).to(tdt)
     in_norm, out_norm = plan.norms(a.agg)
     nw = _native.mask_words(H, _native.ACT_LEAKY)
     mask = torch.empty(E * nw, device=dev, dtype=torch.int64)
@@ -58,24 +61,24 @@ def main():
 
     def run(lib):
         P = _native._ptr
-        S = torch.empty(V, H, device=dev)
-        dQK = torch.empty(V, 2 * H, device=dev)
+        S = torch.empty(V, H, device=dev, dtype=tdt)
+        dQK = torch.empty(V, 2 * H, device=dev, dtype=tdt)
         sp = ctypes.c_void_p(st.cuda_stream)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         d, s_ = plan.dst, plan.src
         Q, K = QK[:, :H], QK[:, H:]
         ev[0].record()
-        rc = lib.sir_edge_agg_fwd(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, 0,
+        rc = lib.sir_edge_agg_fwd(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, dcode,
                                   P(Q), 2 * H, P(K), 2 * H, P(in_norm), P(out_norm), _native.AGG[a.agg],
                                   _native.ACT_LEAKY, 0.2, P(S), H, P(mask), P(partial), sp)
         ev[1].record()
-        rc |= lib.sir_edge_agg_bwd_dst(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, 0,
+        rc |= lib.sir_edge_agg_bwd_dst(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, dcode,
                                        None, H, None, H, P(mask), P(G), H, P(in_norm), P(out_norm),
                                        _native.AGG[a.agg], _native.ACT_LEAKY, 0.2, P(dQK), 2 * H, None, H,
                                        P(partial), sp)
         ev[2].record()
         rc |= lib.sir_edge_agg_bwd_src(P(s_.rowptr), P(s_.col), P(s_.perm), P(s_.items), s_.n_items, P(s_.splits),
-                                       s_.n_splits, H, 0, None, H, None, H, P(mask), P(G), H, P(out_norm),
+                                       s_.n_splits, H, dcode, None, H, None, H, P(mask), P(G), H, P(out_norm),
                                        P(in_norm), _native.AGG[a.agg], _native.ACT_LEAKY, 0.2,
                                        P(dQK[:, H:]), 2 * H, P(partial), sp)
         ev[3].record()

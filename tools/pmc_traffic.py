@@ -25,6 +25,8 @@ PASSES = {0: "sir_edge_agg_fwd", 1: "sir_edge_agg_bwd_dst", 2: "sir_edge_agg_bwd
 def pass_of(short):
     """ABI call of an edge kernel: k_edge<ST, MODE, ...> / k_edge_mask<ST, MODE, ...> (MODE 0 fwd,
     1 dst pass, 2 src pass); None for other kernels."""
+    if short.startswith("k_edge_mask_dual<"):
+        return "sir_edge_agg_bwd"
     for pre in ("k_edge_mask<", "k_edge<"):
         if short.startswith(pre):
             args = short[len(pre):].split(">", 1)[0].split(",")
