@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--workload", default="cfg4", choices=["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--graph", default="S2", help="cfg4 graph: S2 (default), S1, S1u, arxiv")
     ap.add_argument("--hidden", type=int, default=256)
-    ap.add_argument("--agg", default="sum", choices=["sum", "mean", "sym"])
+    ap.add_argument("--agg", default="sum", choices=["sum", "mean", "sym", "max"],
+                    help="max: the fused per-edge W_R + running max (sirgcn.edgemlp), an MFMA-bound kernel")
     ap.add_argument("--dtype", default=None, choices=["f32", "bf16", "f16"],
                     help="feature dtype (16-bit = the autocast path); default f32 (cfg2: bf16)")
     ap.add_argument("--chunk", type=int, default=None)
@@ -210,6 +211,11 @@ def kernel_table(timing, rows_of, edges, H, agg, masked, s):
             fl = sum(w for _, _, w in evs) / len(evs)
             gemm[name] = {"ms": round(t, 4), "launches": len(evs), "flops": fl,
                           "TFLOPs": round(fl / (t * 1e-3) / 1e12, 1)}
+            continue
+        if name == "sir_edge_mlp_fwd":         # fused per-edge dense layer: fp32 MFMA flops per launch
+            fl = sum(w for _, _, w in evs) / len(evs)
+            kernels[name] = {"ms": round(t, 4), "launches": len(evs), "flops": fl,
+                             "TFLOPs": round(fl / (t * 1e-3) / 1e12, 2)}
             continue
         if not name.startswith("sir_edge_agg"):
             kernels[name] = {"ms": round(t, 4), "launches": len(evs)}
@@ -372,10 +378,18 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
 
     from sirgcn.conv import EdgeAggregate
     s = SIZEOF[dtn]
-    masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY))
+    masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY)) and args.agg != "max"
     kernels, gemm = kernel_table(timing, lambda n: rows_src if n == "sir_edge_agg_bwd_src" else rows_local,
                                  edges_local, H, args.agg, masked, s)
-    out["roofline"] = roofline_fwd(args, kernels, rows_local, edges_local, rows_src, H, s, world)
+    if "sir_edge_mlp_fwd" in kernels:      # max: the per-edge W_R GEMM bounds the dominant kernel
+        k = kernels["sir_edge_mlp_fwd"]
+        out["roofline"] = {"bound": "mfma", "kernel": "sir_edge_mlp_fwd (gather -> sigma -> fp32 MFMA W_R -> running max)",
+                           "achieved": k["TFLOPs"], "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(k["TFLOPs"] / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                           "flops_formula": "2 * E * H * O per launch (v_mfma_f32_32x32x2_f32)",
+                           "ms_per_launch": k["ms"]}
+    else:
+        out["roofline"] = roofline_fwd(args, kernels, rows_local, edges_local, rows_src, H, s, world)
     out["roofline"]["all_kernels"] = kernels
     if gemm:
         out["projections"] = projections(gemm, args.steps)

@@ -205,6 +205,48 @@ int sir_segment_max_bwd(const int32_t* items, int64_t n_items, int64_t F, const 
                         const float* dY, int64_t ldy, float* dM, int64_t ldm, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Fused per-edge dense layer.  For every edge u->v of a destination row:
+ *   z = Q[v] + K[u],  a = act1(z),  h = W a + b,  m = act2(h)
+ * reduced into out[v]: SUM / MEAN / SYM (c_e = norm_col[u] * norm_row[v]) as sir_edge_agg_fwd, or
+ * SIR_AGG_MAX: elementwise max with the FIRST arg-max edge's destination-CSR position in arg
+ * (rows without edges: 0 / -1) — DGL fn.max.  Covers conv.py:45 with sigma = Sequential(act1,
+ * Linear(H, F), act2) (dictionary-lookup/model.py:17) and conv.py:46-47 (agg_type='max': W = W_R,
+ * act2 = identity).  No per-edge tensor is written.  fp32 throughout (MFMA fp32 products).
+ * W: [F, H] row-major (an nn.Linear weight), packed once by sir_edge_mlp_pack.  Limits: H % 4 == 0,
+ * H <= 512, F <= 256, Q/K 16-B aligned rows.  act2 in {IDENTITY, RELU}.  Split rows: pval
+ * (n_slots * F floats) and, for MAX, parg (n_slots * F ints).
+ * ------------------------------------------------------------------------------------------- */
+#define SIR_AGG_MAX 3
+int64_t sir_edge_mlp_pack_bytes(int64_t H, int64_t F);
+int sir_edge_mlp_pack(const float* W, int64_t H, int64_t F, void* packed, void* stream);
+int sir_edge_mlp_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                     const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,
+                     const float* Q, int64_t ldq, const float* K, int64_t ldk,
+                     const float* norm_row, const float* norm_col, int agg, int act1, float slope, int act2,
+                     const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda,
+                     float* pval, int32_t* parg, void* stream);
+
+/* Backward of the SUM / MEAN / SYM form (H, F <= 64): the destination pass writes dQ [rows, H] and one
+ * partial [dW (FP x HP) | db (FP)] row per wave into wpart (FP = F rounded up to 32, HP = H rounded up to
+ * 8; sir_edge_mlp_bwd_waves(n_items) rows of FP*HP + FP floats: sum them in row order, e.g. with
+ * sir_col_sum); MEAN also writes Gm = G / deg [rows, F] for the source pass.  The source pass
+ * (rows = sources, col = destinations) writes dK [rows, H] from Gd (= Gm for MEAN, else G).
+ * Split rows: partial = n_slots * H floats.  Deterministic (no atomics). */
+int64_t sir_edge_mlp_bwd_waves(int64_t n_items);
+int sir_edge_mlp_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,
+                         const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* G, int64_t ldg,
+                         const float* norm_row, const float* norm_col, int agg, int act1, float slope, int act2,
+                         const void* packed, const float* W, const float* bias, float* dQ, int64_t lddq,
+                         float* Gm, float* partial, float* wpart, void* stream);
+int sir_edge_mlp_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,
+                         const float* K, int64_t ldk, const float* Q, int64_t ldq, const float* Gd, int64_t ldg,
+                         const float* norm_row, const float* norm_col, int agg, int act1, float slope, int act2,
+                         const void* packed, const float* W, const float* bias, float* dK, int64_t lddk,
+                         float* partial, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * GraphNorm (models/norm.py:7-29) on a batched graph: graph b owns node rows [off[b], off[b+1])
  * (off = int64 [B+1], the prefix sum of batch_num_nodes).  Per graph and feature:
  *   mean = sum x / n,  d = x - mean * mean_scale,  std = sqrt(sum d^2 / n + eps),

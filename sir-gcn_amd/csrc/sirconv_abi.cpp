@@ -318,6 +318,108 @@ int sir_segment_max_bwd(const int32_t* items, int64_t n_items, int64_t F, const 
     return finish(fn, sir::run_seg_max_bwd(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
 }
 
+// ------------------------------------------------------------------------------ fused per-edge dense layer
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+static int check_mlp(const char* fn, const int32_t* rowptr, const int32_t* items, int64_t n_items,
+                     const int32_t* splits, int64_t n_splits, int64_t H, int64_t F, const float* Q, int64_t ldq,
+                     const float* K, int64_t ldk, int agg, int act1, int act2, const void* packed,
+                     const float* norm_row, const float* norm_col, bool bwd) {
+    if (agg < SIR_AGG_SUM || agg > SIR_AGG_MAX || (bwd && agg == SIR_AGG_MAX))
+        return fail(SIR_EINVAL, fn, bwd ? "agg must be SUM, MEAN or SYM" : "agg must be SUM, MEAN, SYM or MAX");
+    if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
+    if (act2 != SIR_ACT_IDENTITY && act2 != SIR_ACT_RELU) return fail(SIR_EUNSUPPORTED, fn, "act2 must be IDENTITY or RELU");
+    if (H <= 0 || H % 4 != 0 || H > (bwd ? 64 : 512)) return fail(SIR_EUNSUPPORTED, fn, bwd ? "H % 4 == 0 and H <= 64" : "H % 4 == 0 and H <= 512");
+    if (F <= 0 || F > (bwd ? 64 : 256)) return fail(SIR_EUNSUPPORTED, fn, bwd ? "F <= 64" : "F <= 256");
+    if (n_items < 0 || n_splits < 0 || n_items > INT32_MAX) return fail(SIR_EINVAL, fn, "bad item count");
+    if (n_items > 0 && (rowptr == nullptr || items == nullptr || packed == nullptr || Q == nullptr || K == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || !al16(Q) || !al16(K))
+        return fail(SIR_EUNSUPPORTED, fn, "Q/K rows must be 16-B aligned (ld % 4 == 0, ld >= H)");
+    if (n_splits > 0 && splits == nullptr) return fail(SIR_EINVAL, fn, "NULL splits");
+    if (agg == SIR_AGG_SYM && n_items > 0 && (norm_row == nullptr || norm_col == nullptr))
+        return fail(SIR_EINVAL, fn, "SYM needs norm_row and norm_col");
+    return SIR_OK;
+}
+
+int64_t sir_edge_mlp_pack_bytes(int64_t H, int64_t F) {
+    if (H <= 0 || F <= 0 || H > 512 || F > 256) return 0;
+    return sir::mlp_pack_floats((int)H, (int)F) * 4;
+}
+
+int sir_edge_mlp_pack(const float* W, int64_t H, int64_t F, void* packed, void* stream) {
+    const char* fn = "sir_edge_mlp_pack";
+    if (H <= 0 || F <= 0 || H > 512 || F > 256) return fail(SIR_EINVAL, fn, "H <= 512, F <= 256");
+    if (W == nullptr || packed == nullptr || !al16(packed)) return fail(SIR_EINVAL, fn, "NULL / unaligned buffer");
+    return finish(fn, sir::run_mlp_pack(W, (int)H, (int)F, packed, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_edge_mlp_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                     const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,
+                     const float* Q, int64_t ldq, const float* K, int64_t ldk,
+                     const float* norm_row, const float* norm_col, int agg, int act1, float slope, int act2,
+                     const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda,
+                     float* pval, int32_t* parg, void* stream) {
+    const char* fn = "sir_edge_mlp_fwd";
+    int rc = check_mlp(fn, rowptr, items, n_items, splits, n_splits, H, F, Q, ldq, K, ldk, agg, act1, act2, packed,
+                       norm_row, norm_col, false);
+    if (rc) return rc;
+    if (n_items > 0 && (out == nullptr || ldo < F)) return fail(SIR_EINVAL, fn, "out / ldo");
+    if (agg == SIR_AGG_MAX && n_items > 0 && (arg == nullptr || lda < F)) return fail(SIR_EINVAL, fn, "MAX needs arg");
+    if (n_splits > 0 && (pval == nullptr || (agg == SIR_AGG_MAX && parg == nullptr)))
+        return fail(SIR_EINVAL, fn, "split rows need pval (and parg for MAX)");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.splits = splits; a.n_splits = n_splits;
+    a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope;
+    a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.bias = bias;
+    a.out = out; a.ldo = ldo; a.arg = arg; a.lda = lda; a.pval = pval; a.parg = parg;
+    return finish(fn, sir::run_mlp_fwd(a, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int64_t sir_edge_mlp_bwd_waves(int64_t n_items) { return sir::mlp_bwd_waves(n_items); }
+
+int sir_edge_mlp_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,
+                         const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* G, int64_t ldg,
+                         const float* norm_row, const float* norm_col, int agg, int act1, float slope, int act2,
+                         const void* packed, const float* W, const float* bias, float* dQ, int64_t lddq,
+                         float* Gm, float* partial, float* wpart, void* stream) {
+    const char* fn = "sir_edge_mlp_bwd_dst";
+    int rc = check_mlp(fn, rowptr, items, n_items, splits, n_splits, H, F, Q, ldq, K, ldk, agg, act1, act2, packed,
+                       norm_row, norm_col, true);
+    if (rc) return rc;
+    if (n_items > 0 && (G == nullptr || ldg < F || W == nullptr || dQ == nullptr || lddq < H || wpart == nullptr))
+        return fail(SIR_EINVAL, fn, "G / W / dQ / wpart");
+    if (n_splits > 0 && partial == nullptr) return fail(SIR_EINVAL, fn, "split rows need partial");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.splits = splits; a.n_splits = n_splits;
+    a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.G = G; a.ldg = ldg; a.norm_row = norm_row; a.norm_col = norm_col;
+    a.slope = slope; a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.W = W; a.bias = bias;
+    a.out = dQ; a.ldo = lddq; a.pval = partial; a.Gm = (agg == SIR_AGG_MEAN) ? Gm : nullptr; a.wpart = wpart;
+    return finish(fn, sir::run_mlp_bwd(a, true, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_edge_mlp_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,
+                         const float* K, int64_t ldk, const float* Q, int64_t ldq, const float* Gd, int64_t ldg,
+                         const float* norm_row, const float* norm_col, int agg, int act1, float slope, int act2,
+                         const void* packed, const float* W, const float* bias, float* dK, int64_t lddk,
+                         float* partial, void* stream) {
+    const char* fn = "sir_edge_mlp_bwd_src";
+    int rc = check_mlp(fn, rowptr_s, items, n_items, splits, n_splits, H, F, Q, ldq, K, ldk, agg, act1, act2, packed,
+                       norm_row, norm_col, true);
+    if (rc) return rc;
+    if (n_items > 0 && (Gd == nullptr || ldg < F || W == nullptr || dK == nullptr || lddk < H))
+        return fail(SIR_EINVAL, fn, "Gd / W / dK");
+    if (n_splits > 0 && partial == nullptr) return fail(SIR_EINVAL, fn, "split rows need partial");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr_s; a.col = col_s; a.items = items; a.n_items = n_items; a.splits = splits; a.n_splits = n_splits;
+    a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.G = Gd; a.ldg = ldg; a.norm_row = norm_row; a.norm_col = norm_col;
+    a.slope = slope; a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.W = W; a.bias = bias;
+    a.out = dK; a.ldo = lddk; a.pval = partial; a.wpart = nullptr;
+    return finish(fn, sir::run_mlp_bwd(a, false, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
+}
+
 // ------------------------------------------------------------------------------ GraphNorm
 int sir_graph_norm_fwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
                        const float* weight, const float* bias, const float* mean_scale, float eps,

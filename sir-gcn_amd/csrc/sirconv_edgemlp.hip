@@ -1,0 +1,556 @@
+// sirconv_edgemlp.hip — a dense layer INSIDE the edge loop, fused with the gather and the reduce:
+//
+//   z_e = Q[v] + K[u],  a_e = act1(z_e),  h_e = W a_e + b,  m_e = act2(h_e)
+//   SUM / MEAN / SYM:  out[v] = sum_e c_e * m_e   (c_e = out_norm[u] * in_norm[v] for SYM, mean / deg)
+//   MAX:               out[v] = max_e m_e, arg[v] = first arg-max edge (DGL fn.max; empty rows 0 / -1)
+//
+// Two reference call sites are exactly this shape:
+//   * conv.py:45 with sigma = Sequential(ReLU, Linear(H, H), ReLU) (dictionary-lookup/model.py:17):
+//     act1 = ReLU, (W, b) = the sigma Linear, act2 = ReLU, reduce = sum/mean/sym;
+//   * conv.py:46-47 (agg_type='max'): the per-edge linear_relation: act1 = sigma, (W, b) = W_R, b_R,
+//     act2 = identity, reduce = max.
+// The reference materialises a_e and m_e as [E, H] / [E, F] tensors (DGL edge UDF); here one wave
+// owns a work item (a destination row, or a <= chunk-edge piece of a hub row), stages 32 edges'
+// a_e in LDS, runs h = a W^T on fp32 MFMA (v_mfma_f32_32x32x2_f32: full fp32 products, fp32
+// accumulation) with W streamed from L2 in fragment order, and reduces m_e in registers — no
+// [E, *] tensor in HBM.
+//
+// Backward of the sum family (H, F <= 64): a destination pass (dQ, and per-wave partial dW / db of
+// the layer) and a source pass (dK), each recomputing z, a, h for its edges:
+//   dm_e = g[v] * c_e,  dh_e = act2'(h_e) dm_e,  da_e = dh_e W,  dz_e = act1'(z_e) da_e,
+//   dQ[v] = sum dz_e,  dK[u] = sum dz_e,  dW = sum dh_e (x) a_e,  db = sum dh_e.
+// Accumulation orders are fixed (no atomics): run-to-run deterministic.
+#include "sirconv_edge_impl.h"
+
+namespace sir {
+namespace {
+
+typedef float mf16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ mf16 mfma32(float a, float b, mf16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// D-layout row (edge within the 32-edge tile) of accumulator register r in lane l
+__device__ __forceinline__ int drow(int r, int l) { return 8 * (r >> 2) + 4 * (l >> 5) + (r & 3); }
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float z, float slope) {
+    return sig<ACT>(z, slope);
+}
+
+// ------------------------------------------------------------------------------ weight packing
+// Forward operand B[k][n] = W[n][k] (W: [F, H] row-major, an nn.Linear weight): float4 per lane,
+// packed[(t * (HP / 8) + q) * 64 + l] = {W[32t + l%32][8q + 2j + l/32], j = 0..3}, 0 outside.
+__global__ void k_mlp_pack(const float* __restrict__ W, int H, int F, int HP, int FP, float4* __restrict__ out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nq = HP / 8;
+    const int64_t total = (int64_t)(FP / 32) * nq * 64;
+    if (idx >= total) return;
+    const int l = (int)(idx & 63);
+    const int q = (int)((idx >> 6) % nq);
+    const int t = (int)((idx >> 6) / nq);
+    const int n = 32 * t + (l & 31);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = 8 * q + 2 * j + (l >> 5);
+        v[j] = (n < F && k < H) ? W[(int64_t)n * H + k] : 0.f;
+    }
+    out[idx] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// ------------------------------------------------------------------------------ forward
+template <int ACT1, int ACT2, int RED, int NT>
+__global__ void __launch_bounds__(64)
+k_mlp_fwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
+          const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
+          const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope,
+          int H, int HP, int F, const float4* __restrict__ Wp, const float* __restrict__ bias,
+          float* __restrict__ out, int64_t ldo, int* __restrict__ arg, int64_t lda,
+          float* __restrict__ pval, int* __restrict__ parg) {
+    extern __shared__ float smem[];
+    const int pitch = HP + 1;
+    float* sA = smem;                    // [32][pitch] a_e
+    float* sC = smem + 32 * pitch;       // [32] c_e (0 past the tile's last edge)
+    const int l = threadIdx.x;
+    const int4 it = uniform_item(items, blockIdx.x);
+    const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
+    const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
+    const float* qp = Q + (int64_t)row * ldq;
+
+    float racc[NT], best[NT];
+    int bidx[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { racc[t] = 0.f; best[t] = -INFINITY; bidx[t] = INT_MAX; }
+    float bb[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int n = 32 * t + (l & 31);
+        bb[t] = (bias != nullptr && n < F) ? bias[n] : 0.f;
+    }
+
+    for (int t0 = e0; t0 < e1; t0 += 32) {
+        const int nv = (e1 - t0) < 32 ? (e1 - t0) : 32;
+        // ---- stage a = act1(Q[v] + K[u]) for the tile's edges (rows past nv: zeros)
+        for (int c0 = 0; c0 < HP; c0 += 256) {
+            const int k = c0 + 4 * l;
+            float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (k < H) q4 = *reinterpret_cast<const float4*>(qp + k);
+#pragma unroll 8
+            for (int i = 0; i < 32; ++i) {
+                float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (i < nv && k < H) {
+                    const int u = col[t0 + i];
+                    const float4 k4 = *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k);
+                    a4.x = act_f<ACT1>(q4.x + k4.x, slope); a4.y = act_f<ACT1>(q4.y + k4.y, slope);
+                    a4.z = act_f<ACT1>(q4.z + k4.z, slope); a4.w = act_f<ACT1>(q4.w + k4.w, slope);
+                }
+                if (k < HP) {
+                    float* d = sA + i * pitch + k;
+                    d[0] = a4.x; d[1] = a4.y; d[2] = a4.z; d[3] = a4.w;
+                }
+            }
+        }
+        if (l < 32) {
+            float c = 0.f;
+            if (l < nv) c = (RED == AGG_SYM) ? norm_col[col[t0 + l]] * nr : 1.f;   // conv.py:45 operand order
+            sC[l] = c;
+        }
+        __syncthreads();
+        // ---- h = a W^T on MFMA
+        mf16 acc[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+        const int nq = HP / 8;
+        const float* arow = sA + (l & 31) * pitch + (l >> 5);
+        for (int q = 0; q < nq; ++q) {
+            float av[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) av[j] = arow[8 * q + 2 * j];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float4 b4 = Wp[(int64_t)(t * nq + q) * 64 + l];
+                acc[t] = mfma32(av[0], b4.x, acc[t]);
+                acc[t] = mfma32(av[1], b4.y, acc[t]);
+                acc[t] = mfma32(av[2], b4.z, acc[t]);
+                acc[t] = mfma32(av[3], b4.w, acc[t]);
+            }
+        }
+        // ---- m = act2(h + b), reduced in edge order within the lane
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = drow(r, l);
+                if (i < nv) {
+                    const float m = act_f<ACT2>(acc[t][r] + bb[t], slope);
+                    if constexpr (RED == 3) {
+                        if (m > best[t]) { best[t] = m; bidx[t] = t0 + i; }    // strict >: first wins
+                    } else {
+                        racc[t] += sC[i] * m;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- the two half-waves hold interleaved edge groups of the same columns: combine, store
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int n = 32 * t + (l & 31);
+        if constexpr (RED == 3) {
+            const float ob = __shfl_xor(best[t], 32);
+            const int oi = __shfl_xor(bidx[t], 32);
+            if (ob > best[t] || (ob == best[t] && oi < bidx[t])) { best[t] = ob; bidx[t] = oi; }
+            if (l < 32 && n < F) {
+                const bool any = bidx[t] != INT_MAX;
+                if (slot < 0) {
+                    out[(int64_t)row * ldo + n] = any ? best[t] : 0.f;
+                    arg[(int64_t)row * lda + n] = any ? bidx[t] : -1;
+                } else {
+                    pval[(int64_t)slot * F + n] = best[t];
+                    parg[(int64_t)slot * F + n] = bidx[t];
+                }
+            }
+        } else {
+            const float other = __shfl_xor(racc[t], 32);
+            float v = (l < 32) ? racc[t] + other : other + racc[t];
+            if (l < 32 && n < F) {
+                if (slot < 0) {
+                    if constexpr (RED == AGG_MEAN) {
+                        const int d = e1 - e0;
+                        v = v / (float)(d > 1 ? d : 1);
+                    }
+                    out[(int64_t)row * ldo + n] = v;
+                } else {
+                    pval[(int64_t)slot * F + n] = v;
+                }
+            }
+        }
+    }
+}
+
+// max: combine the chunk partials of split rows in chunk (= edge) order, strict > (first wins)
+__global__ void k_mlp_max_combine(const int4* __restrict__ splits, int F, const float* __restrict__ pval,
+                                  const int* __restrict__ parg, float* __restrict__ Y, int64_t ldy,
+                                  int* __restrict__ arg, int64_t lda) {
+    const int4 sp = splits[blockIdx.x];
+    for (int f = threadIdx.x; f < F; f += blockDim.x) {
+        float b = pval[(int64_t)sp.y * F + f];
+        int a = parg[(int64_t)sp.y * F + f];
+        for (int k = 1; k < sp.z; ++k) {
+            const float v = pval[(int64_t)(sp.y + k) * F + f];
+            if (v > b) { b = v; a = parg[(int64_t)(sp.y + k) * F + f]; }
+        }
+        Y[(int64_t)sp.x * ldy + f] = b;
+        arg[(int64_t)sp.x * lda + f] = a;
+    }
+}
+
+// sum family: add the partial rows of split rows in slot order (mean: / degree)
+template <bool MEAN_DIV>
+__global__ void k_mlp_sum_combine(const int4* __restrict__ splits, int F, const float* __restrict__ pval,
+                                  float* __restrict__ out, int64_t ldo) {
+    const int4 sp = splits[blockIdx.x];
+    for (int f = threadIdx.x; f < F; f += blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < sp.z; ++k) s += pval[(int64_t)(sp.y + k) * F + f];
+        if (MEAN_DIV) s = s / (float)(sp.w > 1 ? sp.w : 1);
+        out[(int64_t)sp.x * ldo + f] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------ backward (sum family)
+// LDS image of one 32-edge tile: z (pre-activation of act1), a = act1(z), g-rows (source pass: the
+// gathered G[v] rows; destination pass: unused) and dh.  HP, FP <= 64.
+template <int ACT1, int ACT2, int RED, bool DST>
+__global__ void __launch_bounds__(64)
+k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
+          int64_t n_items, const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
+          const float* __restrict__ G, int64_t ldg, const float* __restrict__ norm_row,
+          const float* __restrict__ norm_col, float slope, int H, int HP, int F,
+          const float4* __restrict__ Wp, const float* __restrict__ W, const float* __restrict__ bias,
+          float* __restrict__ out, int64_t ldo, float* __restrict__ partial, float* __restrict__ Gm,
+          float* __restrict__ wpart) {
+    constexpr int NT = 2;                        // FP / 32 <= 2 and HP / 32 <= 2
+    __shared__ float sZ[32 * 65], sA[32 * 65], sG[32 * 65], sDH[32 * 65], sC[32];
+    const int pitch = 65;
+    const int l = threadIdx.x;
+    const int nt = (F + 31) / 32, nh = (HP + 31) / 32;
+    const int nq = HP / 8;
+    // per-wave partial dW [FP x HPad] (destination pass): tiles (tf, th) and db
+    mf16 dw[NT][NT];
+    float db[NT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a) {
+        db[a] = 0.f;
+#pragma unroll
+        for (int b = 0; b < NT; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dw[a][b][r] = 0.f;
+    }
+    float bb[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int n = 32 * t + (l & 31);
+        bb[t] = (bias != nullptr && n < F) ? bias[n] : 0.f;
+    }
+    for (int64_t w = blockIdx.x; w < n_items; w += gridDim.x) {
+        const int4 it = uniform_item(items, w);
+        const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
+        const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
+        // row-side vector: destination pass: Q[v] and g = G[v] (mean: / deg); source pass: K[u]
+        const float* rp = DST ? Q + (int64_t)row * ldq : K + (int64_t)row * ldk;
+        float gl = 0.f;                          // destination pass: g[n] of column n = l (F <= 64)
+        if (DST) {
+            float degf = 1.f;
+            bool first = true;
+            if (RED == AGG_MEAN) {
+                const int rs = rowptr[row];
+                const int d = rowptr[row + 1] - rs;
+                degf = (float)(d > 1 ? d : 1);
+                first = (e0 == rs);
+            }
+            if (l < F) {
+                gl = G[(int64_t)row * ldg + l];
+                if (RED == AGG_MEAN) {
+                    gl = gl / degf;
+                    if (Gm != nullptr && first) Gm[(int64_t)row * F + l] = gl;
+                }
+            }
+        }
+        float dacc[NT] = {0.f, 0.f};             // dQ / dK of column k = 32 t + l%32 (this lane's rows)
+        for (int t0 = e0; t0 < e1; t0 += 32) {
+            const int nv = (e1 - t0) < 32 ? (e1 - t0) : 32;
+            // ---- stage z, a (and the source pass's gathered g rows)
+            const int k = l;                     // HP <= 64: one column per lane
+            const float rv = (k < H) ? rp[k] : 0.f;
+            for (int i = 0; i < 32; ++i) {
+                float z = 0.f, gi = 0.f;
+                if (i < nv) {
+                    const int o = col[t0 + i];
+                    if (k < H) z = DST ? rv + K[(int64_t)o * ldk + k] : Q[(int64_t)o * ldq + k] + rv;
+                    if (!DST && k < F) gi = G[(int64_t)o * ldg + k];
+                }
+                if (k < HP) { sZ[i * pitch + k] = z; sA[i * pitch + k] = (i < nv) ? act_f<ACT1>(z, slope) : 0.f; }
+                if (!DST && k < 64) sG[i * pitch + k] = gi;
+            }
+            if (l < 32) {
+                float c = 0.f;
+                if (l < nv) {
+                    if (RED == AGG_SYM) {
+                        const int o = col[t0 + l];
+                        c = DST ? norm_col[o] * nr : nr * norm_col[o];     // out_norm[u] * in_norm[v]
+                    } else {
+                        c = 1.f;
+                    }
+                }
+                sC[l] = c;
+            }
+            __syncthreads();
+            // ---- h = a W^T + b (MFMA), dh = act2'(h) * (g * c), into sDH[i][n]
+            mf16 acc[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+            const float* arow = sA + (l & 31) * pitch + (l >> 5);
+            for (int q = 0; q < nq; ++q) {
+                float av[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) av[j] = arow[8 * q + 2 * j];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    if (t < nt) {
+                        const float4 b4 = Wp[(int64_t)(t * nq + q) * 64 + l];
+                        acc[t] = mfma32(av[0], b4.x, acc[t]);
+                        acc[t] = mfma32(av[1], b4.y, acc[t]);
+                        acc[t] = mfma32(av[2], b4.z, acc[t]);
+                        acc[t] = mfma32(av[3], b4.w, acc[t]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int n = 32 * t + (l & 31);
+                // g of column n: destination pass from the row vector (lane n holds it), source pass per edge
+                const float gn = __shfl(gl, n & 63);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = drow(r, l);
+                    float dh = 0.f;
+                    if (t < nt && i < nv && n < F) {
+                        const float gi = DST ? gn : sG[i * pitch + n];
+                        const float dm = gi * sC[i];                 // autograd of c * m: grad * c
+                        dh = dsig<ACT2>(acc[t][r] + bb[t], dm, slope);
+                    }
+                    if (t < nt) sDH[i * pitch + n] = dh;
+                    if (DST) db[t] += dh;
+                }
+            }
+            __syncthreads();
+            // ---- destination pass: dW[n][k] += sum_i dh[i][n] a[i][k]  (K = edges, 2 per MFMA)
+            if (DST) {
+#pragma unroll
+                for (int tf = 0; tf < NT; ++tf)
+#pragma unroll
+                    for (int th = 0; th < NT; ++th) {
+                        if (tf < nt && th < nh) {
+                            for (int s = 0; s < 16; ++s) {
+                                const int i = 2 * s + (l >> 5);
+                                const float av = sDH[i * pitch + 32 * tf + (l & 31)];
+                                const float bv = sA[i * pitch + 32 * th + (l & 31)];
+                                dw[tf][th] = mfma32(av, bv, dw[tf][th]);
+                            }
+                        }
+                    }
+            }
+            // ---- da[i][k] = sum_n dh[i][n] W[n][k]  (K = features), dz = act1'(z) da, summed per lane
+#pragma unroll
+            for (int th = 0; th < NT; ++th) {
+                if (th < nh) {
+                    mf16 da;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) da[r] = 0.f;
+                    const int kk = 32 * th + (l & 31);
+                    for (int s = 0; s < (nt * 32) / 2; ++s) {
+                        const int n = 2 * s + (l >> 5);
+                        const float av = sDH[(l & 31) * pitch + n];
+                        const float bv = (n < F && kk < H) ? W[(int64_t)n * H + kk] : 0.f;
+                        da = mfma32(av, bv, da);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int i = drow(r, l);
+                        if (i < nv && kk < H) dacc[th] += dsig<ACT1>(sZ[i * pitch + kk], da[r], slope);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // ---- dQ[v] (destination pass) / dK[u] (source pass): combine the half-waves, store
+#pragma unroll
+        for (int th = 0; th < NT; ++th) {
+            const float other = __shfl_xor(dacc[th], 32);
+            const float v = dacc[th] + other;
+            const int kk = 32 * th + (l & 31);
+            if (th < nh && l < 32 && kk < H) {
+                if (slot < 0) out[(int64_t)row * ldo + kk] = v;
+                else partial[(int64_t)slot * H + kk] = v;
+            }
+        }
+    }
+    if (DST) {   // this wave's partial dW [FP x HP] (row-major n, k) and db [FP]
+        const int FP = nt * 32;
+        const int64_t stride = (int64_t)FP * HP + FP;
+        float* wp = wpart + (int64_t)blockIdx.x * stride;
+#pragma unroll
+        for (int tf = 0; tf < NT; ++tf)
+#pragma unroll
+            for (int th = 0; th < NT; ++th) {
+                if (tf < nt && th < nh) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int n = 32 * tf + drow(r, l);      // MFMA rows = n, columns = k
+                        const int k = 32 * th + (l & 31);
+                        if (k < HP) wp[(int64_t)n * HP + k] = dw[tf][th][r];
+                    }
+                }
+            }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float v = db[t] + __shfl_xor(db[t], 32);
+            if (t < nt && l < 32) wp[(int64_t)FP * HP + 32 * t + l] = v;
+        }
+    }
+}
+
+template <int ACT1, int ACT2, int RED>
+hipError_t mlp_fwd_nt(int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeMlpArgs& a) {
+#define SIR_MLP_FWD(NTV)                                                                                     \
+    hipLaunchKernelGGL((k_mlp_fwd<ACT1, ACT2, RED, NTV>), grid, dim3(64), lds, st, a.rowptr, a.col,           \
+                       reinterpret_cast<const int4*>(a.items), a.Q, a.ldq, a.K, a.ldk, a.norm_row, a.norm_col, \
+                       a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.bias, a.out, a.ldo,  \
+                       a.arg, a.lda, a.pval, a.parg)
+    switch (nt) {
+        case 1: SIR_MLP_FWD(1); break;
+        case 2: SIR_MLP_FWD(2); break;
+        case 3: SIR_MLP_FWD(3); break;
+        case 4: SIR_MLP_FWD(4); break;
+        case 5: SIR_MLP_FWD(5); break;
+        case 6: SIR_MLP_FWD(6); break;
+        case 7: SIR_MLP_FWD(7); break;
+        default: SIR_MLP_FWD(8); break;
+    }
+#undef SIR_MLP_FWD
+    return hipGetLastError();
+}
+
+template <int ACT1, int ACT2>
+hipError_t mlp_fwd_red(int red, int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeMlpArgs& a) {
+    switch (red) {
+        case AGG_SUM: return mlp_fwd_nt<ACT1, ACT2, AGG_SUM>(nt, grid, lds, st, a);
+        case AGG_MEAN: return mlp_fwd_nt<ACT1, ACT2, AGG_MEAN>(nt, grid, lds, st, a);
+        case AGG_SYM: return mlp_fwd_nt<ACT1, ACT2, AGG_SYM>(nt, grid, lds, st, a);
+        default: return mlp_fwd_nt<ACT1, ACT2, 3>(nt, grid, lds, st, a);
+    }
+}
+
+template <int ACT1, int ACT2, int RED, bool DST>
+hipError_t mlp_bwd_launch(dim3 grid, hipStream_t st, const EdgeMlpArgs& a) {
+    hipLaunchKernelGGL((k_mlp_bwd<ACT1, ACT2, RED, DST>), grid, dim3(64), 0, st, a.rowptr, a.col,
+                       reinterpret_cast<const int4*>(a.items), a.n_items, a.Q, a.ldq, a.K, a.ldk, a.G, a.ldg,
+                       a.norm_row, a.norm_col, a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.W,
+                       a.bias, a.out, a.ldo, a.pval, a.Gm, a.wpart);
+    return hipGetLastError();
+}
+
+template <int ACT1, int ACT2, bool DST>
+hipError_t mlp_bwd_red(int red, dim3 grid, hipStream_t st, const EdgeMlpArgs& a) {
+    switch (red) {
+        case AGG_SUM: return mlp_bwd_launch<ACT1, ACT2, AGG_SUM, DST>(grid, st, a);
+        case AGG_MEAN: return mlp_bwd_launch<ACT1, ACT2, AGG_MEAN, DST>(grid, st, a);
+        default: return mlp_bwd_launch<ACT1, ACT2, AGG_SYM, DST>(grid, st, a);
+    }
+}
+
+// act1 in {identity, relu, leaky, gelu, gelu_tanh} x act2 in {identity, relu}
+template <typename Fn>
+hipError_t by_acts(int act1, int act2, Fn&& fn) {
+#define SIR_ACT2(A1)                                                               \
+    return act2 == ACT_RELU ? fn(std::integral_constant<int, A1>{}, std::integral_constant<int, ACT_RELU>{}) \
+                            : fn(std::integral_constant<int, A1>{}, std::integral_constant<int, ACT_IDENTITY>{})
+    switch (act1) {
+        case ACT_IDENTITY: SIR_ACT2(ACT_IDENTITY);
+        case ACT_RELU: SIR_ACT2(ACT_RELU);
+        case ACT_LEAKY: SIR_ACT2(ACT_LEAKY);
+        case ACT_GELU: SIR_ACT2(ACT_GELU);
+        default: SIR_ACT2(ACT_GELU_TANH);
+    }
+#undef SIR_ACT2
+}
+
+}  // namespace
+
+int64_t mlp_pack_floats(int H, int F) {
+    const int HP = (H + 7) / 8 * 8, FP = (F + 31) / 32 * 32;
+    return (int64_t)(FP / 32) * (HP / 8) * 64 * 4;
+}
+
+hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t st) {
+    const int HP = (H + 7) / 8 * 8, FP = (F + 31) / 32 * 32;
+    const int64_t n = (int64_t)(FP / 32) * (HP / 8) * 64;
+    hipLaunchKernelGGL(k_mlp_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, F, HP, FP,
+                       static_cast<float4*>(packed));
+    return hipGetLastError();
+}
+
+hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st) {
+    if (a.n_items > 0) {
+        const int nt = (a.F + 31) / 32;
+        const size_t lds = (size_t)(32 * (a.HP + 1) + 32) * sizeof(float);
+        const dim3 grid((unsigned)a.n_items);
+        hipError_t err = by_acts(act1, act2, [&](auto A1, auto A2) {
+            return mlp_fwd_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, lds, st, a);
+        });
+        if (err != hipSuccess) return err;
+    }
+    if (a.n_splits > 0) {
+        const dim3 g((unsigned)a.n_splits);
+        if (red == 3)
+            hipLaunchKernelGGL(k_mlp_max_combine, g, dim3(256), 0, st, reinterpret_cast<const int4*>(a.splits), a.F,
+                               a.pval, a.parg, a.out, a.ldo, a.arg, a.lda);
+        else if (red == AGG_MEAN)
+            hipLaunchKernelGGL(k_mlp_sum_combine<true>, g, dim3(256), 0, st, reinterpret_cast<const int4*>(a.splits),
+                               a.F, a.pval, a.out, a.ldo);
+        else
+            hipLaunchKernelGGL(k_mlp_sum_combine<false>, g, dim3(256), 0, st, reinterpret_cast<const int4*>(a.splits),
+                               a.F, a.pval, a.out, a.ldo);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
+int mlp_bwd_waves(int64_t n_items) { return (int)(n_items < 2048 ? (n_items > 0 ? n_items : 1) : 2048); }
+
+hipError_t run_mlp_bwd(const EdgeMlpArgs& a, bool dst, int red, int act1, int act2, hipStream_t st) {
+    if (a.n_items > 0) {
+        const dim3 grid((unsigned)mlp_bwd_waves(a.n_items));
+        hipError_t err = by_acts(act1, act2, [&](auto A1, auto A2) {
+            return dst ? mlp_bwd_red<decltype(A1)::value, decltype(A2)::value, true>(red, grid, st, a)
+                       : mlp_bwd_red<decltype(A1)::value, decltype(A2)::value, false>(red, grid, st, a);
+        });
+        if (err != hipSuccess) return err;
+    }
+    if (a.n_splits > 0) {      // the rows' partial dQ / dK (H wide) in slot order
+        hipLaunchKernelGGL(k_mlp_sum_combine<false>, dim3((unsigned)a.n_splits), dim3(256), 0, st,
+                           reinterpret_cast<const int4*>(a.splits), a.H, a.pval, a.out, a.ldo);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
+}  // namespace sir

@@ -106,6 +106,37 @@ hipError_t run_csr_build(const int64_t* rows, const int64_t* cols, int64_t E, in
 hipError_t run_csr_perm(const int64_t* eid_a, const int64_t* eid_b, int64_t E, int* pos_ws, int* perm,
                         hipStream_t st);
 
+// per-edge dense layer fused with the gather and the reduce, sirconv_edgemlp.hip
+struct EdgeMlpArgs {
+    const int* rowptr;
+    const int* col;
+    const int32_t* items;
+    int64_t n_items;
+    const int32_t* splits;
+    int64_t n_splits;
+    const float* Q;  int64_t ldq;
+    const float* K;  int64_t ldk;
+    const float* G;  int64_t ldg;        // backward: dS rows (destination pass) / G or Gm rows (source pass)
+    const float* norm_row;
+    const float* norm_col;
+    float slope;                        // act1's LeakyReLU slope
+    int H, HP, F;                       // a width, a width padded to 8, output width
+    const void* Wp;                     // packed W (run_mlp_pack)
+    const float* W;                     // W [F, H] row-major (backward)
+    const float* bias;                  // [F] or NULL
+    float* out;  int64_t ldo;           // forward: [rows, F]; backward: dQ / dK [rows, H]
+    int* arg;  int64_t lda;             // forward MAX
+    float* pval;                        // split partials (values)
+    int* parg;                          // split partials (MAX args)
+    float* Gm;                          // backward destination pass, MEAN: g / deg rows [rows, F]
+    float* wpart;                       // backward destination pass: per-wave partial [dW | db]
+};
+int64_t mlp_pack_floats(int H, int F);
+hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t st);
+hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st);
+int mlp_bwd_waves(int64_t n_items);
+hipError_t run_mlp_bwd(const EdgeMlpArgs& a, bool dst, int red, int act1, int act2, hipStream_t st);
+
 // projection GEMMs, sirconv_gemm.hip
 int64_t gemm_pack_bytes(int64_t N, int64_t K);
 hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st);

@@ -49,6 +49,15 @@ SIGNATURES = {
                                             _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P]),
     "sir_edge_agg_bwd_src": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
                                             _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _P]),
+    "sir_edge_mlp_pack_bytes": (ctypes.c_int64, [_I64, _I64]),
+    "sir_edge_mlp_pack": (ctypes.c_int, [_P, _I64, _I64, _P, _P]),
+    "sir_edge_mlp_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _I, _I,
+                                        _F, _I, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
+    "sir_edge_mlp_bwd_waves": (ctypes.c_int64, [_I64]),
+    "sir_edge_mlp_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
+                                            _P, _P, _I, _I, _F, _I, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
+    "sir_edge_mlp_bwd_src": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
+                                            _P, _P, _I, _I, _F, _I, _P, _P, _P, _P, _I64, _P, _P]),
     "sir_edge_agg_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _P, _I64, _I64, _I, _P,
                                         _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P, _P]),
 }

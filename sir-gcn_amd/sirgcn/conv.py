@@ -222,11 +222,14 @@ class SIRConv(nn.Module):
     .. math::  h_u^* = \sum_{v \in \mathcal{N}(u)} W_R \, \sigma(W_Q h_u + W_K h_v)
 
     Same parameters as the reference (``conv.py:13-31``).  ``sum``/``mean``/``sym`` with an
-    elementwise sigma (ReLU, LeakyReLU, GELU, Identity) run on the fused edge kernels; ``max`` and
-    any other sigma callable run on the edge-materialised native path (``sirgcn.generic``).
+    elementwise sigma (ReLU, LeakyReLU, GELU, Identity) run on the fused edge kernels; ``max`` with
+    an elementwise sigma and a ``Sequential(act, Linear, ReLU)`` sigma run on the fused edge-MLP
+    kernels (``sirgcn.edgemlp``); any other sigma callable runs on the edge-materialised native
+    path (``sirgcn.generic``).
     """
 
     use_fused = True      # whole-layer Function when dropout is off and inputs are fp32
+    fuse_edge_mlp = True  # Sequential sigma / max aggregation on the fused edge-MLP kernels (sirgcn.edgemlp)
 
     def __init__(self, input_dim, hidden_dim, output_dim, activation, dropout=0, inner_bias=True,
                  outer_bias=True, agg_type='sum'):
@@ -272,10 +275,26 @@ class SIRConv(nn.Module):
             act, slope = activation_code(self.activation)
         except NotImplementedError:
             act = None
+        H = self.linear_query.out_features
+        if self.fuse_edge_mlp and feat_query.dtype != torch.float64:
+            from .edgemlp import EdgeMaxLinear, EdgeMLPSum, max_supported, seq_sigma
+            if self._agg_type == "max" and act is not None and \
+                    max_supported(H, self.linear_relation.out_features):
+                # conv.py:46-47 + fn.max: per-edge W_R fused with the gather and the running max
+                QK = self._project(feat_key, feat_query)
+                Y = EdgeMaxLinear.apply(QK, self.linear_relation.weight, self.linear_relation.bias, plan, H, act,
+                                        slope)
+                return Y.to(QK.dtype)
+            sq = seq_sigma(self.activation, H) if act is None and self._agg_type != "max" else None
+            if sq is not None:
+                # conv.py:45 with sigma = Sequential(act1, Linear, act2): the Linear runs inside the edge loop
+                a1, sl, lin, a2 = sq
+                QK = self._project(feat_key, feat_query)
+                S = EdgeMLPSum.apply(QK, lin.weight, lin.bias, plan, H, self._agg_type, a1, sl, a2)
+                return self.linear_relation(S.to(QK.dtype))
         if act is None or self._agg_type == "max":
             from .generic import generic_forward       # edge-materialised native path
             return generic_forward(self, plan, feat_key, feat_query)
-        H = self.linear_query.out_features
         fused = (self.use_fused and feat_key is feat_query and feat_query.dtype == torch.float32 and feat_query.is_cuda
                  and not torch.is_autocast_enabled() and not (self.training and self.dropout.p > 0)
                  and self.linear_query.weight.dtype == torch.float32)

@@ -1,0 +1,216 @@
+"""Fused per-edge dense layer (``sir_edge_mlp_*``, csrc/sirconv_edgemlp.hip): the two SIRConv forms
+whose message runs a Linear on every edge, without any [E, *] tensor in the forward.
+
+* ``Sequential(act1, Linear(H, F), act2)`` sigma (``dictionary-lookup/model.py:17``, used through
+  ``conv.py:45``) with sum / mean / sym: :class:`EdgeMLPSum` — forward and backward fused (the
+  backward kernels cover H, F <= 64; the config-1 shape is H = F = 64).
+* ``agg_type='max'`` (``conv.py:46-47``: ``linear_relation`` per edge, DGL ``fn.max``):
+  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge); the backward
+  recomputes the edge activations once (the gradient needs the arg edges' activations, dW_R is an
+  edge-contracted GEMM) and runs them through the native gather / GEMM / segment kernels.
+
+Everything is fp32; a CPU tensor or a shape outside the kernels' limits is never silently served
+by another path — :func:`seq_sigma` / :func:`max_supported` say up front which form applies.
+"""
+import ctypes
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from . import _native, linalg
+
+AGG_MAX = 3
+
+
+def _elementwise_code(m):
+    """Kernel code of an elementwise activation module (None if not one of the kernel's)."""
+    if isinstance(m, nn.LeakyReLU):
+        return _native.ACT_LEAKY, float(m.negative_slope)
+    if isinstance(m, nn.ReLU):
+        return _native.ACT_RELU, 0.0
+    if isinstance(m, nn.GELU):
+        return (_native.ACT_GELU_TANH if m.approximate == "tanh" else _native.ACT_GELU), 0.0
+    if isinstance(m, nn.Identity):
+        return _native.ACT_IDENTITY, 0.0
+    return None
+
+
+def seq_sigma(act, H):
+    """(act1, slope, linear, act2) when ``act`` is Sequential(elementwise, Linear(H, F), ReLU|Identity)
+    within the fused kernels' limits, else None."""
+    if not isinstance(act, nn.Sequential) or len(act) != 3:
+        return None
+    a1, lin, a2 = act[0], act[1], act[2]
+    c1 = _elementwise_code(a1)
+    c2 = _elementwise_code(a2)
+    if c1 is None or c2 is None or c2[0] not in (_native.ACT_RELU, _native.ACT_IDENTITY):
+        return None
+    if not isinstance(lin, nn.Linear) or lin.in_features != H or H % 4 or H > 64 or lin.out_features > 64:
+        return None
+    return c1[0], c1[1], lin, c2[0]
+
+
+def max_supported(H, O):
+    return H % 4 == 0 and H <= 512 and O <= 256
+
+
+def _pack(W):
+    lib = _native.load()
+    Fo, H = W.shape
+    nbytes = lib.sir_edge_mlp_pack_bytes(H, Fo)
+    packed = torch.empty((nbytes,), dtype=torch.uint8, device=W.device)
+    rc = lib.sir_edge_mlp_pack(_native._ptr(W), H, Fo, _native._ptr(packed), _native._stream(W.device))
+    _native._check(rc, lib)
+    return packed
+
+
+def _fwd(plan, Q, K, W, b, agg, act1, slope, act2, out, arg=None):
+    lib = _native.load()
+    csr = plan.dst
+    Fo, H = W.shape
+    in_norm, out_norm = plan.norms(agg if agg != "max" else "sum")
+    packed = _pack(W)
+    n = csr.n_slots
+    pval = torch.empty((max(n, 1) * Fo,), device=Q.device, dtype=torch.float32) if n else None
+    parg = torch.empty((max(n, 1) * Fo,), device=Q.device, dtype=torch.int32) if (n and arg is not None) else None
+    code = AGG_MAX if agg == "max" else _native.AGG[agg]
+    P = _native._ptr
+    with _native._Timed("sir_edge_mlp_fwd", Q.device, 2 * csr.col.numel() * H * Fo):
+        rc = lib.sir_edge_mlp_fwd(P(csr.rowptr), P(csr.col), P(csr.items), csr.n_items, P(csr.splits), csr.n_splits,
+                                  H, Fo, P(Q), Q.stride(0), P(K), K.stride(0), P(in_norm), P(out_norm), code, act1,
+                                  float(slope), act2, P(packed), P(b), P(out), out.stride(0), P(arg),
+                                  arg.stride(0) if arg is not None else Fo, P(pval), P(parg), _native._stream(Q.device))
+    _native._check(rc, lib)
+    return packed
+
+
+class EdgeMLPSum(torch.autograd.Function):
+    """S[v] = sum_e c_e act2(W act1(Q[v] + K[u]) + b) (mean: / deg) for QK = [Q | K]."""
+
+    @staticmethod
+    def forward(ctx, QK, W, b, plan, H, agg, act1, slope, act2):
+        if QK.device.type != "cuda":
+            raise RuntimeError("sirgcn fused edge MLP needs a ROCm GPU tensor (no CPU fallback)")
+        QK = QK.contiguous().float()
+        W = W.contiguous().float()
+        b = b.contiguous().float() if b is not None else None
+        Fo = W.shape[0]
+        S = torch.empty((plan.dst.n_rows, Fo), device=QK.device, dtype=torch.float32)
+        packed = _fwd(plan, QK[:, :H], QK[:, H:], W, b, agg, act1, slope, act2, S)
+        ctx.save_for_backward(QK, W, b if b is not None else W.new_zeros(0), packed)
+        ctx.plan, ctx.H, ctx.agg, ctx.act1, ctx.slope, ctx.act2, ctx.has_b = plan, H, agg, act1, slope, act2, b is not None
+        return S
+
+    @staticmethod
+    def backward(ctx, dS):
+        QK, W, b, packed = ctx.saved_tensors
+        plan, H, agg, act1, slope, act2 = ctx.plan, ctx.H, ctx.agg, ctx.act1, ctx.slope, ctx.act2
+        lib = _native.load()
+        P = _native._ptr
+        G = dS.contiguous().float()
+        Fo = W.shape[0]
+        dev = G.device
+        bias = b if ctx.has_b else None
+        in_norm, out_norm = plan.norms(agg)
+        Q, K = QK[:, :H], QK[:, H:]
+        dQK = torch.empty_like(QK)
+        d, s = plan.dst, plan.src
+        waves = lib.sir_edge_mlp_bwd_waves(d.n_items)
+        FP, HP = (Fo + 31) // 32 * 32, (H + 7) // 8 * 8
+        wpart = torch.empty((waves, FP * HP + FP), device=dev, dtype=torch.float32)
+        part = torch.empty((max(d.n_slots, s.n_slots, 1) * H,), device=dev, dtype=torch.float32)
+        Gm = torch.empty((d.n_rows, Fo), device=dev, dtype=torch.float32) if agg == "mean" else None
+        st = _native._stream(dev)
+        code = _native.AGG[agg]
+        with _native._Timed("sir_edge_mlp_bwd_dst", dev):
+            rc = lib.sir_edge_mlp_bwd_dst(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, Fo,
+                                          P(Q), Q.stride(0), P(K), K.stride(0), P(G), G.stride(0), P(in_norm),
+                                          P(out_norm), code, act1, float(slope), act2, P(packed), P(W), P(bias),
+                                          P(dQK), dQK.stride(0), P(Gm), P(part), P(wpart), st)
+        _native._check(rc, lib)
+        Gd = Gm if Gm is not None else G
+        with _native._Timed("sir_edge_mlp_bwd_src", dev):
+            rc = lib.sir_edge_mlp_bwd_src(P(s.rowptr), P(s.col), P(s.items), s.n_items, P(s.splits), s.n_splits, H, Fo,
+                                          P(K), K.stride(0), P(Q), Q.stride(0), P(Gd), Gd.stride(0), P(out_norm),
+                                          P(in_norm), code, act1, float(slope), act2, P(packed), P(W), P(bias),
+                                          P(dQK[:, H:]), dQK.stride(0), P(part), st)
+        _native._check(rc, lib)
+        tot = _native.col_sum(wpart)                    # per-wave partials summed in wave order
+        dW = tot[:FP * HP].view(FP, HP)[:Fo, :H].contiguous()
+        db = tot[FP * HP:FP * HP + Fo].contiguous() if ctx.has_b else None
+        return dQK, dW, db, None, None, None, None, None, None
+
+
+class EdgeMaxLinear(torch.autograd.Function):
+    """Y[v] = max_e (W_R act1(Q[v] + K[u]) + b_R), first arg-max edge (DGL fn.max), empty rows 0."""
+
+    @staticmethod
+    def forward(ctx, QK, W, b, plan, H, act1, slope):
+        if QK.device.type != "cuda":
+            raise RuntimeError("sirgcn fused max path needs a ROCm GPU tensor (no CPU fallback)")
+        QK = QK.contiguous().float()
+        W = W.contiguous().float()
+        b = b.contiguous().float() if b is not None else None
+        O = W.shape[0]
+        V = plan.dst.n_rows
+        Y = torch.empty((V, O), device=QK.device, dtype=torch.float32)
+        arg = torch.empty((V, O), device=QK.device, dtype=torch.int32)
+        _fwd(plan, QK[:, :H], QK[:, H:], W, b, "max", act1, slope, _native.ACT_IDENTITY, Y, arg)
+        ctx.save_for_backward(QK, W, arg)
+        ctx.plan, ctx.H, ctx.act1, ctx.slope, ctx.has_b = plan, H, act1, slope, b is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        QK, W, arg = ctx.saved_tensors
+        plan, H, act1, slope = ctx.plan, ctx.H, ctx.act1, ctx.slope
+        dY = dY.contiguous().float()
+        E = plan.dst.col.numel()
+        O = W.shape[0]
+        dev = dY.device
+        # the arg edges' activations are needed for dW_R: recompute z_e once (no copy kept from the forward)
+        Z = torch.empty((E, H), device=dev, dtype=torch.float32)
+        _native.edge_gather_add(plan.dst, QK[:, :H], QK[:, H:], Z)
+        A = _act(Z, act1, slope)
+        dM = torch.empty((E, O), device=dev, dtype=torch.float32)
+        _native.segment_max_bwd(plan.dst, arg, dY, dM)                 # dY to the first arg-max edge
+        dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
+        del A
+        dA = linalg.mm_w(dM, W)                                        # [E, H]
+        del dM
+        dZ = _act_bwd(Z, dA, act1, slope)
+        del Z, dA
+        dQK = torch.empty_like(QK)
+        n_slots = max(plan.dst.n_slots, plan.src.n_slots)
+        part = torch.empty((max(n_slots, 1) * H,), device=dev, dtype=torch.float32) if n_slots else None
+        _native.segment_sum(plan.dst, dZ, dQK[:, :H], partial=part)                     # dQ
+        _native.segment_sum(plan.src, dZ, dQK[:, H:], perm=plan.src.perm, partial=part)  # dK
+        return dQK, dW, (db if ctx.has_b else None), None, None, None, None
+
+
+def _act(z, code, slope):
+    if code == _native.ACT_RELU:
+        return torch.relu(z)
+    if code == _native.ACT_LEAKY:
+        return F.leaky_relu(z, slope)
+    if code == _native.ACT_GELU:
+        return F.gelu(z)
+    if code == _native.ACT_GELU_TANH:
+        return F.gelu(z, approximate="tanh")
+    return z.clone()
+
+
+def _act_bwd(z, g, code, slope):
+    """sigma'(z) * g as torch's backward computes it (in place into g where possible)."""
+    if code == _native.ACT_RELU:
+        return g.masked_fill_(z <= 0, 0.0)
+    if code == _native.ACT_LEAKY:
+        return torch.where(z > 0, g, g * slope)
+    if code in (_native.ACT_GELU, _native.ACT_GELU_TANH):
+        zz = z.detach().requires_grad_(True)
+        with torch.enable_grad():
+            y = _act(zz, code, slope)
+            (r,) = torch.autograd.grad(y, zz, g)
+        return r
+    return g

@@ -6,7 +6,8 @@ their autograd: ``mm_wt`` = A W^T (+ b) (forward projections), ``mm_w`` = A W (G
 dX = dQK [W_Q; W_K]), ``mm_tn`` = A^T B (the weight gradients, contraction over the node rows).
 fp32 in / fp32 out at fp32 accuracy (tests/test_gemm_gpu.py).  Operands the kernels do not take
 (CPU tensors of the gloo rehearsals, non-fp32, feature widths not a multiple of 4, unaligned
-views) go to torch's own GEMM; ``USE_NATIVE = False`` forces that for A/B runs.
+views, fewer than ``MIN_ROWS`` node rows) go to torch's own GEMM; ``USE_NATIVE = False`` forces that
+for A/B runs.
 """
 import torch
 
@@ -15,10 +16,14 @@ from . import _native
 USE_NATIVE = True
 MAX_DIM = 65536          # N, K (and M, N of the TN GEMM) limit of the native kernels
 MAX_LD = 1 << 20         # SIR_GEMM_MAX_LD (include/sirconv.h)
+# Below this many node rows the native kernels (256-row tiles, split-K over rows) cannot fill the
+# 256 CUs and the call is launch-bound: small batches (config 5: ~1.6k nodes) use torch's fp32 GEMM
+# (hipBLASLt), which is also IEEE fp32.
+MIN_ROWS = 32768
 
 
 def _ok(t):
-    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and t.shape[0] >= MIN_ROWS
             and t.stride(0) % 4 == 0 and t.shape[1] % 4 == 0 and t.data_ptr() % 16 == 0
             and t.shape[1] <= MAX_DIM and t.stride(0) <= MAX_LD)
 
@@ -48,7 +53,7 @@ def mm_w(A, W):
 
 
 def _tn_ok(t):
-    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and t.shape[0] >= MIN_ROWS
             and 0 < t.shape[1] <= MAX_DIM and t.stride(0) <= MAX_LD)
 
 

@@ -32,6 +32,18 @@ def load_case(name):
         return {k: z[k] for k in z.files}
 
 
+@pytest.fixture(autouse=True)
+def _native_gemm_at_every_size():
+    """The product routes GEMMs with fewer than linalg.MIN_ROWS node rows to torch (launch-bound
+    sizes); the tests' small graphs would then never reach the native split-fp16 MFMA kernels, so
+    the suite lowers the threshold to 0 (every fp32 GEMM the kernels accept runs natively)."""
+    from sirgcn import linalg
+    old = linalg.MIN_ROWS
+    linalg.MIN_ROWS = 0
+    yield
+    linalg.MIN_ROWS = old
+
+
 @pytest.fixture(scope="session")
 def manifest():
     return golden_manifest()
