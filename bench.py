@@ -67,6 +67,8 @@ def parse():
                     help="nccl (= RCCL) for real runs; gloo to rehearse N ranks (CPU without a GPU)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the edge-cut (sirgcn.dist) code path even at world size 1")
+    ap.add_argument("--no-capture", action="store_true",
+                    help="stack workloads: launch every kernel from Python instead of replaying a captured HIP graph")
     ap.add_argument("--no-dual", action="store_true",
                     help="A/B only: the two backward edge passes as two launches instead of one")
     ap.add_argument("--torch-gemm", action="store_true",
@@ -493,13 +495,33 @@ def run_stack(args, world, rank, dev, torch, dist):
         model.zero_grad(set_to_none=True)
         X.grad = None
         if dt != torch.float32:
-            with torch.autocast("cuda", dtype=dt):
+            with torch.autocast("cuda", dtype=dt, cache_enabled=False):
                 Y = model(g, X)
         else:
             Y = model(g, X)
         Y.backward(dY.to(Y.dtype))
 
-    el, timing = timed_loop(step, args.steps, args.warmup, world, dist, dev)
+    # Batched small graphs are launch-bound (SURVEY §7 "tiny batched graphs"): at N = 1 the whole
+    # fwd+bwd step (every kernel, every ctypes launch, the allocator's work) is captured once into
+    # a HIP graph and replayed; per-kernel HIP-event timing is then measured on the eager step.
+    captured = None
+    if world == 1 and not args.no_capture:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        captured = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(captured):
+            step()
+        torch.cuda.synchronize(dev)
+    if captured is not None:
+        _, timing = timed_loop(step, 3, 1, world, dist, dev)          # eager: per-kernel events
+        el, _ = timed_loop(captured.replay, args.steps, args.warmup, world, dist, dev)
+    else:
+        el, timing = timed_loop(step, args.steps, args.warmup, world, dist, dev)
     el = max_over_ranks(el, world, dist, dev)
     L, H, E, V = c["layers"], c["hidden"], g.num_edges(), g.num_nodes()
     tot = torch.tensor([E, V, g.batch_size], dtype=torch.float64, device=dev)
@@ -509,6 +531,7 @@ def run_stack(args, world, rank, dev, torch, dist):
     from sirgcn.conv import EdgeAggregate
     masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY))
     kernels, gemm = kernel_table(timing, lambda n: V, E, H, c["agg"], masked, SIZEOF[dtn])
+    eager_steps = 3 if captured is not None else args.steps
     out = {"metric": "layer-edges/sec SIRConv stack fwd+bwd (E x layers / step time)",
            "value": round(E_all * L / (el / args.steps), 1), "unit": "edges/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
@@ -518,9 +541,11 @@ def run_stack(args, world, rank, dev, torch, dist):
                                   f"{' per rank, DDP over RCCL' if world > 1 else ''}",
                       "graphs_per_s": round(B_all / (el / args.steps), 1), "V_total": V_all, "E_total": E_all,
                       "parallelism": f"data-parallel x{world}" if world > 1 else "single GPU"},
-           "kernels": kernels}
+           "kernels": kernels, "hip_graph": captured is not None}
+    if captured is not None:
+        out["kernels_note"] = "per-kernel times from 3 eager steps; value / ms_per_step from the replayed HIP graph"
     if gemm:
-        out["projections"] = projections(gemm, args.steps)
+        out["projections"] = projections(gemm, eager_steps)
     return out
 
 

@@ -61,8 +61,10 @@ __global__ void k_mlp_pack(const float* __restrict__ W, int H, int F, int HP, in
 }
 
 // ------------------------------------------------------------------------------ forward
-template <int ACT1, int ACT2, int RED, int NT>
-__global__ void __launch_bounds__(64)
+// One block per work item: NW waves share the staged a-tile (LDS) of 32 edges; wave w computes the
+// output tiles t = w + NW * j (j < TPW) of 32 features each.
+template <int ACT1, int ACT2, int RED, int NW, int TPW>
+__global__ void __launch_bounds__(64 * NW)
 k_mlp_fwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
           const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
           const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope,
@@ -73,32 +75,33 @@ k_mlp_fwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
     const int pitch = HP + 1;
     float* sA = smem;                    // [32][pitch] a_e
     float* sC = smem + 32 * pitch;       // [32] c_e (0 past the tile's last edge)
-    const int l = threadIdx.x;
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int4 it = uniform_item(items, blockIdx.x);
     const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
     const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
     const float* qp = Q + (int64_t)row * ldq;
+    const int nq = HP / 8;
+    const int ntile = (F + 31) / 32;
 
-    float racc[NT], best[NT];
-    int bidx[NT];
+    float racc[TPW], best[TPW], bb[TPW];
+    int bidx[TPW];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) { racc[t] = 0.f; best[t] = -INFINITY; bidx[t] = INT_MAX; }
-    float bb[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int n = 32 * t + (l & 31);
-        bb[t] = (bias != nullptr && n < F) ? bias[n] : 0.f;
+    for (int j = 0; j < TPW; ++j) {
+        racc[j] = 0.f; best[j] = -INFINITY; bidx[j] = INT_MAX;
+        const int n = 32 * (w + NW * j) + (l & 31);
+        bb[j] = (bias != nullptr && n < F) ? bias[n] : 0.f;
     }
 
     for (int t0 = e0; t0 < e1; t0 += 32) {
         const int nv = (e1 - t0) < 32 ? (e1 - t0) : 32;
-        // ---- stage a = act1(Q[v] + K[u]) for the tile's edges (rows past nv: zeros)
+        // ---- stage a = act1(Q[v] + K[u]) (wave w: rows w, w + NW, ...; rows past nv: zeros)
         for (int c0 = 0; c0 < HP; c0 += 256) {
             const int k = c0 + 4 * l;
             float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
             if (k < H) q4 = *reinterpret_cast<const float4*>(qp + k);
 #pragma unroll 8
-            for (int i = 0; i < 32; ++i) {
+            for (int i = w; i < 32; i += NW) {
                 float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (i < nv && k < H) {
                     const int u = col[t0 + i];
@@ -112,45 +115,46 @@ k_mlp_fwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
                 }
             }
         }
-        if (l < 32) {
+        if (w == 0 && l < 32) {
             float c = 0.f;
             if (l < nv) c = (RED == AGG_SYM) ? norm_col[col[t0 + l]] * nr : 1.f;   // conv.py:45 operand order
             sC[l] = c;
         }
         __syncthreads();
-        // ---- h = a W^T on MFMA
-        mf16 acc[NT];
+        // ---- h = a W^T on MFMA (this wave's output tiles)
+        mf16 acc[TPW];
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+        for (int j = 0; j < TPW; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-        const int nq = HP / 8;
+            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
         const float* arow = sA + (l & 31) * pitch + (l >> 5);
         for (int q = 0; q < nq; ++q) {
             float av[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) av[j] = arow[8 * q + 2 * j];
+            for (int jj = 0; jj < 4; ++jj) av[jj] = arow[8 * q + 2 * jj];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) {
+            for (int j = 0; j < TPW; ++j) {
+                const int t = w + NW * j;
+                if (t >= ntile) continue;            // wave-uniform: tiles past F have no packed W
                 const float4 b4 = Wp[(int64_t)(t * nq + q) * 64 + l];
-                acc[t] = mfma32(av[0], b4.x, acc[t]);
-                acc[t] = mfma32(av[1], b4.y, acc[t]);
-                acc[t] = mfma32(av[2], b4.z, acc[t]);
-                acc[t] = mfma32(av[3], b4.w, acc[t]);
+                acc[j] = mfma32(av[0], b4.x, acc[j]);
+                acc[j] = mfma32(av[1], b4.y, acc[j]);
+                acc[j] = mfma32(av[2], b4.z, acc[j]);
+                acc[j] = mfma32(av[3], b4.w, acc[j]);
             }
         }
         // ---- m = act2(h + b), reduced in edge order within the lane
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
+        for (int j = 0; j < TPW; ++j) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int i = drow(r, l);
                 if (i < nv) {
-                    const float m = act_f<ACT2>(acc[t][r] + bb[t], slope);
+                    const float m = act_f<ACT2>(acc[j][r] + bb[j], slope);
                     if constexpr (RED == 3) {
-                        if (m > best[t]) { best[t] = m; bidx[t] = t0 + i; }    // strict >: first wins
+                        if (m > best[j]) { best[j] = m; bidx[j] = t0 + i; }    // strict >: first wins
                     } else {
-                        racc[t] += sC[i] * m;
+                        racc[j] += sC[i] * m;
                     }
                 }
             }
@@ -159,25 +163,25 @@ k_mlp_fwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
     }
     // ---- the two half-waves hold interleaved edge groups of the same columns: combine, store
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int n = 32 * t + (l & 31);
+    for (int j = 0; j < TPW; ++j) {
+        const int n = 32 * (w + NW * j) + (l & 31);
         if constexpr (RED == 3) {
-            const float ob = __shfl_xor(best[t], 32);
-            const int oi = __shfl_xor(bidx[t], 32);
-            if (ob > best[t] || (ob == best[t] && oi < bidx[t])) { best[t] = ob; bidx[t] = oi; }
+            const float ob = __shfl_xor(best[j], 32);
+            const int oi = __shfl_xor(bidx[j], 32);
+            if (ob > best[j] || (ob == best[j] && oi < bidx[j])) { best[j] = ob; bidx[j] = oi; }
             if (l < 32 && n < F) {
-                const bool any = bidx[t] != INT_MAX;
+                const bool any = bidx[j] != INT_MAX;
                 if (slot < 0) {
-                    out[(int64_t)row * ldo + n] = any ? best[t] : 0.f;
-                    arg[(int64_t)row * lda + n] = any ? bidx[t] : -1;
+                    out[(int64_t)row * ldo + n] = any ? best[j] : 0.f;
+                    arg[(int64_t)row * lda + n] = any ? bidx[j] : -1;
                 } else {
-                    pval[(int64_t)slot * F + n] = best[t];
-                    parg[(int64_t)slot * F + n] = bidx[t];
+                    pval[(int64_t)slot * F + n] = best[j];
+                    parg[(int64_t)slot * F + n] = bidx[j];
                 }
             }
         } else {
-            const float other = __shfl_xor(racc[t], 32);
-            float v = (l < 32) ? racc[t] + other : other + racc[t];
+            const float other = __shfl_xor(racc[j], 32);
+            float v = (l < 32) ? racc[j] + other : other + racc[j];
             if (l < 32 && n < F) {
                 if (slot < 0) {
                     if constexpr (RED == AGG_MEAN) {
@@ -430,21 +434,16 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
 
 template <int ACT1, int ACT2, int RED>
 hipError_t mlp_fwd_nt(int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeMlpArgs& a) {
-#define SIR_MLP_FWD(NTV)                                                                                     \
-    hipLaunchKernelGGL((k_mlp_fwd<ACT1, ACT2, RED, NTV>), grid, dim3(64), lds, st, a.rowptr, a.col,           \
-                       reinterpret_cast<const int4*>(a.items), a.Q, a.ldq, a.K, a.ldk, a.norm_row, a.norm_col, \
-                       a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.bias, a.out, a.ldo,  \
+#define SIR_MLP_FWD(NWV, TPWV)                                                                                 \
+    hipLaunchKernelGGL((k_mlp_fwd<ACT1, ACT2, RED, NWV, TPWV>), grid, dim3(64 * NWV), lds, st, a.rowptr, a.col, \
+                       reinterpret_cast<const int4*>(a.items), a.Q, a.ldq, a.K, a.ldk, a.norm_row, a.norm_col,   \
+                       a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.bias, a.out, a.ldo,    \
                        a.arg, a.lda, a.pval, a.parg)
-    switch (nt) {
-        case 1: SIR_MLP_FWD(1); break;
-        case 2: SIR_MLP_FWD(2); break;
-        case 3: SIR_MLP_FWD(3); break;
-        case 4: SIR_MLP_FWD(4); break;
-        case 5: SIR_MLP_FWD(5); break;
-        case 6: SIR_MLP_FWD(6); break;
-        case 7: SIR_MLP_FWD(7); break;
-        default: SIR_MLP_FWD(8); break;
-    }
+    // nt output tiles of 32 features over NW waves x TPW tiles (tiles past nt only compute zeros)
+    if (nt <= 1) SIR_MLP_FWD(1, 1);
+    else if (nt <= 2) SIR_MLP_FWD(2, 1);
+    else if (nt <= 4) SIR_MLP_FWD(4, 1);
+    else SIR_MLP_FWD(4, 2);
 #undef SIR_MLP_FWD
     return hipGetLastError();
 }

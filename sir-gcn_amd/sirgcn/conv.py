@@ -216,6 +216,71 @@ class SIRConvFunction(torch.autograd.Function):
         return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None
 
 
+class SIRConvFunction16(torch.autograd.Function):
+    """The whole layer under autocast (bf16 / fp16 ``dt``, the reference's AMP path,
+    ``heterophilous-datasets/train.py:75``), hand-scheduled like :class:`SIRConvFunction`:
+
+    forward : QK = X [W_Q; W_K]^T + [b_Q; 0] in dt (library GEMM, as autocast's nn.Linear)
+              -> S = edge kernels on dt rows (fp32 math inside) -> Y = S W_R^T + b_R in dt
+    backward: G = dY W_R and dX = dQK [W_Q; W_K] in dt (library GEMMs, as autocast's autograd);
+              the weight gradients dW = dY^T S, [dQ dK]^T X and the bias gradients — contractions
+              over all V node rows, the shape half-precision library GEMMs run slowest — on the
+              native split-fp16 TN kernel from the dt values widened to fp32 (more accurate than
+              autocast's half-precision mm), fp32 like the parameters."""
+
+    @staticmethod
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on, dt):
+        H = W_Q.shape[0]
+        Xh = X.to(dt)
+        W_cat = torch.cat([W_Q, W_K], 0).to(dt)
+        b_cat = torch.cat([b_Q, b_Q.new_zeros(H)]).to(dt) if b_Q is not None else None
+        QK = F.linear(Xh, W_cat, b_cat)
+        V = QK.shape[0]
+        in_norm, out_norm = plan.norms(agg)
+        S = torch.empty((V, H), device=X.device, dtype=dt)
+        partial = _partial(plan, H, X.device)
+        training = grad_on and any(ctx.needs_input_grad[:6])
+        nw = _native.mask_words(H, act) if (EdgeAggregate.use_mask and training) else 0
+        mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=X.device, dtype=torch.int64) if nw else None
+        _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, act, slope, S, partial, mask)
+        W_Rh = W_R.to(dt)
+        Y = F.linear(S, W_Rh, b_R.to(dt) if b_R is not None else None)
+        ctx.save_for_backward(Xh, W_cat, W_Rh, S, mask if mask is not None else QK)
+        ctx.masked = mask is not None
+        ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.x_dtype = plan, agg, act, slope, X.dtype
+        ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        Xh, W_cat, W_Rh, S, saved = ctx.saved_tensors
+        plan, agg, act, slope = ctx.plan, ctx.agg, ctx.act, ctx.slope
+        H = W_Rh.shape[1]
+        V = Xh.shape[0]
+        dY = dY.contiguous().to(W_Rh.dtype)
+        G = dY @ W_Rh
+        dW_R = db_R = None
+        if ctx.needs_input_grad[4] or ctx.needs_input_grad[5]:
+            dW_R, db_R = _weight_and_bias_grad(dY.float(), S.float(), ctx.needs_input_grad[4],
+                                               ctx.has_br and ctx.needs_input_grad[5])
+        if ctx.masked:
+            Q = K = None
+            mask = saved
+        else:
+            Q, K = saved[:, :H], saved[:, H:]
+            mask = None
+        dQK = torch.empty((V, 2 * H), device=Xh.device, dtype=W_Rh.dtype)
+        edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK)
+        dX = (dQK @ W_cat).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+        dW_Q = dW_K = db_Q = None
+        need_bq = ctx.has_bq and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3] or need_bq:
+            dW, cs = _weight_and_bias_grad(dQK.float(), Xh.float(), True, need_bq)
+            dW_Q, dW_K = dW[:H], dW[H:]
+            db_Q = cs[:H] if need_bq else None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None
+
+
 class SIRConv(nn.Module):
     r"""Soft-Isomorphic Relational Graph Convolution (SIR-GCN), MI355X-native.
 
@@ -303,6 +368,17 @@ class SIRConv(nn.Module):
                                          self.linear_key.weight, self.linear_relation.weight,
                                          self.linear_relation.bias, plan, self._agg_type, act, slope,
                                          torch.is_grad_enabled())
+        if (self.use_fused and feat_key is feat_query and torch.is_autocast_enabled() and H % 4 == 0
+                and not (self.training and self.dropout.p > 0) and feat_query.dtype in (torch.float32, torch.bfloat16,
+                                                                                      torch.float16)
+                and self.linear_query.weight.dtype == torch.float32):
+            dt = torch.get_autocast_dtype("cuda")
+            if dt in (torch.bfloat16, torch.float16):
+                with torch.autocast("cuda", enabled=False):
+                    return SIRConvFunction16.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
+                                                   self.linear_key.weight, self.linear_relation.weight,
+                                                   self.linear_relation.bias, plan, self._agg_type, act, slope,
+                                                   torch.is_grad_enabled(), dt)
         QK = self._project(feat_key, feat_query)
         S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope, torch.is_grad_enabled())
         return self.linear_relation(S)
