@@ -95,3 +95,17 @@ def test_empty_work_is_a_no_op():
 def test_package_surface():
     for name in ("SIRConv", "Graph", "get_plan", "EdgeAggregate"):
         assert hasattr(sirgcn, name)
+
+
+def test_abi_argument_checks_under_asan_ubsan(tmp_path):
+    """the C ABI's validation built with host AddressSanitizer + UBSan
+    (tools/build_abi_asan.sh, tools/abi_sanitize.cpp): every bad call rejected, no sanitizer report."""
+    import shutil
+    import subprocess
+    if shutil.which("/opt/rocm/bin/hipcc") is None:
+        import pytest
+        pytest.skip("hipcc not available")
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "build_abi_asan.sh"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ok: 0 failure(s)" in r.stdout
