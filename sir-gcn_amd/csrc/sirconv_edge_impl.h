@@ -472,7 +472,7 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
                                            const uint64_t* __restrict__ mask,
                                            const float* __restrict__ norm_col, float nr, float slope,
                                            int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4],
-                                           uint64_t pre = 0, int pre_lane = 0) {
+                                           uint64_t pre = 0, int pre_lane = 0, float cfw = 0.f, int cf_lane = 0) {
     constexpr int NW = NV * 4;
     int p[UU];
     int v[UU];
@@ -483,7 +483,7 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
             p[i] = __builtin_amdgcn_readfirstlane(perm[e + i]);
         } else {
             p[i] = e + i;
-            if constexpr (AGG == AGG_SYM) v[i] = __builtin_amdgcn_readfirstlane(col[e + i]);
+            if constexpr (AGG == AGG_SYM && !PRE) v[i] = __builtin_amdgcn_readfirstlane(col[e + i]);
         }
     }
     uint64_t wd[UU][NW];
@@ -519,7 +519,12 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
         for (int k = 0; k < NW; ++k) wd[i][k] = uniform64(mask[(int64_t)p[i] * NW + k]);
     }
     float cf[UU];
-    if constexpr (AGG == AGG_SYM) {
+    if constexpr (AGG == AGG_SYM && PRE) {
+        // norms already gathered one per lane (mask_item_dst_wide): edge e+i's in lane cf_lane + i
+#pragma unroll
+        for (int i = 0; i < UU; ++i)
+            cf[i] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cfw), cf_lane + i)) * nr;
+    } else if constexpr (AGG == AGG_SYM) {
 #pragma unroll
         for (int i = 0; i < UU; ++i) cf[i] = norm_col[v[i]] * nr;
     }
@@ -624,6 +629,88 @@ __device__ __forceinline__ void mask_item_dst(int e0, int e1, const int* __restr
                                                             slope, lane, HC, gv, acc, cur, i * NW);
 }
 
+#ifndef SIR_DQ_WIDE
+#define SIR_DQ_WIDE 1           // dQ pass: a whole wave of mask words per load (mask_item_dst_wide)
+#endif
+
+// dQ pass, wide form: the per-batch loads of mask_item_dst leave a wave one U-edge batch (U*NW*8 B)
+// in flight, so a row of ~20 edges costs ~4 serial memory latencies and the pass is latency-bound.
+// Here every load fetches a full chunk of CH = 64/NW edges (all 64 lanes: 512 B for H = 256), the
+// row's first two chunks are loaded together and the next chunk is in flight while one is summed (a
+// row of <= 2*CH edges costs one latency); a chunk is summed in SB-edge sub-batches
+// (compile-time readlane lanes, SB*NW word pairs of SGPRs).  Same per-column edge order as
+// mask_item_dst, so the sums are bit-identical.
+template <int ST, int ACT, int AGG, int NV>
+__device__ __forceinline__ void mask_item_dst_wide(int e0, int e1, const int* __restrict__ col,
+                                                   const uint64_t* __restrict__ mask,
+                                                   const float* __restrict__ norm_col, float nr, float slope, int lane,
+                                                   int HC, const float (&gv)[NV][4], float (&acc)[NV][4]) {
+    constexpr int NW = NV * 4, CH = 64 / NW, SB = (NV == 1) ? 4 : (NV == 2 ? 2 : 1);
+    static_assert(CH % SB == 0, "sub-batches tile a chunk");
+    constexpr bool kSym = (AGG == AGG_SYM);
+    if (e0 >= e1) return;
+    // Loads are unconditional (lanes past the row re-read edge e0's first word, whose value is never
+    // used): a lane-guarded load compiles to a branch that may skip it, and the compiler then waits
+    // for every outstanding load (vmcnt(0)) instead of the oldest chunk only.
+    auto load_chunk = [&](int eb) -> uint64_t {
+        const int n = e1 - eb;
+        const int lim = (n >= CH ? CH : n) * NW;
+        return mask[(lane < lim) ? (int64_t)eb * NW + lane : (int64_t)e0 * NW];
+    };
+    // SYM: lane i < CH also fetches the chunk's edge i source id, then its norm (one gather per chunk
+    // instead of two dependent scalar loads per edge); the norm of the next chunk is gathered while
+    // the current one is summed
+    auto load_col = [&](int eb) -> int {
+        const int n = e1 - eb;
+        return col[(lane < (n >= CH ? CH : n)) ? eb + lane : e0];
+    };
+    auto gather_norm = [&](int c) -> float { return norm_col[c]; };
+    auto full = [&](uint64_t c, int eb, float f) {
+#pragma unroll
+        for (int s = 0; s < CH / SB; ++s)
+            mask_batch<ST, MODE_BWD_DST, ACT, AGG, NV, SB, true>(eb + s * SB, nullptr, nullptr, nullptr, 0, mask,
+                                                                 nullptr, nr, slope, lane, HC, gv, acc, c, s * SB * NW,
+                                                                 f, s * SB);
+    };
+    auto tail = [&](uint64_t c, int eb, float f) {   // 0 .. CH-1 edges
+        const int r = e1 - eb;
+#pragma unroll
+        for (int i = 0; i < CH - 1; ++i)
+            if (i < r)
+                mask_batch<ST, MODE_BWD_DST, ACT, AGG, NV, 1, true>(eb + i, nullptr, nullptr, nullptr, 0, mask, nullptr,
+                                                                nr, slope, lane, HC, gv, acc, c, i * NW, f, i);
+    };
+    // chunk registers a / b alternate roles in a loop unrolled by two over the row's full chunks (a
+    // register copy of a value still being loaded would make the compiler wait for that load)
+    const int nfull = (e1 - e0) / CH;
+    uint64_t ca = load_chunk(e0);
+    int ka = 0, kb = 0;
+    if constexpr (kSym) ka = load_col(e0);
+    uint64_t cb = load_chunk(e0 + CH);
+    if constexpr (kSym) kb = load_col(e0 + CH);
+    float fa = 0.f, fb = 0.f;
+    if constexpr (kSym) fa = gather_norm(ka);
+    int e = e0;
+    for (int k = 2; k <= nfull; k += 2) {
+        full(ca, e, fa);
+        if constexpr (kSym) fb = gather_norm(kb);
+        ca = load_chunk(e + 2 * CH);
+        if constexpr (kSym) ka = load_col(e + 2 * CH);
+        full(cb, e + CH, fb);
+        if constexpr (kSym) fa = gather_norm(ka);
+        cb = load_chunk(e + 3 * CH);
+        if constexpr (kSym) kb = load_col(e + 3 * CH);
+        e += 2 * CH;
+    }
+    if (nfull & 1) {
+        full(ca, e, fa);
+        if constexpr (kSym) fb = gather_norm(kb);
+        tail(cb, e + CH, fb);
+    } else {
+        tail(ca, e, fa);
+    }
+}
+
 __device__ __forceinline__ int4 uniform_item(const int4* __restrict__ items, int64_t i) {
     int4 it = items[i];
     it.x = __builtin_amdgcn_readfirstlane(it.x);
@@ -677,7 +764,9 @@ mask_pass_item(int64_t wave, const int* __restrict__ rowptr, const int* __restri
     }
     float nr = 1.f;
     if constexpr (AGG == AGG_SYM) nr = norm_row[row];
-    if constexpr (SIR_DQ_PF && MODE == MODE_BWD_DST && AGG != AGG_SYM && U * NV * 4 <= 64)
+    if constexpr (SIR_DQ_WIDE && MODE == MODE_BWD_DST)
+        mask_item_dst_wide<ST, ACT, AGG, NV>(e0, e1, col, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    else if constexpr (SIR_DQ_PF && MODE == MODE_BWD_DST && AGG != AGG_SYM && U * NV * 4 <= 64)
         mask_item_dst<ST, ACT, AGG, NV, U>(e0, e1, col, mask, norm_col, nr, slope, lane, HC, gv, acc);
     else
         mask_item<ST, MODE, ACT, AGG, NV, U>(e0, e1, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);

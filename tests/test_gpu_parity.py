@@ -678,3 +678,34 @@ def test_one_launch_backward_bit_identical_to_two_passes(agg, dtype, chunk):
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     assert torch.isfinite(outs[0]).all()
+
+
+@pytest.mark.parametrize("H", [136, 256, 512, 776, 1024])
+@pytest.mark.parametrize("agg", ["sum", "mean", "sym"])
+@pytest.mark.parametrize("act", ["relu", "leaky"])
+def test_sign_mask_backward_bit_identical_all_widths(H, agg, act):
+    """Sign-mask backward (wide-chunk dQ pass, every word count per edge: H = 136 .. 1024, rows of
+    0 .. 300 edges, split hubs) == the recompute backward, bit for bit."""
+    from sirgcn.conv import edge_backward
+    gen = torch.Generator().manual_seed(H + len(agg) + len(act))
+    V, E = 1500, 24000
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V - 40, (E,), generator=gen)   # 40 isolated destinations
+    dst[:300] = 11                                        # a hub row (split at chunk 64)
+    plan = GraphPlan(src, dst, V, DEV, chunk=64)
+    code = _native.ACT_RELU if act == "relu" else _native.ACT_LEAKY
+    QK = torch.randn(V, 2 * H, generator=gen).to(DEV)
+    G = torch.randn(V, H, generator=gen).to(DEV)
+    in_norm, out_norm = plan.norms(agg)
+    S = torch.empty(V, H, device=DEV)
+    mask = torch.empty(E * _native.mask_words(H, code), device=DEV, dtype=torch.int64)
+    part = torch.empty(max(plan.dst.n_slots, plan.src.n_slots, 1) * H, device=DEV)
+    _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, code, 0.2, S, part, mask)
+    outs = []
+    for m in (mask, None):
+        dQK = torch.full((V, 2 * H), float("nan"), device=DEV)
+        edge_backward(plan, H, agg, code, 0.2, G, QK[:, :H], QK[:, H:], m, dQK)
+        outs.append(dQK)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert torch.isfinite(outs[0]).all()

@@ -56,7 +56,9 @@ def main():
     partial = torch.empty(max(n_slots, 1) * H, device=dev)
     outs = {}
     libs = [(kv.split("=", 1)[0], open_lib(kv.split("=", 1)[1])) for kv in a.libs]
-    times = {(n, p): [] for n, _ in libs for p in ("fwd", "dst", "src")}
+    PASSES = ("fwd", "dst", "src", "both")
+    times = {(n, p): [] for n, _ in libs for p in PASSES}
+    partial_s = torch.empty(max(n_slots, 1) * H, device=dev)
     st = torch.cuda.current_stream()
 
     def run(lib):
@@ -64,7 +66,7 @@ def main():
         S = torch.empty(V, H, device=dev, dtype=tdt)
         dQK = torch.empty(V, 2 * H, device=dev, dtype=tdt)
         sp = ctypes.c_void_p(st.cuda_stream)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         d, s_ = plan.dst, plan.src
         Q, K = QK[:, :H], QK[:, H:]
         ev[0].record()
@@ -82,7 +84,19 @@ def main():
                                        P(in_norm), _native.AGG[a.agg], _native.ACT_LEAKY, 0.2,
                                        P(dQK[:, H:]), 2 * H, P(partial), sp)
         ev[3].record()
+        # the one-launch backward (sum / sym): both passes again, into a second dQK
+        dQK2 = torch.empty(V, 2 * H, device=dev, dtype=tdt)
+        if a.agg in ("sum", "sym"):
+            rc |= lib.sir_edge_agg_bwd(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits,
+                                       P(s_.rowptr), P(s_.col), P(s_.perm), P(s_.items), s_.n_items, P(s_.splits),
+                                       s_.n_splits, H, dcode, P(mask), P(G), H, P(in_norm), P(out_norm),
+                                       _native.AGG[a.agg], _native.ACT_LEAKY, 0.2, P(dQK2), 2 * H, P(dQK2[:, H:]),
+                                       2 * H, P(partial), P(partial_s), sp)
+        ev[4].record()
         assert rc == 0, lib.sir_last_error()
+        if a.agg in ("sum", "sym"):
+            torch.cuda.synchronize()
+            assert torch.equal(dQK2, dQK), "one-launch backward differs from the two passes"
         return ev, S, dQK
 
     for r in range(a.rounds):
@@ -95,13 +109,15 @@ def main():
                 times[(name, "fwd")].append(ev[0].elapsed_time(ev[1]))
                 times[(name, "dst")].append(ev[1].elapsed_time(ev[2]))
                 times[(name, "src")].append(ev[2].elapsed_time(ev[3]))
+                times[(name, "both")].append(ev[3].elapsed_time(ev[4]))
     base = libs[0][0]
     for name, _ in libs:
         same = torch.equal(outs[name][0], outs[base][0]) and torch.equal(outs[name][1], outs[base][1])
-        med = {p: statistics.median(times[(name, p)]) for p in ("fwd", "dst", "src")}
-        mn = {p: min(times[(name, p)]) for p in ("fwd", "dst", "src")}
+        med = {p: statistics.median(times[(name, p)]) for p in PASSES}
+        mn = {p: min(times[(name, p)]) for p in PASSES}
         print(f"{name:10s} fwd {med['fwd']:.3f} ({mn['fwd']:.3f})  dst {med['dst']:.3f} ({mn['dst']:.3f})  "
-              f"src {med['src']:.3f} ({mn['src']:.3f}) ms   bitwise-equal-to-{base}: {same}")
+              f"src {med['src']:.3f} ({mn['src']:.3f})  one-launch {med['both']:.3f} ({mn['both']:.3f}) ms   "
+              f"bitwise-equal-to-{base}: {same}", flush=True)
 
 
 if __name__ == "__main__":
