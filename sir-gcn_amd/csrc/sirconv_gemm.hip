@@ -28,6 +28,8 @@
 //   k_gemm_reduce : C = sum_p part[p] in p order (deterministic).
 // LDS stage image (both kernels): [part hi/lo][k-step 0/1][rows in fimg order] — one k-step of
 // 32 rows is 1 KiB contiguous, exactly one ds_read_b128 per lane, in lane order (conflict-free).
+#include <type_traits>
+
 #include "sirconv_internal.h"
 
 namespace sir {
@@ -43,7 +45,8 @@ constexpr int KC = 32;          // contraction elements per LDS stage (two k16 M
 #define SIR_ABL_TN 0            // timing-only ablation: TN loads dropped (zero-record descriptors)
 #endif
 #ifndef SIR_ABL_NT
-#define SIR_ABL_NT 0            // timing-only ablations: 1 = NT data loads dropped, 2 = NT C stores dropped
+#define SIR_ABL_NT 0            // timing-only ablations: 1 = NT data loads dropped, 2 = NT C stores dropped,
+                                // persistent NT only: 4 = no split arithmetic, 8 = no MFMAs
 #endif
 #ifndef SIR_HR
 #define SIR_HR 8                // headroom bits of a reset running scale (see next_se)
@@ -468,6 +471,309 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #endif
 
 // ------------------------------------------------------------------------------------------
+// Persistent NT GEMM (N <= NT_P_NMAX, K = 32 * NCT).  k_gemm_nt's tiles are short at the layer's
+// shapes (K = 256: 8 chunks), and with one block per CU every tile paid the pipeline fill (one
+// memory latency) and an epilogue during which the CU's MFMAs idled: a fixed ~11 us per tile
+// against ~23 us of chunk work (fit over K = 256 / 512 on MI355X).  Here one 512-thread block per
+// CU walks a contiguous range of 256 x 256 output tiles (both feature tiles of a data tile back to
+// back, so A's second read is an L2 hit), the chunk pipeline runs on across tile boundaries (the
+// next tile's first chunks are loaded and split while the current tile's last ones are
+// multiplied), and the epilogue stores straight from the accumulators with buffer stores — rows
+// past M and columns past N fall outside the store's range and are dropped, so no store is
+// guarded by a branch and the compiler's wait counts stay exact.  Per-tile data and arithmetic
+// are those of k_gemm_nt<2, 4, 4, 2, true>: results are bit-identical.
+#ifndef SIR_NT_PERSIST
+#define SIR_NT_PERSIST 1
+#endif
+#ifndef SIR_NT_PRIO
+#define SIR_NT_PRIO 0           // 1: s_setprio 1 around each step's MFMA cluster; 2: waves 4-7 at priority 1
+#endif
+#ifndef SIR_NT_P_UNROLL
+#define SIR_NT_P_UNROLL 1       // the steps between the first and the last three fully unrolled
+#endif
+#ifndef SIR_NT_P_KSB
+#define SIR_NT_P_KSB 1
+#endif
+constexpr int NT_P_NMAX = 512;
+
+template <int NCT>
+__global__ void __launch_bounds__(512)
+k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
+            const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
+            int64_t ldc, int n_ftiles, int n_tiles, int tiles_per_block) {
+    constexpr int WF = 4, TDT = 4, TFT = 2;
+    constexpr int NT = 512, BD = 256, BF = 256, TPR = NT / BD, FPT = KC / TPR, WPT = BF * 8 / NT;
+    static_assert(TPR == 2 && WPT == 4 && NCT >= 4 && NCT % 2 == 0, "mapping");
+    constexpr int D_BYTES = BD * 128, W_BYTES = BF * 128;
+    constexpr int STAGE = D_BYTES + W_BYTES + BD * 4;
+    constexpr int FIN_OFF = 2 * STAGE;                // [2][BD]: 2^-se of the rows of the last two tiles
+    constexpr int EPI_OFF = FIN_OFF + 2 * BD * 4;     // inv_t[NT_P_NMAX], bias[NT_P_NMAX]
+    __shared__ __attribute__((aligned(16))) char lds[EPI_OFF + 2 * NT_P_NMAX * 4];
+
+    const int t = threadIdx.x;
+    const int tb = blockIdx.x * tiles_per_block;
+    const int te = (tb + tiles_per_block < n_tiles) ? tb + tiles_per_block : n_tiles;
+    if (tb >= te) return;
+    float* const inv_l = reinterpret_cast<float*>(lds + EPI_OFF);
+    float* const bias_l = inv_l + NT_P_NMAX;
+    float* const fin = reinterpret_cast<float*>(lds + FIN_OFF);
+    // x + (-0) == x for every x (-0 included): without a bias the epilogue adds -0, which leaves
+    // the result bit-identical to adding nothing (no branch around the stores)
+    for (int n = t; n < Npad; n += NT) {          // visible after the prologue's barrier
+        inv_l[n] = inv_t[n];
+        bias_l[n] = (bias != nullptr && n < N) ? bias[n] : -0.f;
+    }
+
+    // loader role
+    const int rho = t / TPR, kp = t % TPR;
+    const int aoff = (rho * (int)lda + kp * FPT) * 4;
+    const rsrc_t wrsrc = mk_rsrc(Wp, (uint32_t)((int64_t)NCT * Npad * 128));
+    // weight piece t + i*NT of a stage: plane i (BF * 2 == NT), row nl / half q from t; with
+    // fimg(f0 + nl, q) = f0 * 32 + fimg(nl, q) (f0 % 256 == 0) the plane and the tile's f0 go to
+    // the scalar offset and one VGPR holds the lane's part
+    static_assert(BF * 2 == NT, "one weight plane per loader pass");
+    const int woff = fimg((t >> 6) * 32 + (t & 31), (t >> 5) & 1);
+    struct TileP { rsrc_t a; int64_t d0; int f0; int rows; };
+    auto tile_p = [&](int tt) {   // a tile past the block's range loads zeros (0-record resource)
+        TileP p;
+        if (tt < te) {
+            p.d0 = (int64_t)(tt / n_ftiles) * BD;
+            p.f0 = (tt % n_ftiles) * BF;
+            p.rows = (M - p.d0 < BD) ? (int)(M - p.d0) : BD;
+            p.a = mk_rsrc(A + p.d0 * lda, (SIR_ABL_NT & 1) ? 0u : (uint32_t)(p.rows * lda * 4));
+        } else {
+            p.d0 = 0;
+            p.f0 = 0;
+            p.rows = 0;
+            p.a = mk_rsrc(A, 0u);
+        }
+        return p;
+    };
+    int se_run = SE_INIT;
+
+    // compute role
+    const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    const int d_w = (w / WF) * TDT * 32, f_w = (w % WF) * TFT * 32;
+
+    float4 dv[2][FPT / 4];
+    u4v wv[WPT];
+    auto load_a = [&](int set, const TileP& p, int c) {
+#pragma unroll
+        for (int i = 0; i < FPT / 4; ++i) {
+            const u4v u = __builtin_amdgcn_raw_buffer_load_b128(p.a, aoff + 16 * i, c * KC * 4, 0);
+            dv[set][i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                                     __uint_as_float(u.w));
+        }
+    };
+    auto load_w = [&](const TileP& p, int c) {
+#pragma unroll
+        for (int i = 0; i < WPT; ++i)
+            wv[i] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, woff, c * Npad * 128 + i * Npad * 32 + p.f0 * 32, 0);
+    };
+    // split chunk of register set `set` into stage `buf`; first: a tile's first chunk (fresh row
+    // scale, factor 1); last: a tile's last chunk (its final row scale goes to fin[slot])
+    auto store = [&](int set, int buf, bool first, bool last, int slot) {
+        char* st = lds + buf * STAGE;
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < FPT / 4; ++i) m = fmax4(m, dv[set][i]);
+        m = fmaxf(m, __shfl_xor(m, 1));
+        const int se_old = first ? SE_INIT : se_run, se = next_se(se_old, bexp(m));
+        se_run = se;
+        const float s = pow2(se);
+#pragma unroll
+        for (int j = 0; j < FPT; j += 8) {
+            const int kl = kp * FPT + j, ks = kl >> 4, pos = kl & 15;
+            h8 hv, lv;
+#if SIR_ABL_NT & 4
+            hv = __builtin_bit_cast(h8, dv[set][j / 4]);         // timing-only: no split arithmetic
+            lv = __builtin_bit_cast(h8, dv[set][j / 4 + 1]);
+#else
+            split8(dv[set][j / 4], dv[set][j / 4 + 1], s, hv, lv);
+#endif
+            *reinterpret_cast<h8*>(st + (0 * 2 + ks) * BD * 32 + fimg(rho, pos >> 3)) = hv;
+            *reinterpret_cast<h8*>(st + (1 * 2 + ks) * BD * 32 + fimg(rho, pos >> 3)) = lv;
+        }
+        reinterpret_cast<float*>(st + D_BYTES + W_BYTES)[rho] = first ? 1.f : pow2(se - se_old);
+        if (last) {
+            int rq = threadIdx.x;                     // recomputed here: see the epilogue
+            asm volatile("" : "+v"(rq));
+            fin[slot * BD + rq / TPR] = pow2(-se);
+        }
+#pragma unroll
+        for (int i = 0; i < WPT; ++i)
+            *reinterpret_cast<u4v*>(st + D_BYTES + (t + i * NT) * 16) = wv[i];
+    };
+
+    f16v acc[TFT][TDT];
+    auto rescale = [&](int buf) {
+        const float* fac = reinterpret_cast<const float*>(lds + buf * STAGE + D_BYTES + W_BYTES);
+        float f[TDT];
+        bool ch = false;
+#pragma unroll
+        for (int b = 0; b < TDT; ++b) { f[b] = fac[d_w + 32 * b + r]; ch |= f[b] != 1.f; }
+        if (__builtin_amdgcn_ballot_w64(ch) != 0) {
+#pragma unroll
+            for (int b = 0; b < TDT; ++b)
+#pragma unroll
+                for (int a = 0; a < TFT; ++a) acc[a][b] *= f[b];
+        }
+    };
+    auto mfma = [&](int buf, bool zinit) {       // zinit: a tile's first chunk starts from zero
+        const char* st = lds + buf * STAGE;
+        const f16v zero = {};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#if SIR_NT_P_KSB
+            if (ks == 1) __builtin_amdgcn_sched_barrier(0);   // ks 1's fragments not loaded under ks 0's MFMAs
+#endif
+            h8 wf[TFT][2], df[TDT][2];
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) {
+#pragma unroll
+                for (int a = 0; a < TFT; ++a)
+                    wf[a][pt] = *reinterpret_cast<const h8*>(st + D_BYTES + (pt * 2 + ks) * BF * 32 + fimg(f_w + 32 * a + r, h));
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    df[b][pt] = *reinterpret_cast<const h8*>(st + (pt * 2 + ks) * BD * 32 + fimg(d_w + 32 * b + r, h));
+            }
+#if SIR_ABL_NT & 8
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    asm volatile("" :: "v"(wf[a][0]), "v"(wf[a][1]), "v"(df[b][0]), "v"(df[b][1]));   // timing-only
+            continue;
+#endif
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][0], df[b][0],
+                                                                       (zinit && ks == 0) ? zero : acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][0], df[b][1], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][1], df[b][0], acc[a][b], 0, 0, 0);
+        }
+    };
+    // C[m][n] = acc * 2^-se(m) * inv_t[n] + bias[n], one buffer store per float4
+    // Store offsets: the lane's row (voffset, so the range check drops rows past M) plus the
+    // lane's column; the static column parts and f0 go to the scalar offset.  The lane indices are
+    // re-derived from an opaque copy of threadIdx.x inside the epilogue: hoisted out of the tile
+    // loop, its addresses and offsets would hold VGPRs through every step and force spills
+    // (whose reloads, vector-memory ops, drain the load queue).
+    auto epilogue = [&](const TileP& p, int slot) {
+        int tq = threadIdx.x;
+        asm volatile("" : "+v"(tq));
+        const int lq = tq & 63, rq = lq & 31, hq = lq >> 5, wq = tq >> 6;
+        const int d_wq = (wq / WF) * TDT * 32, f_wq = (wq % WF) * TFT * 32;
+        const uint32_t ldc4 = (uint32_t)ldc * 4u;
+        const uint32_t nrec = (uint32_t)p.rows * ldc4;
+        const rsrc_t crs = mk_rsrc(C + p.d0 * ldc, (SIR_ABL_NT & 2) ? 0u : nrec);
+        const float* sc = fin + slot * BD;
+        // < 2^30: row < 256, ldc <= SIR_GEMM_MAX_LD
+        const uint32_t rv = (uint32_t)(d_wq + rq) * ldc4 + (uint32_t)(f_wq + 4 * hq) * 4u;
+#pragma unroll
+        for (int b = 0; b < TDT; ++b) {
+            const float is = sc[d_wq + 32 * b + rq];
+            const uint32_t rb = rv + (uint32_t)(32 * b) * ldc4;
+#pragma unroll
+            for (int a = 0; a < TFT; ++a) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int nc0 = p.f0 + 32 * a + 8 * g;                 // wave-uniform column part
+                    const int n = nc0 + f_wq + 4 * hq;
+                    const float4 it = *reinterpret_cast<const float4*>(inv_l + n);
+                    float4 o;
+                    o.x = acc[a][b][4 * g + 0] * is * it.x;
+                    o.y = acc[a][b][4 * g + 1] * is * it.y;
+                    o.z = acc[a][b][4 * g + 2] * is * it.z;
+                    o.w = acc[a][b][4 * g + 3] * is * it.w;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_l + n);   // -0 without bias
+                    o.x += bb.x; o.y += bb.y; o.z += bb.z; o.w += bb.w;
+                    u4v ov;
+                    ov.x = __float_as_uint(o.x); ov.y = __float_as_uint(o.y);
+                    ov.z = __float_as_uint(o.z); ov.w = __float_as_uint(o.w);
+                    // columns past N: an offset at the end of the range (dropped)
+                    __builtin_amdgcn_raw_buffer_store_b128(ov, crs, (n < N) ? rb : nrec, nc0 * 4, 0);
+                    // A 16-byte store reads its data VGPRs over several cycles: hipcc (ROCm 7.2) put a
+                    // v_pk_mul_f32 overwriting them right after the store with no wait state, and
+                    // lanes 12-15 of each 16-lane group stored the new value (measured on MI355X).
+                    // Pin the order and pad the window.
+                    __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_nop 1" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+    };
+
+#if SIR_NT_PRIO == 2
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+    TileP cur = tile_p(tb), nxt = tile_p(tb + 1);
+    load_a(0, cur, 0);
+    load_w(cur, 0);
+    store(0, 0, true, false, 0);
+    load_a(1, cur, 1);
+    load_w(cur, 1);
+    load_a(0, cur, 2);
+    __syncthreads();
+    // step c: chunk c is multiplied out of stage c&1; chunk c+1 (registers, set (c+1)&1) is split
+    // into the other stage; W(c+2) and A(c+3) (into the freed set) are issued.  Chunks past the
+    // tile's last belong to the next tile.  Steps 0 and NCT-3 .. NCT-1 are written out (first
+    // chunk / tile crossing); the ones between run as a loop of step pairs (static set parity).
+    // SK: 0 store chunk c+1 of this tile, 1 the same as the tile's last chunk, 2 the next tile's
+    // chunk 0; WN / AN: W(c+2) / A(c+3) come from the next tile.
+    typedef std::integral_constant<int, 0> I0;
+    typedef std::integral_constant<int, 1> I1;
+    typedef std::integral_constant<int, 2> I2;
+    auto step = [&](int c, int j, const TileP& cu, const TileP& nx, auto P_, auto Z_, auto SK_, auto WN_, auto AN_) {
+        constexpr int P = decltype(P_)::value, SK = decltype(SK_)::value;
+        constexpr bool Z = decltype(Z_)::value != 0, WN = decltype(WN_)::value != 0, AN = decltype(AN_)::value != 0;
+        if constexpr (!Z) rescale(P);
+#if SIR_NT_PRIO == 1
+        __builtin_amdgcn_s_setprio(1);
+#endif
+        mfma(P, Z);
+#if SIR_NT_PRIO == 1
+        __builtin_amdgcn_s_setprio(0);
+#endif
+        if constexpr (SK == 2) store(0, 0, true, false, 0);
+        else store(P ^ 1, P ^ 1, false, SK == 1, j & 1);
+        if constexpr (WN) load_w(nx, c + 2 - NCT);
+        else load_w(cu, c + 2);
+        if constexpr (AN) load_a(P ^ 1, nx, c + 3 - NCT);
+        else load_a(P ^ 1, cu, c + 3);
+        __syncthreads();
+    };
+    for (int j = 0; tb + j < te; ++j) {
+        const TileP nn = tile_p(tb + j + 2);
+        step(0, j, cur, nxt, I0(), I1(), I0(), I0(), I0());
+#if SIR_NT_P_UNROLL
+#pragma unroll
+#endif
+        for (int c = 1; c + 1 <= NCT - 4; c += 2) {
+            step(c, j, cur, nxt, I1(), I0(), I0(), I0(), I0());
+            step(c + 1, j, cur, nxt, I0(), I0(), I0(), I0(), I0());
+        }
+        step(NCT - 3, j, cur, nxt, I1(), I0(), I0(), I0(), I1());
+        step(NCT - 2, j, cur, nxt, I0(), I0(), I1(), I1(), I1());
+        step(NCT - 1, j, cur, nxt, I1(), I0(), I2(), I1(), I1());
+        epilogue(cur, j & 1);
+        cur = nxt;
+        nxt = nn;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // TN GEMM (split over row ranges).  WM x WN waves, each TMT x TNT tiles of 32 x 32.
 // Loader: one slot per thread — threads [0, 2BM) own column t/2 of the A block, threads
 // [2BM, 2BM+2BN) column (t-2BM)/2 of the B block; t&1 selects the k-step (16 rows of the chunk).
@@ -702,6 +1008,23 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     const u4v* wp = static_cast<const u4v*>(packed);
     const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
     const bool kfull = K % KC == 0;
+    if (SIR_NT_PERSIST && N > 128 && np <= NT_P_NMAX && kfull && (kc == 4 || kc == 8 || kc == 16)) {
+        constexpr int BD = 256, BF = 256;
+        const int nft = (N + BF - 1) / BF;
+        const int64_t ntiles = (M + BD - 1) / BD * nft;
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        if (ntiles < (int64_t)1 << 30) {
+            const int tpb = (int)((ntiles + ncu - 1) / ncu);
+            const int nblk = (int)((ntiles + tpb - 1) / tpb);
+            auto kern = kc == 4 ? k_gemm_nt_p<4> : (kc == 8 ? k_gemm_nt_p<8> : k_gemm_nt_p<16>);
+            hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, ldc,
+                               nft, (int)ntiles, tpb);
+            return hipGetLastError();
+        }
+    }
     if (N > 128) {
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;

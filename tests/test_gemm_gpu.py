@@ -91,6 +91,23 @@ def test_gemm_nt_wide_dynamic_range_and_running_scale():
     _check(C, A.double(), W.double().t(), A @ W.t(), None, "nt dynamic range")
 
 
+@pytest.mark.parametrize("M,K,N", [(70001, 256, 260), (513, 128, 512), (1, 512, 300), (66000, 512, 256)])
+def test_gemm_nt_persistent_strided_out_and_ragged_tiles(M, K, N):
+    """The persistent NT kernel (K = 128 / 256 / 512, N <= 512) writes through buffer stores whose
+    range check drops rows past M and columns past N: C as a column slice of a wider tensor
+    (ldc > N) keeps its neighbours, and a partial last data tile / feature tile is exact."""
+    g = torch.Generator(device=DEV).manual_seed(M + K + N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g)
+    wide = torch.full((M, N + 44), 7.0, device=DEV)
+    C = _native.gemm_nt(A, _native.gemm_pack(W), b, out=wide[:, 8:8 + N])
+    assert torch.all(wide[:, :8] == 7.0) and torch.all(wide[:, 8 + N:] == 7.0)
+    _check(C, A.double(), W.double().t(), torch.addmm(b, A, W.t()), b, f"nt strided M={M} K={K} N={N}")
+    C0 = _native.gemm_nt(A, _native.gemm_pack(W))          # no bias: the epilogue adds -0 (an identity)
+    _check(C0, A.double(), W.double().t(), A @ W.t(), None, f"nt no bias M={M}")
+
+
 @pytest.mark.parametrize("R", [0, 1, 31, 33, 1000, 70001])
 @pytest.mark.parametrize("M,N", [(4, 4), (32, 36), (256, 256), (512, 256), (300, 100)])
 def test_gemm_tn_vs_fp64(R, M, N):
