@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 5
+#define SIR_ABI_VERSION 6
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -327,6 +327,15 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
 int64_t sir_gemm_tn_workspace(int64_t R, int64_t M, int64_t N);
 int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int64_t M, int64_t N,
                 float* C, int64_t ldc, float* colsum_a, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* The same contraction on 16-bit operands (the autocast path's weight gradients): A [R, M], B [R, N]
+ * bf16 (dtype SIR_DTYPE_BF16) or fp16 (SIR_DTYPE_F16), C [M, N] and colsum_a [M] fp32.  Each 16-bit
+ * product is exact in fp32, so one 16-bit MFMA per step with fp32 accumulation (no operand split,
+ * no fp32 copies of A and B).  M, N, lda, ldb even; A, B 4-B aligned.  Replaces autograd's
+ * mm(dY^T, S) / mm(dQK^T, X) of the half-precision nn.Linear (and their fp32 casts).
+ * workspace: sir_gemm_tn_workspace(R, M, N) bytes. */
+int sir_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t R, int64_t M, int64_t N, int dtype,
+                  float* C, int64_t ldc, float* colsum_a, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -535,4 +535,24 @@ int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_
     return finish(fn, err, nullptr);
 }
 
+int sir_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t R, int64_t M, int64_t N, int dtype,
+                  float* C, int64_t ldc, float* colsum_a, void* workspace, int64_t workspace_bytes, void* stream) {
+    const char* fn = "sir_gemm_tn16";
+    if (dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "dtype must be BF16 or F16");
+    if (R < 0 || M <= 0 || N <= 0 || M > 65536 || N > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if (lda < M || ldb < N || ldc < N) return fail(SIR_EINVAL, fn, "leading dimension too small");
+    if (M % 2 != 0 || N % 2 != 0 || lda % 2 != 0 || ldb % 2 != 0)
+        return fail(SIR_EINVAL, fn, "M, N, lda, ldb must be even");
+    if (lda > SIR_GEMM_MAX_LD || ldb > SIR_GEMM_MAX_LD)
+        return fail(SIR_EINVAL, fn, "lda/ldb too large (a 32-row chunk must span < 2^31 bytes)");
+    if (C == nullptr || workspace == nullptr || (R > 0 && (A == nullptr || B == nullptr)))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 3u) != 0)
+        return fail(SIR_EINVAL, fn, "A and B must be 4-B aligned");
+    if (workspace_bytes < sir::gemm_tn_workspace(R, M, N)) return fail(SIR_EINVAL, fn, "workspace too small");
+    hipError_t err = sir::run_gemm_tn16(A, lda, B, ldb, R, (int)M, (int)N, dtype, C, ldc, colsum_a, workspace,
+                                        static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
 }  // extern "C"

@@ -31,9 +31,11 @@
 #include <type_traits>
 
 #include "sirconv_internal.h"
+#include "sirconv_gemm_util.h"
 
 namespace sir {
 namespace {
+using namespace gemm;
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
@@ -88,28 +90,8 @@ __device__ inline void split8(float4 a, float4 b, float s, h8& hi, h8& lo) {
 }
 #undef SIR_SPLIT1
 
-// Fragment image of one LDS plane (and of the packed weights): the 16 halves of a row's k16
-// step are two 16-byte pieces h = 0, 1; piece (row, h) sits at byte
-//   (row / 32) * 1024 + h * 512 + (row % 32) * 16
-// so the 64 lanes of an MFMA operand read (lane = h * 32 + row % 32) fetch 1 KiB in lane order:
-// every 16-lane group of a ds_read_b128 covers 256 contiguous bytes (no bank conflict).
-__host__ __device__ constexpr int fimg(int row, int h) { return ((row >> 5) << 10) + (h << 9) + ((row & 31) << 4); }
-
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-// raw buffer resource over [p, p + bytes): out-of-range loads return 0 (gfx9 word3 0x00020000)
-__device__ inline rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
-}
-
 __device__ inline float fmax4(float m, float4 v) {
     return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
-}
-
-// Bijective XCD-aware remap: consecutive wgids land on the same XCD (blocks are dispatched
-// round-robin over the 8 XCDs).
-__device__ inline int xcd_remap(int bid, int nblk) {
-    const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -491,6 +473,9 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #ifndef SIR_NT_P_UNROLL
 #define SIR_NT_P_UNROLL 1       // the steps between the first and the last three fully unrolled
 #endif
+#ifndef SIR_NT_STAGGER
+#define SIR_NT_STAGGER 0        // 1: waves 4-7 split / load before their MFMAs (see step)
+#endif
 #ifndef SIR_NT_P_KSB
 #define SIR_NT_P_KSB 1
 #endif
@@ -735,10 +720,26 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
     typedef std::integral_constant<int, 0> I0;
     typedef std::integral_constant<int, 1> I1;
     typedef std::integral_constant<int, 2> I2;
-    auto step = [&](int c, int j, const TileP& cu, const TileP& nx, auto P_, auto Z_, auto SK_, auto WN_, auto AN_) {
+    // LATE (SIR_NT_STAGGER, waves 4-7 = the second wave of every SIMD): split the next chunk
+    // BEFORE the MFMAs of the step instead of after, so that on each SIMD one wave's MFMAs run
+    // beside its partner's split VALU / LDS writes rather than both waves doing the same phase
+    // together (MI355X_MICROARCH.md "Two waves per SIMD" item 9).  Within a step the order is
+    // free: the MFMAs read stage P, the split writes stage P^1, the barrier closes the step.
+    auto step = [&](int c, int j, const TileP& cu, const TileP& nx, auto P_, auto Z_, auto SK_, auto WN_, auto AN_,
+                    auto L_) {
         constexpr int P = decltype(P_)::value, SK = decltype(SK_)::value;
         constexpr bool Z = decltype(Z_)::value != 0, WN = decltype(WN_)::value != 0, AN = decltype(AN_)::value != 0;
+        constexpr bool LATE = decltype(L_)::value != 0;
         if constexpr (!Z) rescale(P);
+        auto split = [&]() {
+            if constexpr (SK == 2) store(0, 0, true, false, 0);
+            else store(P ^ 1, P ^ 1, false, SK == 1, j & 1);
+        };
+        if constexpr (LATE) split();
+#if SIR_NT_STAGGER == 3
+        const bool late_w = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
+        if (late_w) split();
+#endif
 #if SIR_NT_PRIO == 1
         __builtin_amdgcn_s_setprio(1);
 #endif
@@ -746,31 +747,47 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
 #if SIR_NT_PRIO == 1
         __builtin_amdgcn_s_setprio(0);
 #endif
-        if constexpr (SK == 2) store(0, 0, true, false, 0);
-        else store(P ^ 1, P ^ 1, false, SK == 1, j & 1);
+#if SIR_NT_STAGGER == 3
+        if (!late_w) split();
+#else
+        if constexpr (!LATE) split();
+#endif
         if constexpr (WN) load_w(nx, c + 2 - NCT);
         else load_w(cu, c + 2);
         if constexpr (AN) load_a(P ^ 1, nx, c + 3 - NCT);
         else load_a(P ^ 1, cu, c + 3);
         __syncthreads();
     };
-    for (int j = 0; tb + j < te; ++j) {
-        const TileP nn = tile_p(tb + j + 2);
-        step(0, j, cur, nxt, I0(), I1(), I0(), I0(), I0());
+    auto run = [&](auto L_) {
+        TileP cu = cur, nx = nxt;
+        for (int j = 0; tb + j < te; ++j) {
+            const TileP nn = tile_p(tb + j + 2);
+            step(0, j, cu, nx, I0(), I1(), I0(), I0(), I0(), L_);
 #if SIR_NT_P_UNROLL
 #pragma unroll
 #endif
-        for (int c = 1; c + 1 <= NCT - 4; c += 2) {
-            step(c, j, cur, nxt, I1(), I0(), I0(), I0(), I0());
-            step(c + 1, j, cur, nxt, I0(), I0(), I0(), I0(), I0());
+            for (int c = 1; c + 1 <= NCT - 4; c += 2) {
+                step(c, j, cu, nx, I1(), I0(), I0(), I0(), I0(), L_);
+                step(c + 1, j, cu, nx, I0(), I0(), I0(), I0(), I0(), L_);
+            }
+            step(NCT - 3, j, cu, nx, I1(), I0(), I0(), I0(), I1(), L_);
+            step(NCT - 2, j, cu, nx, I0(), I0(), I1(), I1(), I1(), L_);
+            step(NCT - 1, j, cu, nx, I1(), I0(), I2(), I1(), I1(), L_);
+            epilogue(cu, j & 1);
+            cu = nx;
+            nx = nn;
         }
-        step(NCT - 3, j, cur, nxt, I1(), I0(), I0(), I0(), I1());
-        step(NCT - 2, j, cur, nxt, I0(), I0(), I1(), I1(), I1());
-        step(NCT - 1, j, cur, nxt, I1(), I0(), I2(), I1(), I1());
-        epilogue(cur, j & 1);
-        cur = nxt;
-        nxt = nn;
-    }
+    };
+#if SIR_NT_STAGGER == 2
+    run(I1());
+#elif SIR_NT_STAGGER == 3
+    run(I0());
+#elif SIR_NT_STAGGER
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) run(I1());
+    else run(I0());
+#else
+    run(I0());
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1046,6 +1063,13 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
             hipLaunchKernelGGL((k_gemm_nt<4, 2, 2, 2, false>), dim3((unsigned)nblk), dim3(512), 0, st,
                                A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
     }
+    return hipGetLastError();
+}
+
+hipError_t run_gemm_reduce(const float* part, int P, int64_t count, int Nc, float* C, int64_t ldc, hipStream_t st) {
+    if (count > 0)
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, part, P, count, Nc, C,
+                           ldc);
     return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -43,6 +43,7 @@ SIGNATURES = {
     "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
     "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
+    "sir_gemm_tn16": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _I, _P, _I64, _P, _P, _I64, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
@@ -382,5 +383,28 @@ def gemm_tn(A, B, out=None, colsum=False):
     with _Timed("sir_gemm_tn", A.device, 2 * R * M * N):
         rc = lib.sir_gemm_tn(_ptr(A), A.stride(0), _ptr(B), B.stride(0), R, M, N, _ptr(out), out.stride(0),
                              _ptr(cs), _ptr(ws), ws.numel(), _stream(A.device))
+    _check(rc, lib)
+    return (out, cs) if colsum else out
+
+
+_DT16 = {torch.bfloat16: 1, torch.float16: 2}      # SIR_DTYPE_BF16 / SIR_DTYPE_F16
+
+
+def gemm_tn16(A, B, out=None, colsum=False):
+    """C = A^T B for bf16 / fp16 A [R, M], B [R, N] (same dtype), fp32 result, on the 16-bit MFMA
+    kernel (each 16-bit product exact in fp32; no operand split).  ``colsum=True`` also returns
+    A.sum(0) in fp32 from the same pass."""
+    lib = load()
+    R, M = A.shape
+    N = B.shape[1]
+    assert B.shape[0] == R and A.stride(1) == 1 and B.stride(1) == 1 and A.dtype == B.dtype and A.dtype in _DT16
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    cs = torch.empty((M,), dtype=torch.float32, device=A.device) if colsum else None
+    ws_bytes = lib.sir_gemm_tn_workspace(R, M, N)
+    ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=A.device)
+    with _Timed("sir_gemm_tn16", A.device, 2 * R * M * N):
+        rc = lib.sir_gemm_tn16(_ptr(A), A.stride(0), _ptr(B), B.stride(0), R, M, N, _DT16[A.dtype], _ptr(out),
+                               out.stride(0), _ptr(cs), _ptr(ws), ws.numel(), _stream(A.device))
     _check(rc, lib)
     return (out, cs) if colsum else out

@@ -156,6 +156,14 @@ def _weight_and_bias_grad(G, X, need_w, need_b):
     return None, (_bias_grad(G) if need_b else None)
 
 
+def _weight_and_bias_grad16(G, X, need_w, need_b):
+    """:func:`_weight_and_bias_grad` for the 16-bit tensors of the autocast layer: dW = G^T X and
+    db = sum_rows G in fp32 (``sir_gemm_tn16``: exact 16-bit products, fp32 sums; no fp32 copies)."""
+    if need_w:
+        return linalg.mm_tn16(G, X, colsum=True) if need_b else (linalg.mm_tn16(G, X), None)
+    return None, (_bias_grad(G.float()) if need_b else None)
+
+
 class SIRConvFunction(torch.autograd.Function):
     """The whole layer (``conv.py:49-67``) with a hand-scheduled backward:
 
@@ -261,8 +269,8 @@ class SIRConvFunction16(torch.autograd.Function):
         G = dY @ W_Rh
         dW_R = db_R = None
         if ctx.needs_input_grad[4] or ctx.needs_input_grad[5]:
-            dW_R, db_R = _weight_and_bias_grad(dY.float(), S.float(), ctx.needs_input_grad[4],
-                                               ctx.has_br and ctx.needs_input_grad[5])
+            dW_R, db_R = _weight_and_bias_grad16(dY, S, ctx.needs_input_grad[4],
+                                                 ctx.has_br and ctx.needs_input_grad[5])
         if ctx.masked:
             Q = K = None
             mask = saved
@@ -275,7 +283,7 @@ class SIRConvFunction16(torch.autograd.Function):
         dW_Q = dW_K = db_Q = None
         need_bq = ctx.has_bq and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[3] or need_bq:
-            dW, cs = _weight_and_bias_grad(dQK.float(), Xh.float(), True, need_bq)
+            dW, cs = _weight_and_bias_grad16(dQK, Xh, True, need_bq)
             dW_Q, dW_K = dW[:H], dW[H:]
             db_Q = cs[:H] if need_bq else None
         return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None

@@ -66,6 +66,27 @@ def mm_tn(A, B, colsum=False):
     return (out, A.sum(0)) if colsum else out
 
 
+def _tn16_ok(t):
+    return (t.is_cuda and t.dtype in (torch.bfloat16, torch.float16) and t.dim() == 2 and t.stride(1) == 1
+            and t.shape[0] >= MIN_ROWS_16 and 0 < t.shape[1] <= MAX_DIM and t.shape[1] % 2 == 0
+            and t.stride(0) % 2 == 0 and t.stride(0) <= MAX_LD and t.data_ptr() % 4 == 0)
+
+
+# The 16-bit TN kernel moves half the bytes and does a third of the MFMA work of the split one;
+# it still splits the rows over >= 2048-row ranges, so below this it cannot fill the chip.
+MIN_ROWS_16 = 16384
+
+
+def mm_tn16(A, B, colsum=False):
+    """A^T B (and A.sum(0) with ``colsum``) in fp32 for bf16 / fp16 A [R, M], B [R, N]: the weight
+    and bias gradients of a half-precision nn.Linear (autocast), with fp32 accumulation of the
+    exact 16-bit products.  Native ``sir_gemm_tn16`` when the operands allow, else torch on the
+    values widened to fp32 (the same products, summed in fp32)."""
+    if USE_NATIVE and A.dtype == B.dtype and _tn16_ok(A) and _tn16_ok(B):
+        return _native.gemm_tn16(A, B, colsum=colsum)
+    return mm_tn(A.float(), B.float(), colsum=colsum)
+
+
 def _tn_torch(A, B):
     """torch A^T B; long-K shapes run as k row blocks of one batched GEMM (hipBLASLt is 2x faster
     that way than as one GEMM) summed in a fixed order."""

@@ -154,6 +154,44 @@ def test_gemm_tn_dynamic_range_strided_and_deterministic():
     _check(C1, A.double().t(), B.double(), A.t() @ B, None, "tn dynamic range")
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("R,M,N", [(0, 8, 4), (1, 256, 256), (31, 32, 36), (1000, 512, 256), (70001, 256, 256),
+                                   (4099, 300, 100), (20000, 128, 128), (66000, 512, 256)])
+def test_gemm_tn16_vs_fp64(dt, R, M, N):
+    """sir_gemm_tn16 (the autocast weight gradients): 16-bit A, B; every product exact in fp32, so
+    the bar is the fp32 GEMM's on the widened values — vs fp64 of the same (exactly widened)
+    values, torch's fp32 A.float()^T B.float() as the yardstick; column sums likewise; the product
+    unchanged by asking for the column sums; run-to-run deterministic."""
+    g = torch.Generator(device=DEV).manual_seed(R + 5 * M + N)
+    A = torch.randn(R, M, device=DEV, generator=g).to(dt)
+    B = torch.randn(R, N, device=DEV, generator=g).to(dt)
+    C, cs = _native.gemm_tn16(A, B, colsum=True)
+    if R == 0:
+        assert torch.all(C == 0) and torch.all(cs == 0)
+        return
+    assert torch.equal(C, _native.gemm_tn16(A, B)), "product must not depend on colsum / must be deterministic"
+    _check(C, A.double().t(), B.double(), A.float().t() @ B.float(), None, f"tn16 {dt} R={R} M={M} N={N}")
+    ref64 = A.double().sum(0)
+    e_ours, e_torch = _rel(cs.double(), ref64), _rel(A.float().sum(0).double(), ref64)
+    assert e_ours <= max(2 * e_torch, 1e-6), (e_ours, e_torch)
+
+
+def test_gemm_tn16_strided_and_wide_range():
+    """lda > M (a column slice of a wider tensor, as dQK[:, :H]), values spread over many binades
+    (bf16 keeps fp32's exponent range; no scaling is involved), and errors are loud."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    R = 40000
+    A0 = torch.randn(R, 600, device=DEV, generator=g)
+    A0 *= torch.exp2(torch.randint(-60, 60, (1, 600), device=DEV, generator=g).float())
+    A = A0.to(torch.bfloat16)[:, 40:552]
+    B = torch.randn(R, 256, device=DEV, generator=g).to(torch.bfloat16)
+    C = _native.gemm_tn16(A, B)
+    _check(C, A.double().t(), B.double(), A.float().t() @ B.float(), None, "tn16 strided wide range")
+    with pytest.raises(RuntimeError, match="even"):
+        _native.gemm_tn16(torch.zeros(10, 3, device=DEV, dtype=torch.bfloat16),
+                          torch.zeros(10, 4, device=DEV, dtype=torch.bfloat16))
+
+
 def test_gemm_errors_are_loud():
     A = torch.randn(10, 6, device=DEV)
     pk = _native.gemm_pack(torch.randn(8, 6, device=DEV))
