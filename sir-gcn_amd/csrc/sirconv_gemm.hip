@@ -56,6 +56,9 @@ constexpr int KC = 32;          // contraction elements per LDS stage (two k16 M
 #ifndef SIR_TN_CFG
 #define SIR_TN_CFG 2            // TN tiling: 1 = 16 waves 64x64 (4 per SIMD), 2 = 8 waves 128x64 (2 per SIMD)
 #endif
+#ifndef SIR_TN_PF
+#define SIR_TN_PF 2             // TN chunks in flight in registers (1 or 2; 2: -3..-5 %, profiles/r02_ab_tn_pf2.txt)
+#endif
 #ifndef SIR_NT_PF
 #define SIR_NT_PF 2             // NT chunks in flight in registers ahead of the LDS stage (1 or 2)
 #endif
@@ -840,15 +843,26 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
     const int m_w = (w / WN) * TMT * 32, n_w = (w % WN) * TNT * 32;
 
-    float4 xv[XR / 4];
+    float4 xv_[SIR_TN_PF][XR / 4];
     // bias gradient of the same linear (column sums of A) rides on the A loads: one partial row
     // per split, written by the blocks of the first n-tile
     const bool do_cs = csum_part != nullptr && is_a;
     float cs = 0.f;
-    auto load = [&](int c) {
+    auto load = [&](int set, int c) {
+        float4 (&xv)[XR / 4] = xv_[set];
         const int64_t vc = v_begin + (int64_t)c * KC;
         const float* src = xbase + vc * ldx;                 // wave-uniform chunk base
         float x[XR];
+#if SIR_TN_PF == 2
+        // one branch-free form for every chunk (a load on only one side of a branch makes the
+        // compiler's wait counts pessimistic): rows past v_end, and whole chunks past the split,
+        // fail the range check and read as 0
+        const int64_t nrow = v_end - vc;
+        const rsrc_t rs = mk_rsrc(src, (SIR_ABL_TN || nrow <= 0) ? 0u : (uint32_t)((nrow < KC ? nrow : KC) * ldx * 4));
+#pragma unroll
+        for (int j = 0; j < XR; ++j)
+            x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, xoff * 4, j * ldx * 4, 0));
+#else
         if (vc + KC <= v_end) {
             const rsrc_t rs = mk_rsrc(src, SIR_ABL_TN ? 0u : (uint32_t)(KC * ldx * 4));
 #pragma unroll
@@ -862,13 +876,15 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
             for (int j = 0; j < XR; ++j)
                 x[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + j * ldx * 4, 0, 0));
         }
+#endif
         // no zeroing of columns past Mc / Nc (they re-read column 0): such a column only feeds
         // its own output row / column, which is never stored, under its own scale.  A select
         // here would make the compiler wait for the loads right after issuing them.
 #pragma unroll
         for (int j = 0; j < XR / 4; ++j) xv[j] = make_float4(x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]);
     };
-    auto store = [&](int buf, int chunk, bool first = false) {   // first chunk: factor 1 (acc is zero)
+    auto store = [&](int set, int buf, int chunk, bool first = false) {   // first chunk: factor 1 (acc is zero)
+        const float4 (&xv)[XR / 4] = xv_[set];
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
@@ -904,16 +920,8 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
 
-    if (t < 2) rescaled[t] = -1;
-    if (nc > 0) {
-        load(0);
-        store(0, 0, true);
-    }
-    __syncthreads();
-    for (int c = 0; c < nc; ++c) {
+    auto compute = [&](int c) {
         const int buf = c & 1;
-        const bool more = c + 1 < nc;
-        if (more) load(c + 1);
         const char* st = lds + buf * STAGE;
         if (rescaled[buf] == c) {
             const float* fac = reinterpret_cast<const float*>(st + A_BYTES + B_BYTES);
@@ -962,9 +970,45 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                 for (int b = 0; b < TNT; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[a][1], bf[b][0], acc[a][b], 0, 0, 0);
         }
-        if (more) store(buf ^ 1, c + 1);
+    };
+
+    if (t < 2) rescaled[t] = -1;
+#if SIR_TN_PF == 2
+    // two chunks in flight: step c multiplies chunk c (stage c&1) while chunks c+1 (set (c+1)&1)
+    // and c+2 (set c&1, issued at the top of the step) load; chunks past the split load as zeros
+    // (empty range), so every step issues the same loads and the wait counts stay exact.
+    if (nc > 0) {
+        load(0, 0);
+        load(1, 1);
+        store(0, 0, 0, true);
+    }
+    __syncthreads();
+    auto step = [&](int c, int set) {            // set = c & 1 (static)
+        load(set, c + 2);
+        compute(c);
+        if (c + 1 < nc) store(set ^ 1, (c + 1) & 1, c + 1);
+        __syncthreads();
+    };
+    int c = 0;
+    for (; c + 2 <= nc; c += 2) {
+        step(c, 0);
+        step(c + 1, 1);
+    }
+    if (c < nc) step(c, 0);
+#else
+    if (nc > 0) {
+        load(0, 0);
+        store(0, 0, 0, true);
+    }
+    __syncthreads();
+    for (int c = 0; c < nc; ++c) {
+        const bool more = c + 1 < nc;
+        if (more) load(0, c + 1);
+        compute(c);
+        if (more) store(0, (c & 1) ^ 1, c + 1);
         __syncthreads();
     }
+#endif
 
     // epilogue: part[p][m][n] = acc * 2^-se_a(m) * 2^-se_b(n)
     float* sc = reinterpret_cast<float*>(lds);
