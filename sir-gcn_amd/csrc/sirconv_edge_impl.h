@@ -21,6 +21,7 @@
 
 #pragma once
 #include "sirconv_internal.h"
+#include "sirconv_gemm_util.h"
 
 namespace sir {
 
@@ -88,6 +89,7 @@ template <> struct Stor<ST_BF16> { typedef __bf16 T; };
 template <> struct Stor<ST_F16> { typedef _Float16 T; };
 
 typedef unsigned int sir_u2 __attribute__((ext_vector_type(2)));
+typedef unsigned int sir_u4 __attribute__((ext_vector_type(4)));
 
 template <int ST>
 __device__ __forceinline__ float h2f(uint32_t bits16) {
@@ -116,6 +118,12 @@ __device__ __forceinline__ float round_st(float x) {
 #endif
 #ifndef SIR_NT_GATHER
 #define SIR_NT_GATHER 0
+#endif
+#ifndef SIR_FWD_BUFGATHER
+#define SIR_FWD_BUFGATHER 1     // fp32 forward (mask mode): K rows gathered by 16-B buffer loads (not narrowed)
+#endif
+#ifndef SIR_MASK_WRITELANE
+#define SIR_MASK_WRITELANE 1    // forward sign-mask words built by v_writelane (1) or per-lane selects (0)
 #endif
 typedef float sir_f4 __attribute__((ext_vector_type(4)));
 
@@ -215,6 +223,12 @@ __device__ __forceinline__ void vstore(float* __restrict__ p, const float (&s)[V
     }
 }
 
+// lane K of v takes the wave-uniform x (v_writelane_b32; this clang has no builtin for it)
+// (k must fold to a constant after unrolling: an inline-constant lane select, no hazard)
+__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x, int k) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(k));
+}
+
 // ------------------------------------------------------------------------------ edge batch
 // Processes UU consecutive edges [e, e+UU) of one row: all gathers issued before any use.
 template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int UU, bool MASKW>
@@ -228,6 +242,7 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
     int u[UU];
 #pragma unroll
     for (int i = 0; i < UU; ++i) u[i] = col[e + i];
+    constexpr bool kBufGather = SIR_FWD_BUFGATHER && MODE == MODE_FWD && ST == ST_F32 && VW == 4 && LPR == 64 && MASKW;
     float cv[UU][NV][VW];
     float gc[(MODE == MODE_BWD_SRC) ? UU : 1][NV][VW];
 #pragma unroll
@@ -237,10 +252,24 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
         // compiler may copy inside the branch, i.e. wait for right after issuing it — that
         // serialised the gathers of some instances (sym forward: +50%).
         const auto* cp = C + (int64_t)u[i] * ldc;
+        if constexpr (kBufGather) {
+            // one 16-B buffer load per lane off the (wave-uniform) row base; lanes past the row
+            // fail the range check and read 0.  A plain float4 load whose halves feed packed
+            // (v_pk_*) math only is narrowed by the DAG into two 8-B loads, the second issued
+            // after a wait for the first (fp32 forward +20 %, measured)
+            const gemm::rsrc_t rs = gemm::mk_rsrc(cp, (uint32_t)(HC * 16));
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            const int c = li + LPR * j;
-            vload_gather<ST, VW>(cv[i][j], cp + (c < HC ? c : 0) * VW);
+            for (int j = 0; j < NV; ++j) {
+                const sir_u4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (li + LPR * j) * 16, 0, 0);
+                cv[i][j][0] = __uint_as_float(t.x); cv[i][j][1] = __uint_as_float(t.y);
+                cv[i][j][2] = __uint_as_float(t.z); cv[i][j][3] = __uint_as_float(t.w);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                const int c = li + LPR * j;
+                vload_gather<ST, VW>(cv[i][j], cp + (c < HC ? c : 0) * VW);
+            }
         }
         if constexpr (MODE == MODE_BWD_SRC) {
             const auto* gp = G + (int64_t)u[i] * ldg;
@@ -265,6 +294,28 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
         static_assert(LPR == 64 && VW == 4, "mask layout needs full-wave rows of float4");
         constexpr int NW = NV * VW;
         static_assert(UU * NW <= 64, "one mask store per batch");
+#if SIR_MASK_WRITELANE
+        // The compare IS the ballot (v_cmp writes the 64-lane mask to SGPRs; the row's column-range
+        // mask is ANDed on the scalar unit) and v_writelane drops each word into its lane: 3 VALU
+        // per word.  The select form (lane == k ? b : mine) compiled to ~8 VALU per word (the compare
+        // materialised as 0/1 and re-compared, SGPR->VGPR moves, per-lane selects) — more VALU per
+        // edge than sigma and the sum together.
+        uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint64_t okm = __builtin_amdgcn_ballot_w64((li + LPR * j) < HC);
+#pragma unroll
+            for (int i = 0; i < UU; ++i) {
+#pragma unroll
+                for (int w = 0; w < VW; ++w) {
+                    const uint64_t b = __builtin_amdgcn_ballot_w64((rv[j][w] + cv[i][j][w]) > 0.f) & okm;
+                    writelane(mlo, (uint32_t)b, i * NW + j * VW + w);
+                    writelane(mhi, (uint32_t)(b >> 32), i * NW + j * VW + w);
+                }
+            }
+        }
+        const uint64_t mine = ((uint64_t)mhi << 32) | mlo;
+#else
         uint64_t mine = 0;
 #pragma unroll
         for (int i = 0; i < UU; ++i) {
@@ -278,6 +329,7 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                 }
             }
         }
+#endif
         if (lane < UU * NW) {
             if constexpr (SIR_NT_STREAM) __builtin_nontemporal_store(mine, mask + (int64_t)e * NW + lane);
             else mask[(int64_t)e * NW + lane] = mine;
@@ -462,6 +514,9 @@ __device__ __forceinline__ float sel_mask(uint64_t m, float t, float slope) {
     else return lane_select(m, t * slope, t);
 }
 
+#ifndef SIR_DK_VMASK
+#define SIR_DK_VMASK 0          // dK pass: mask words by one per-lane load + v_readlane (1) or scalar loads (0)
+#endif
 #ifndef SIR_DQ_VMASK
 #define SIR_DQ_VMASK 1          // dQ pass: mask words by one vector load + v_readlane (1; -9% sum, -19% sym) or scalar loads (0)
 #endif
@@ -497,6 +552,23 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
             for (int k = 0; k < NW; ++k) {
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(mlo, pre_lane + i * NW + k);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(mhi, pre_lane + i * NW + k);
+                wd[i][k] = ((uint64_t)hi << 32) | lo;
+            }
+    } else if constexpr (SIR_DK_VMASK && MODE == MODE_BWD_SRC && UU * NW <= 64) {
+        // dK pass: lane k fetches word k % NW of edge k / NW (its dst-CSR position perm[e + k / NW],
+        // one per-lane load), then the words go to SGPRs by v_readlane as in the dQ pass: the
+        // batch's mask words take no SGPRs while in flight (8 per edge by scalar loads), so more
+        // edges fit in one batch
+        const int ie = (lane / NW < UU) ? lane / NW : UU - 1;
+        const int pk = perm[e + ie];
+        const uint64_t mv = mask[(int64_t)pk * NW + lane % NW];
+        const int mlo = (int)(uint32_t)mv, mhi = (int)(uint32_t)(mv >> 32);
+#pragma unroll
+        for (int i = 0; i < UU; ++i)
+#pragma unroll
+            for (int k = 0; k < NW; ++k) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(mlo, i * NW + k);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(mhi, i * NW + k);
                 wd[i][k] = ((uint64_t)hi << 32) | lo;
             }
     } else if constexpr (SIR_DQ_VMASK && MODE == MODE_BWD_DST && UU * NW <= 64) {
