@@ -119,6 +119,9 @@ __device__ __forceinline__ float round_st(float x) {
 #ifndef SIR_NT_GATHER
 #define SIR_NT_GATHER 0
 #endif
+#ifndef SIR_FWD_PF
+#define SIR_FWD_PF 1            // row-CSR edge loop (full-wave rows, fp32): next batch's col[] prefetched per lane
+#endif
 #ifndef SIR_FWD_BUFGATHER
 #define SIR_FWD_BUFGATHER 1     // fp32 forward (mask mode): K rows gathered by 16-B buffer loads (not narrowed)
 #endif
@@ -238,10 +241,11 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                                            const float* __restrict__ norm_col, float nr, float slope,
                                            int li, int HC,
                                            const float (&rv)[NV][VW], const float (&gv)[NV][VW],
-                                           float (&acc)[NV][VW], uint64_t* __restrict__ mask, int lane) {
+                                           float (&acc)[NV][VW], uint64_t* __restrict__ mask, int lane,
+                                           const int* __restrict__ upre = nullptr) {
     int u[UU];
 #pragma unroll
-    for (int i = 0; i < UU; ++i) u[i] = col[e + i];
+    for (int i = 0; i < UU; ++i) u[i] = (upre != nullptr) ? upre[i] : col[e + i];
     constexpr bool kBufGather = SIR_FWD_BUFGATHER && MODE == MODE_FWD && ST == ST_F32 && VW == 4 && LPR == 64 && MASKW;
     float cv[UU][NV][VW];
     float gc[(MODE == MODE_BWD_SRC) ? UU : 1][NV][VW];
@@ -437,8 +441,31 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
     if constexpr (AGG == AGG_SYM) nr = norm_row[row];
 
     int e = e0;
-    for (; e + U <= e1; e += U)
-        edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+    if constexpr (SIR_FWD_PF && LPR == 64 && ST == ST_F32) {
+        // software-pipelined column indices (as in the dK pass): the next batch's col[] by one
+        // per-lane load issued with the current batch's gathers, moved to SGPRs by v_readlane
+        // (S2 forward f32 sum -2 %, mean -2 %, sym -1 %; 16-bit storage +10 %: fp32 only,
+        // profiles/r02_ab_index_prefetch.txt)
+        if (e + U <= e1) {
+            auto load_col = [&](int eb) {
+                const int q0 = eb + (lane < U ? lane : 0);
+                return col[q0 < e1 ? q0 : e1 - 1];
+            };
+            int vc = load_col(e);
+            for (; e + U <= e1; e += U) {
+                int uc[U];
+#pragma unroll
+                for (int i = 0; i < U; ++i) uc[i] = __builtin_amdgcn_readlane(vc, i);
+                vc = load_col(e + U);
+                edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC,
+                                                                     rv, gv, acc, mask, lane, uc);
+            }
+        }
+    } else {
+        for (; e + U <= e1; e += U)
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv,
+                                                                 acc, mask, lane);
+    }
     if constexpr (U > 8) {
         if (e + 8 <= e1) {
             edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 8, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
@@ -514,26 +541,33 @@ __device__ __forceinline__ float sel_mask(uint64_t m, float t, float slope) {
     else return lane_select(m, t * slope, t);
 }
 
-#ifndef SIR_DK_VMASK
-#define SIR_DK_VMASK 0          // dK pass: mask words by one per-lane load + v_readlane (1) or scalar loads (0)
+#ifndef SIR_DK_PF
+#define SIR_DK_PF 1             // dK pass: the next batch's col / perm indices loaded with the current batch's rows
 #endif
+
+// wave-uniform (scalar) edge indices of one batch: source / destination id and dst-CSR position
+template <int UU> struct EdgeIdx { int v[UU]; int p[UU]; };
 #ifndef SIR_DQ_VMASK
 #define SIR_DQ_VMASK 1          // dQ pass: mask words by one vector load + v_readlane (1; -9% sum, -19% sym) or scalar loads (0)
 #endif
 
-template <int ST, int MODE, int ACT, int AGG, int NV, int UU, bool PRE = false>
+template <int ST, int MODE, int ACT, int AGG, int NV, int UU, bool PRE = false, bool PIDX = false>
 __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, const int* __restrict__ perm,
                                            const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
                                            const uint64_t* __restrict__ mask,
                                            const float* __restrict__ norm_col, float nr, float slope,
                                            int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4],
-                                           uint64_t pre = 0, int pre_lane = 0, float cfw = 0.f, int cf_lane = 0) {
+                                           uint64_t pre = 0, int pre_lane = 0, float cfw = 0.f, int cf_lane = 0,
+                                           const EdgeIdx<UU>* idx = nullptr) {
     constexpr int NW = NV * 4;
     int p[UU];
     int v[UU];
 #pragma unroll
     for (int i = 0; i < UU; ++i) {
-        if constexpr (MODE == MODE_BWD_SRC) {
+        if constexpr (MODE == MODE_BWD_SRC && PIDX) {
+            v[i] = idx->v[i];
+            p[i] = idx->p[i];
+        } else if constexpr (MODE == MODE_BWD_SRC) {
             v[i] = __builtin_amdgcn_readfirstlane(col[e + i]);
             p[i] = __builtin_amdgcn_readfirstlane(perm[e + i]);
         } else {
@@ -552,23 +586,6 @@ __device__ __forceinline__ void mask_batch(int e, const int* __restrict__ col, c
             for (int k = 0; k < NW; ++k) {
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(mlo, pre_lane + i * NW + k);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(mhi, pre_lane + i * NW + k);
-                wd[i][k] = ((uint64_t)hi << 32) | lo;
-            }
-    } else if constexpr (SIR_DK_VMASK && MODE == MODE_BWD_SRC && UU * NW <= 64) {
-        // dK pass: lane k fetches word k % NW of edge k / NW (its dst-CSR position perm[e + k / NW],
-        // one per-lane load), then the words go to SGPRs by v_readlane as in the dQ pass: the
-        // batch's mask words take no SGPRs while in flight (8 per edge by scalar loads), so more
-        // edges fit in one batch
-        const int ie = (lane / NW < UU) ? lane / NW : UU - 1;
-        const int pk = perm[e + ie];
-        const uint64_t mv = mask[(int64_t)pk * NW + lane % NW];
-        const int mlo = (int)(uint32_t)mv, mhi = (int)(uint32_t)(mv >> 32);
-#pragma unroll
-        for (int i = 0; i < UU; ++i)
-#pragma unroll
-            for (int k = 0; k < NW; ++k) {
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(mlo, i * NW + k);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(mhi, i * NW + k);
                 wd[i][k] = ((uint64_t)hi << 32) | lo;
             }
     } else if constexpr (SIR_DQ_VMASK && MODE == MODE_BWD_DST && UU * NW <= 64) {
@@ -639,8 +656,37 @@ __device__ __forceinline__ void mask_item(int e0, int e1, const int* __restrict_
                                           const float* __restrict__ norm_col, float nr, float slope,
                                           int lane, int HC, const float (&gv)[NV][4], float (&acc)[NV][4]) {
     int e = e0;
-    for (; e + U <= e1; e += U)
-        mask_batch<ST, MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    if constexpr (SIR_DK_PF && MODE == MODE_BWD_SRC) {
+        // software-pipelined indices: the next batch's col / perm are fetched by one per-lane
+        // vector load (lane i < U: edge eb + i, clamped to the item) issued with the current
+        // batch's mask words and rows, and moved to SGPRs by v_readlane when the batch starts; a
+        // batch then costs one memory latency instead of two (index load, then the gathers), and
+        // the prefetched indices hold 2 VGPRs instead of 2U SGPRs
+        if (e + U <= e1) {
+            auto load_idx = [&](int eb, int& vc, int& pc) {
+                const int q0 = eb + (lane < U ? lane : 0);
+                const int q = q0 < e1 ? q0 : e1 - 1;
+                vc = col[q];
+                pc = perm[q];
+            };
+            int vc, pc;
+            load_idx(e, vc, pc);
+            for (; e + U <= e1; e += U) {
+                EdgeIdx<U> cur;
+#pragma unroll
+                for (int i = 0; i < U; ++i) {
+                    cur.v[i] = __builtin_amdgcn_readlane(vc, i);
+                    cur.p[i] = __builtin_amdgcn_readlane(pc, i);
+                }
+                load_idx(e + U, vc, pc);
+                mask_batch<ST, MODE, ACT, AGG, NV, U, false, true>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane,
+                                                                   HC, gv, acc, 0, 0, 0.f, 0, &cur);
+            }
+        }
+    } else {
+        for (; e + U <= e1; e += U)
+            mask_batch<ST, MODE, ACT, AGG, NV, U>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
+    }
     if constexpr (U > 8) {
         if (e + 8 <= e1) {
             mask_batch<ST, MODE, ACT, AGG, NV, 8>(e, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
