@@ -345,6 +345,10 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
         rows_local, edges_local, rows_src = r1 - r0, dg.num_local_edges, dg.n_ext
     del X_full, dY_full
 
+    # the incoming gradient in the dtype of Y (a 16-bit tensor under autocast: the gradient a
+    # downstream autocast layer hands back), cast once outside the timed region
+    dY_in = dY if dt == torch.float32 else dY.to(dt)
+
     def step():
         conv.zero_grad(set_to_none=True)
         X.grad = None
@@ -353,7 +357,7 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
                 Y = layer()
         else:
             Y = layer()
-        Y.backward(dY.to(Y.dtype))
+        Y.backward(dY_in if dY_in.dtype == Y.dtype else dY_in.to(Y.dtype))
         if dconv is not None:
             dconv.allreduce_grads()
 
@@ -490,6 +494,7 @@ def run_stack(args, world, rank, dev, torch, dist):
         model = torch.nn.parallel.DistributedDataParallel(stack, device_ids=[dev.index])
     X, dY = make_inputs(name, g.num_nodes(), dev, seed=3 + rank)
     X.requires_grad_(True)
+    dY_in = dY if dt == torch.float32 else dY.to(dt)      # cast outside the timed region (as in run_edge_cut)
 
     def step():
         model.zero_grad(set_to_none=True)
@@ -499,7 +504,7 @@ def run_stack(args, world, rank, dev, torch, dist):
                 Y = model(g, X)
         else:
             Y = model(g, X)
-        Y.backward(dY.to(Y.dtype))
+        Y.backward(dY_in if dY_in.dtype == Y.dtype else dY_in.to(Y.dtype))
 
     # Batched small graphs are launch-bound (SURVEY §7 "tiny batched graphs"): at N = 1 the whole
     # fwd+bwd step (every kernel, every ctypes launch, the allocator's work) is captured once into

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 6
+#define SIR_ABI_VERSION 7
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -336,6 +336,23 @@ int sir_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_
  * workspace: sir_gemm_tn_workspace(R, M, N) bytes. */
 int sir_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t R, int64_t M, int64_t N, int dtype,
                   float* C, int64_t ldc, float* colsum_a, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* The forward projections and input gradients of the autocast path on 16-bit MFMA: the
+ * half-precision nn.Linear (x W^T + b in bf16 / fp16, conv.py:60-61,65 under torch.autocast) and
+ * its input gradient (dY W).  Weight operand packed by sir_gemm_pack16 (rounded to dtype, RNE;
+ * re-pack whenever W changes; sir_gemm_pack16_bytes(N, K) bytes, 16-B aligned):
+ *   C[M, N] = A[M, K] B^T + bias,  B[n][k] = W[n*ldw + k] (trans = 0) or W[k*ldw + n] (trans = 1).
+ * dtype (SIR_DTYPE_BF16 / F16) is the MFMA type; a_dtype = dtype (A already 16-bit) or
+ * SIR_DTYPE_F32 (A rounded to dtype on load: the autocast cast fused into the GEMM; with
+ * Acopy != NULL the rounded A is also written to Acopy [M, K] (ldac)); c_dtype = dtype (RNE of the
+ * fp32 accumulator) or SIR_DTYPE_F32.  bias [N] fp32 (the caller passes the dtype-rounded bias of
+ * autocast) or NULL.  K in {128, 256, 512}; N <= 512, N and lda multiples of 8 (16-bit A) / 4;
+ * ldc >= N; A, C, Acopy, packed 16-B aligned.  One 16-bit MFMA per step, fp32 accumulation. */
+int64_t sir_gemm_pack16_bytes(int64_t N, int64_t K);
+int sir_gemm_pack16(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, int dtype, void* packed, void* stream);
+int sir_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int64_t K, const void* packed, int64_t N,
+                  int dtype, const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac,
+                  void* stream);
 
 #ifdef __cplusplus
 }

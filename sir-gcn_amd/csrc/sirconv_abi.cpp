@@ -555,4 +555,45 @@ int sir_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_
     return finish(fn, err, nullptr);
 }
 
+int64_t sir_gemm_pack16_bytes(int64_t N, int64_t K) {
+    if (N <= 0 || K <= 0 || N > 65536 || K > 65536 || K % 16 != 0) return 0;
+    return sir::gemm_pack16_bytes(N, K);
+}
+
+int sir_gemm_pack16(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, int dtype, void* packed, void* stream) {
+    const char* fn = "sir_gemm_pack16";
+    if (dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "dtype must be BF16 or F16");
+    if (N <= 0 || K <= 0 || N > 65536 || K > 65536 || K % 16 != 0)
+        return fail(SIR_EINVAL, fn, "N in [1, 65536], K in [16, 65536] and a multiple of 16");
+    if (W == nullptr || packed == nullptr) return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (ldw < (trans ? N : K)) return fail(SIR_EINVAL, fn, "ldw too small");
+    if ((reinterpret_cast<uintptr_t>(packed) & 15u) != 0) return fail(SIR_EINVAL, fn, "packed must be 16-B aligned");
+    hipError_t err = sir::run_gemm_pack16(W, ldw, (int)N, (int)K, trans ? 1 : 0, dtype, packed, static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
+int sir_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int64_t K, const void* packed, int64_t N,
+                  int dtype, const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac,
+                  void* stream) {
+    const char* fn = "sir_gemm_nt16";
+    if (dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "dtype must be BF16 or F16");
+    if (a_dtype != dtype && a_dtype != SIR_DTYPE_F32) return fail(SIR_EINVAL, fn, "a_dtype must be dtype or F32");
+    if (c_dtype != dtype && c_dtype != SIR_DTYPE_F32) return fail(SIR_EINVAL, fn, "c_dtype must be dtype or F32");
+    if (M < 0 || N <= 0 || N > 512 || (K != 128 && K != 256 && K != 512)) return fail(SIR_EINVAL, fn, "bad shape");
+    if ((M + 255) / 256 * ((N + 255) / 256) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
+    const int64_t av = a_dtype == SIR_DTYPE_F32 ? 4 : 8;     // elements per 16 B of A
+    if (N % 4 != 0 || lda % av != 0 || lda < K || ldc < N || ldc % 4 != 0)
+        return fail(SIR_EINVAL, fn, "N, ldc multiples of 4, lda a multiple of 16 B, lda >= K, ldc >= N");
+    if (lda > SIR_GEMM_MAX_LD || ldc > SIR_GEMM_MAX_LD) return fail(SIR_EINVAL, fn, "lda/ldc too large");
+    if (Acopy != nullptr && (a_dtype != SIR_DTYPE_F32 || ldac < K || ldac % 8 != 0 || ldac > SIR_GEMM_MAX_LD))
+        return fail(SIR_EINVAL, fn, "Acopy needs an fp32 A and ldac >= K, a multiple of 8");
+    if (M > 0 && (A == nullptr || C == nullptr || packed == nullptr)) return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(Acopy) |
+          reinterpret_cast<uintptr_t>(packed)) & 15u) != 0)
+        return fail(SIR_EINVAL, fn, "A, C, Acopy and packed must be 16-B aligned");
+    hipError_t err = sir::run_gemm_nt16(A, lda, a_dtype, M, (int)K, packed, (int)N, dtype, bias, C, ldc, c_dtype, Acopy,
+                                        ldac, static_cast<hipStream_t>(stream));
+    return finish(fn, err, nullptr);
+}
+
 }  // extern "C"

@@ -22,6 +22,8 @@
 #include "sirconv_internal.h"
 #include "sirconv_gemm_util.h"
 
+#include <type_traits>
+
 namespace sir {
 namespace {
 using namespace gemm;
@@ -211,6 +213,245 @@ k_gemm_tn16(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// NT GEMM on 16-bit MFMA: the autocast layer's forward projections and input gradients
+// (QK = X [W_Q; W_K]^T + b, Y = S W_R^T + b, G = dY W_R, dX = dQK [W_Q; W_K]):
+//   C[M, N] = A[M, K] B[N, K]^T (+ bias),  B packed 16-bit in fragment order (k_pack16),
+// A in the 16-bit type, or fp32 rounded (RNE) to it on load — the autocast cast X.to(dt) fused
+// into the GEMM; the rounded copy can be written out (Acopy, the first feature tile only) for the
+// weight-gradient GEMM.  C in the 16-bit type (RNE of the fp32 accumulator, what the library
+// GEMM returns) or fp32 (dX: the fp32 gradient of an fp32 input, without the 16-bit rounding and
+// the separate .to(float32) pass).  One 16-bit MFMA per 32x32x16 step, fp32 accumulation.
+//
+// Persistent: one 512-thread block per CU walks a contiguous range of 256 x 256 output tiles;
+// 8 waves, 128 x 64 outputs each (4 x 2 MFMA tiles, MFMA rows = features, columns = data rows).
+// Chunks of KC k-values: a thread loads half of one row's chunk (KC/2 values) and the same
+// number of packed weight bytes into a register set, two sets alternate (two chunks in flight
+// while one is multiplied out of LDS), and the pipeline runs on across tile boundaries.
+#ifndef SIR_NT16_ABL
+#define SIR_NT16_ABL 0          // timing-only ablations: 1 = A loads dropped, 2 = C stores dropped, 4 = no MFMAs
+#endif
+
+template <int I, int N_, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N_) {
+        f(std::integral_constant<int, I>());
+        static_for<I + 1, N_>(f);
+    }
+}
+
+__device__ inline uint32_t pack2(float a, float b, bool bf) {
+    if (bf) return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a) |
+                   ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
+    return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)a) |
+           ((uint32_t)__builtin_bit_cast(unsigned short, (_Float16)b) << 16);
+}
+
+template <bool BF, bool A32, bool C32, int KC, int NC, int NS>
+__global__ void __launch_bounds__(512)
+k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
+            const float* __restrict__ bias, int N, void* __restrict__ C, int64_t ldc, unsigned short* __restrict__ Acopy,
+            int64_t ldac, int n_ftiles, int n_tiles, int tiles_per_block) {
+    constexpr int BD = 256, BFT = 256, WF = 4, TDT = 4, TFT = 2;
+    constexpr int KS = KC / 16;                       // k16 planes per chunk
+    constexpr int PLANE = 256 * 32;                   // one k16 plane of 256 rows
+    constexpr int STAGE = 2 * KS * PLANE;             // A planes, then W planes
+    constexpr int EA = A32 ? 4 : 2;                   // bytes per A element
+    constexpr int AV = (KC / 2) * EA / 16;            // u4v A loads per thread and chunk
+    constexpr int WV = KS * PLANE * 1 / (16 * 512);   // u4v W pieces per thread and chunk
+    constexpr int EC = C32 ? 4 : 2;
+    static_assert(KC == 32 || KC == 64, "chunk");
+    static_assert(WV >= 1, "weight loader");
+    static_assert(NS >= 2 && NS <= NC && NC % NS == 0, "register sets: a tile's chunks map to sets the same way");
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 512 * 4];
+    float* const bias_l = reinterpret_cast<float*>(lds + 2 * STAGE);
+
+    const int t = threadIdx.x;
+    const int tb = blockIdx.x * tiles_per_block;
+    const int te = (tb + tiles_per_block < n_tiles) ? tb + tiles_per_block : n_tiles;
+    if (tb >= te) return;
+    // x + (-0) == x for every x: without a bias the epilogue adds -0 (no branch)
+    for (int n = t; n < Npad; n += 512) bias_l[n] = (bias != nullptr && n < N) ? bias[n] : -0.f;
+
+    // loader role: row rho of the tile, k half kh of the chunk (planes kh*KS/2 ..)
+    const int rho = t >> 1, kh = t & 1;
+    const int aoff = (int)(rho * lda + kh * (KC / 2)) * EA;
+    const int coff = (int)(rho * ldac + kh * (KC / 2)) * 2;
+    const rsrc_t wrs = mk_rsrc(Wp, (uint32_t)((int64_t)NC * KS * Npad * 32));
+    struct TileP { rsrc_t a; rsrc_t cp; int64_t d0; int f0; int rows; };
+    auto tile_p = [&](int tt) {      // a tile past the block's range loads zeros (0-record resource)
+        TileP p;
+        if (tt < te) {
+            p.d0 = (int64_t)(tt / n_ftiles) * BD;
+            p.f0 = (tt % n_ftiles) * BFT;
+            p.rows = (M - p.d0 < BD) ? (int)(M - p.d0) : BD;
+            p.a = mk_rsrc(static_cast<const char*>(A) + p.d0 * lda * EA, (SIR_NT16_ABL & 1) ? 0u : (uint32_t)(p.rows * lda * EA));
+            p.cp = mk_rsrc(Acopy + p.d0 * ldac, (Acopy != nullptr && p.f0 == 0) ? (uint32_t)(p.rows * ldac * 2) : 0u);
+        } else {
+            p.d0 = 0;
+            p.f0 = 0;
+            p.rows = 0;
+            p.a = mk_rsrc(A, 0u);
+            p.cp = mk_rsrc(A, 0u);
+        }
+        return p;
+    };
+
+    const int w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    const int d_w = (w / WF) * TDT * 32, f_w = (w % WF) * TFT * 32;
+
+    u4v av[NS][AV], wv[NS][WV];
+    auto load = [&](int set, const TileP& p, int c) {
+#pragma unroll
+        for (int i = 0; i < AV; ++i) av[set][i] = __builtin_amdgcn_raw_buffer_load_b128(p.a, aoff + 16 * i, c * KC * EA, 0);
+#pragma unroll
+        for (int i = 0; i < WV; ++i)
+            wv[set][i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, ((i * 512 + t) >> 9) * Npad * 32 + ((i * 512 + t) & 511) * 16,
+                                                              (c * KS * Npad + p.f0) * 32, 0);
+    };
+    auto store = [&](int set, int buf, const TileP& p, int c) {
+        char* st = lds + buf * STAGE;
+        u4v q[KC / 16];                                // this thread's KC/2 values as 16-bit, in k order
+        if constexpr (A32) {
+#pragma unroll
+            for (int i = 0; i < KC / 16; ++i) {
+                const u4v x0 = av[set][2 * i], x1 = av[set][2 * i + 1];
+                q[i].x = pack2(__uint_as_float(x0.x), __uint_as_float(x0.y), BF);
+                q[i].y = pack2(__uint_as_float(x0.z), __uint_as_float(x0.w), BF);
+                q[i].z = pack2(__uint_as_float(x1.x), __uint_as_float(x1.y), BF);
+                q[i].w = pack2(__uint_as_float(x1.z), __uint_as_float(x1.w), BF);
+            }
+#pragma unroll
+            for (int i = 0; i < KC / 16; ++i)       // the rounded copy (first feature tile only)
+                __builtin_amdgcn_raw_buffer_store_b128(q[i], p.cp, coff + 16 * i, c * KC * 2, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < KC / 16; ++i) q[i] = av[set][i];
+        }
+        // piece i covers k = kh*KC/2 + 8i .. +7: plane kh*KS/2 + i/2, half i%2
+#pragma unroll
+        for (int i = 0; i < KC / 16; ++i)
+            *reinterpret_cast<u4v*>(st + (kh * (KS / 2) + (i >> 1)) * PLANE + fimg(rho, i & 1)) = q[i];
+#pragma unroll
+        for (int i = 0; i < WV; ++i) *reinterpret_cast<u4v*>(st + KS * PLANE + (i * 512 + t) * 16) = wv[set][i];
+    };
+
+    f16v acc[TFT][TDT];
+    auto mfma = [&](int buf, bool zinit) {
+        const char* st = lds + buf * STAGE;
+        const f16v zero = {};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            u4v wf[TFT], df[TDT];
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+                wf[a] = *reinterpret_cast<const u4v*>(st + (KS + ks) * PLANE + fimg(f_w + 32 * a + r, h));
+#pragma unroll
+            for (int b = 0; b < TDT; ++b)
+                df[b] = *reinterpret_cast<const u4v*>(st + ks * PLANE + fimg(d_w + 32 * b + r, h));
+#if SIR_NT16_ABL & 4
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b) {
+                    asm volatile("" :: "v"(wf[a]), "v"(df[b]));      // timing-only: no MFMAs
+                    if (zinit && ks == 0) acc[a][b] = zero;
+                }
+#else
+#pragma unroll
+            for (int a = 0; a < TFT; ++a)
+#pragma unroll
+                for (int b = 0; b < TDT; ++b)
+                    acc[a][b] = mfma16<BF>(wf[a], df[b], (zinit && ks == 0) ? zero : acc[a][b]);
+#endif
+        }
+    };
+    // C[m][n] = acc + bias[n]; rows past M fall outside the store's range, columns past N are
+    // sent past its end (dropped).  Lane indices re-derived from an opaque threadIdx copy so that
+    // they do not hold VGPRs through the steps.
+    auto epilogue = [&](const TileP& p) {
+        int tq = threadIdx.x;
+        asm volatile("" : "+v"(tq));
+        const int lq = tq & 63, rq = lq & 31, hq = lq >> 5, wq = tq >> 6;
+        const int d_wq = (wq / WF) * TDT * 32, f_wq = (wq % WF) * TFT * 32;
+        const uint32_t ldcb = (uint32_t)ldc * EC;
+        const uint32_t nrec = (uint32_t)p.rows * ldcb;
+        const rsrc_t crs = mk_rsrc(static_cast<char*>(C) + p.d0 * ldc * EC, (SIR_NT16_ABL & 2) ? 0u : nrec);
+        const uint32_t rv = (uint32_t)(d_wq + rq) * ldcb + (uint32_t)(f_wq + 4 * hq) * EC;
+#pragma unroll
+        for (int b = 0; b < TDT; ++b) {
+            const uint32_t rb = rv + (uint32_t)(32 * b) * ldcb;
+#pragma unroll
+            for (int a = 0; a < TFT; ++a) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int nc0 = p.f0 + 32 * a + 8 * g;
+                    const int n = nc0 + f_wq + 4 * hq;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_l + n);
+                    const float o0 = acc[a][b][4 * g + 0] + bb.x, o1 = acc[a][b][4 * g + 1] + bb.y;
+                    const float o2 = acc[a][b][4 * g + 2] + bb.z, o3 = acc[a][b][4 * g + 3] + bb.w;
+                    const uint32_t off = (n < N) ? rb : nrec;
+                    if constexpr (C32) {
+                        u4v ov;
+                        ov.x = __float_as_uint(o0); ov.y = __float_as_uint(o1);
+                        ov.z = __float_as_uint(o2); ov.w = __float_as_uint(o3);
+                        __builtin_amdgcn_raw_buffer_store_b128(ov, crs, off, nc0 * EC, 0);
+                    } else {
+                        typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+                        u2v ov;
+                        ov.x = pack2(o0, o1, BF);
+                        ov.y = pack2(o2, o3, BF);
+                        __builtin_amdgcn_raw_buffer_store_b64(ov, crs, off, nc0 * EC, 0);
+                    }
+                    // the store reads its data VGPRs over several cycles: keep the next writes of
+                    // them away (see k_gemm_nt_p's epilogue)
+                    __builtin_amdgcn_sched_barrier(0);
+                    asm volatile("s_nop 1" ::: "memory");
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+    };
+
+    // step c: chunk c is multiplied out of LDS buffer c & 1, chunks c+1 .. c+NS are in flight in
+    // register sets (c+1) % NS .. c % NS; chunk c+NS is issued into set c % NS (chunk c's, already
+    // in LDS), chunk c+1 is written into the other buffer.  Chunks past the tile's last come from
+    // the next tile (NC % NS == 0: its chunk i lands in set i % NS).
+    TileP cu = tile_p(tb), nx = tile_p(tb + 1);
+    static_for<0, NS>([&](auto I_) { load(decltype(I_)::value, cu, decltype(I_)::value); });
+    store(0, 0, cu, 0);
+    __syncthreads();
+    for (int j = 0; tb + j < te; ++j) {
+        const TileP nn = tile_p(tb + j + 2);
+        static_for<0, NC>([&](auto C_) {
+            constexpr int c = decltype(C_)::value;
+            constexpr int s = c % NS;
+            if constexpr (c + NS < NC) load(s, cu, c + NS);
+            else load(s, nx, c + NS - NC);
+            mfma(c & 1, c == 0);
+            if constexpr (c == NC - 1) epilogue(cu);
+            if constexpr (c + 1 < NC) store((c + 1) % NS, (c + 1) & 1, cu, c + 1);
+            else store(0, 0, nx, 0);
+            __syncthreads();
+        });
+        cu = nx;
+        nx = nn;
+    }
+}
+
+// 16-bit weight operand of k_gemm_nt16: B[n][k] (W[n][k], or W[k][n] with trans) rounded to the
+// MFMA type, in planes of 16 k: plane P = k / 16 holds the Npad rows in fimg order.
+__global__ void __launch_bounds__(64)
+k_pack16(const float* __restrict__ W, int64_t ldw, int N, int K, int trans, int bf, int Npad, unsigned short* __restrict__ out) {
+    const int n = blockIdx.x;
+    for (int k = threadIdx.x; k < K; k += 64) {
+        const float x = (n < N) ? (trans ? W[(int64_t)k * ldw + n] : W[(int64_t)n * ldw + k]) : 0.f;
+        const unsigned short b = bf ? __builtin_bit_cast(unsigned short, (__bf16)x) : __builtin_bit_cast(unsigned short, (_Float16)x);
+        const int P = k >> 4, j = k & 15;
+        out[((int64_t)P * Npad * 32 + fimg(n, j >> 3)) / 2 + (j & 7)] = b;
+    }
+}
+
 }  // namespace
 
 hipError_t run_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t R, int Mc, int Nc, int dtype,
@@ -235,6 +476,71 @@ hipError_t run_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb,
     e = run_gemm_reduce(part, P, (int64_t)Mc * Nc, Nc, C, ldc, st);
     if (e != hipSuccess || colsum == nullptr) return e;
     return run_gemm_reduce(cpart, P, (int64_t)Mc, Mc, colsum, 0, st);
+}
+
+
+int64_t gemm_pack16_bytes(int64_t N, int64_t K) { return (N + 255) / 256 * 256 * K * 2; }
+
+hipError_t run_gemm_pack16(const float* W, int64_t ldw, int N, int K, int trans, int dtype, void* packed, hipStream_t st) {
+    const int np = (N + 255) / 256 * 256;
+    hipLaunchKernelGGL(k_pack16, dim3(np), dim3(64), 0, st, W, ldw, N, K, trans, dtype == SIR_DTYPE_BF16 ? 1 : 0, np,
+                       static_cast<unsigned short*>(packed));
+    return hipGetLastError();
+}
+
+#ifndef SIR_NT16_KC
+#define SIR_NT16_KC 32          // k values per chunk of the 16-bit NT GEMM (32 or 64; 16-bit A only)
+#endif
+#ifndef SIR_NT16_NS
+#define SIR_NT16_NS 2           // register sets (chunks in flight) of the 16-bit NT GEMM, 16-bit A
+#endif
+#ifndef SIR_NT16_NS32
+#define SIR_NT16_NS32 2         // the same for an fp32 A
+#endif
+
+template <bool BF, bool A32, bool C32>
+static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, const void* packed, int N, const float* bias,
+                              void* C, int64_t ldc, unsigned short* Acopy, int64_t ldac, hipStream_t st) {
+    const int np = (N + 255) / 256 * 256, nft = np / 256;
+    const int64_t ntiles = (M + 255) / 256 * nft;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+        ncu = 256;
+    const int tpb = (int)((ntiles + ncu - 1) / ncu);
+    const int nblk = (int)((ntiles + tpb - 1) / tpb);
+    const auto* wp = static_cast<const u4v*>(packed);
+    constexpr int KC = (SIR_NT16_KC == 64 && !A32) ? 64 : 32;
+    constexpr int NS = A32 ? SIR_NT16_NS32 : SIR_NT16_NS;
+    const int nc = K / KC;
+#define SIR_NT16_L(NCV, NSV)                                                                                           \
+    hipLaunchKernelGGL((k_gemm_nt16<BF, A32, C32, KC, NCV, NSV>), dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, \
+                       np, bias, N, C, ldc, Acopy, ldac, nft, (int)ntiles, tpb)
+    if (nc == 256 / KC) SIR_NT16_L(256 / KC, (NS <= 256 / KC ? NS : 256 / KC));
+    else if (nc == 512 / KC) SIR_NT16_L(512 / KC, NS);
+    else if (nc == 128 / KC) SIR_NT16_L(128 / KC, (NS <= 128 / KC ? NS : 128 / KC));
+    else return hipErrorInvalidValue;
+#undef SIR_NT16_L
+    return hipGetLastError();
+}
+
+hipError_t run_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int K, const void* packed, int N, int dtype,
+                         const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac, hipStream_t st) {
+    if (M == 0) return hipSuccess;
+    const bool bf = dtype == SIR_DTYPE_BF16, a32 = a_dtype == SIR_DTYPE_F32, c32 = c_dtype == SIR_DTYPE_F32;
+    auto* acp = static_cast<unsigned short*>(Acopy);
+#define SIR_NT16_D(B, A3, C3) \
+    if (bf == B && a32 == A3 && c32 == C3) return launch_nt16<B, A3, C3>(A, lda, M, K, packed, N, bias, C, ldc, acp, ldac, st)
+    SIR_NT16_D(true, false, false);
+    SIR_NT16_D(true, false, true);
+    SIR_NT16_D(true, true, false);
+    SIR_NT16_D(true, true, true);
+    SIR_NT16_D(false, false, false);
+    SIR_NT16_D(false, false, true);
+    SIR_NT16_D(false, true, false);
+    SIR_NT16_D(false, true, true);
+#undef SIR_NT16_D
+    return hipErrorInvalidValue;
 }
 
 }  // namespace sir

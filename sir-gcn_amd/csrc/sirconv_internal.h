@@ -151,5 +151,10 @@ hipError_t run_gemm_reduce(const float* part, int P, int64_t count, int Nc, floa
 // 16-bit TN GEMM (sirconv_gemm16.hip): A, B bf16 (dtype SIR_DTYPE_BF16) or fp16, fp32 result
 hipError_t run_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t R, int Mc, int Nc, int dtype,
                          float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st);
+// 16-bit NT GEMM (sirconv_gemm16.hip): packed 16-bit weights, A 16-bit or fp32, C 16-bit or fp32
+int64_t gemm_pack16_bytes(int64_t N, int64_t K);
+hipError_t run_gemm_pack16(const float* W, int64_t ldw, int N, int K, int trans, int dtype, void* packed, hipStream_t st);
+hipError_t run_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int K, const void* packed, int N, int dtype,
+                         const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac, hipStream_t st);
 
 }  // namespace sir

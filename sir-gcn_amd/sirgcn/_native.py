@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -44,6 +44,9 @@ SIGNATURES = {
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
     "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
     "sir_gemm_tn16": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _I, _P, _I64, _P, _P, _I64, _P]),
+    "sir_gemm_pack16_bytes": (ctypes.c_int64, [_I64, _I64]),
+    "sir_gemm_pack16": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _I, _P, _P]),
+    "sir_gemm_nt16": (ctypes.c_int, [_P, _I64, _I, _I64, _I64, _P, _I64, _I, _P, _P, _I64, _I, _P, _I64, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
@@ -408,3 +411,41 @@ def gemm_tn16(A, B, out=None, colsum=False):
                                out.stride(0), _ptr(cs), _ptr(ws), ws.numel(), _stream(A.device))
     _check(rc, lib)
     return (out, cs) if colsum else out
+
+
+def gemm_pack16(W, dtype, trans=False):
+    """Pack the weight operand of ``gemm_nt16``: B = W ([N, K]) or W^T (trans), rounded to the
+    16-bit ``dtype`` (what autocast's ``W.to(dtype)`` holds).  Returns (packed, N, K, dtype)."""
+    lib = load()
+    assert W.dtype == torch.float32 and W.dim() == 2 and W.stride(1) == 1 and dtype in _DT16
+    N, K = (W.shape[1], W.shape[0]) if trans else (W.shape[0], W.shape[1])
+    nbytes = lib.sir_gemm_pack16_bytes(N, K)
+    if nbytes <= 0:
+        raise RuntimeError(f"sir_gemm_pack16_bytes({N}, {K}) failed")
+    packed = torch.empty((nbytes,), dtype=torch.uint8, device=W.device)
+    with _Timed("sir_gemm_pack16", W.device):
+        rc = lib.sir_gemm_pack16(_ptr(W), W.stride(0), N, K, int(bool(trans)), _DT16[dtype], _ptr(packed),
+                                 _stream(W.device))
+    _check(rc, lib)
+    return packed, N, K, dtype
+
+
+def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None):
+    """C = A B^T (+ bias) on the 16-bit MFMA kernel (``packed`` from gemm_pack16).  A in the
+    packed dtype or fp32 (rounded on load; ``acopy`` [M, K] of that dtype receives the rounded A);
+    C in ``out_dtype`` (the packed dtype by default, or fp32).  ``bias`` fp32 [N] (pass autocast's
+    dtype-rounded bias to match its nn.Linear)."""
+    lib = load()
+    pk, N, K, dt = packed
+    M = A.shape[0]
+    assert A.dim() == 2 and A.shape[1] == K and A.stride(1) == 1 and A.dtype in (dt, torch.float32)
+    od = out_dtype or dt
+    out = torch.empty((M, N), dtype=od, device=A.device)
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous()
+    with _Timed("sir_gemm_nt16", A.device, 2 * M * N * K):
+        rc = lib.sir_gemm_nt16(_ptr(A), A.stride(0), STORAGE[A.dtype], M, K, _ptr(pk), N, _DT16[dt], _ptr(bias),
+                               _ptr(out), out.stride(0), STORAGE[od], _ptr(acopy),
+                               acopy.stride(0) if acopy is not None else 0, _stream(A.device))
+    _check(rc, lib)
+    return out

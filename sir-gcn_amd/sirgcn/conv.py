@@ -228,21 +228,28 @@ class SIRConvFunction16(torch.autograd.Function):
     """The whole layer under autocast (bf16 / fp16 ``dt``, the reference's AMP path,
     ``heterophilous-datasets/train.py:75``), hand-scheduled like :class:`SIRConvFunction`:
 
-    forward : QK = X [W_Q; W_K]^T + [b_Q; 0] in dt (library GEMM, as autocast's nn.Linear)
+    forward : QK = X [W_Q; W_K]^T + [b_Q; 0] in dt (autocast's nn.Linear; native 16-bit MFMA
+              ``sir_gemm_nt16`` with the X.to(dt) cast fused into its loads)
               -> S = edge kernels on dt rows (fp32 math inside) -> Y = S W_R^T + b_R in dt
-    backward: G = dY W_R and dX = dQK [W_Q; W_K] in dt (library GEMMs, as autocast's autograd);
-              the weight gradients dW = dY^T S, [dQ dK]^T X and the bias gradients — contractions
-              over all V node rows, the shape half-precision library GEMMs run slowest — on the
-              native split-fp16 TN kernel from the dt values widened to fp32 (more accurate than
-              autocast's half-precision mm), fp32 like the parameters."""
+    backward: G = dY W_R in dt and dX = dQK [W_Q; W_K] (``sir_gemm_nt16``; dX for an fp32 X
+              straight from the fp32 accumulator); the weight gradients dW = dY^T S, [dQ dK]^T X
+              and the bias gradients — contractions over all V node rows — on the native 16-bit
+              TN kernel (exact 16-bit products, fp32 sums), fp32 like the parameters.  Small
+              graphs (and shapes the kernels do not take) run the same dataflow on torch's
+              half-precision GEMMs (``linalg.mm16_*``)."""
 
     @staticmethod
     def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on, dt):
         H = W_Q.shape[0]
-        Xh = X.to(dt)
-        W_cat = torch.cat([W_Q, W_K], 0).to(dt)
-        b_cat = torch.cat([b_Q, b_Q.new_zeros(H)]).to(dt) if b_Q is not None else None
-        QK = F.linear(Xh, W_cat, b_cat)
+        W_cat = torch.cat([W_Q, W_K], 0)
+        b_cat = torch.cat([b_Q, b_Q.new_zeros(H)]) if b_Q is not None else None
+        X = X.contiguous()
+        if X.dtype == dt:
+            Xh = X
+            QK = linalg.mm16_wt(X, W_cat, b_cat, dt)
+        else:       # X.to(dt) fused into the GEMM's loads; the rounded X (for dW) written by it
+            Xh = torch.empty(X.shape, dtype=dt, device=X.device)
+            QK = linalg.mm16_wt(X, W_cat, b_cat, dt, acopy=Xh)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=dt)
@@ -251,22 +258,21 @@ class SIRConvFunction16(torch.autograd.Function):
         nw = _native.mask_words(H, act) if (EdgeAggregate.use_mask and training) else 0
         mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=X.device, dtype=torch.int64) if nw else None
         _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, act, slope, S, partial, mask)
-        W_Rh = W_R.to(dt)
-        Y = F.linear(S, W_Rh, b_R.to(dt) if b_R is not None else None)
-        ctx.save_for_backward(Xh, W_cat, W_Rh, S, mask if mask is not None else QK)
+        Y = linalg.mm16_wt(S, W_R, b_R, dt)
+        ctx.save_for_backward(Xh, W_cat, W_R, S, mask if mask is not None else QK)
         ctx.masked = mask is not None
-        ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.x_dtype = plan, agg, act, slope, X.dtype
+        ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.x_dtype, ctx.dt = plan, agg, act, slope, X.dtype, dt
         ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
         return Y
 
     @staticmethod
     def backward(ctx, dY):
-        Xh, W_cat, W_Rh, S, saved = ctx.saved_tensors
-        plan, agg, act, slope = ctx.plan, ctx.agg, ctx.act, ctx.slope
-        H = W_Rh.shape[1]
+        Xh, W_cat, W_R, S, saved = ctx.saved_tensors
+        plan, agg, act, slope, dt = ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.dt
+        H = W_R.shape[1]
         V = Xh.shape[0]
-        dY = dY.contiguous().to(W_Rh.dtype)
-        G = dY @ W_Rh
+        dY = dY.contiguous().to(dt)
+        G = linalg.mm16_w(dY, W_R, dt)
         dW_R = db_R = None
         if ctx.needs_input_grad[4] or ctx.needs_input_grad[5]:
             dW_R, db_R = _weight_and_bias_grad16(dY, S, ctx.needs_input_grad[4],
@@ -277,9 +283,10 @@ class SIRConvFunction16(torch.autograd.Function):
         else:
             Q, K = saved[:, :H], saved[:, H:]
             mask = None
-        dQK = torch.empty((V, 2 * H), device=Xh.device, dtype=W_Rh.dtype)
+        dQK = torch.empty((V, 2 * H), device=Xh.device, dtype=dt)
         edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK)
-        dX = (dQK @ W_cat).to(ctx.x_dtype) if ctx.needs_input_grad[0] else None
+        # dX straight from the fp32 accumulator for an fp32 input (no 16-bit rounding, no cast pass)
+        dX = linalg.mm16_w(dQK, W_cat, dt, out_dtype=ctx.x_dtype) if ctx.needs_input_grad[0] else None
         dW_Q = dW_K = db_Q = None
         need_bq = ctx.has_bq and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[3] or need_bq:

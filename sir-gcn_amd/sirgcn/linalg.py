@@ -101,3 +101,46 @@ def _tn_torch(A, B):
     if n < V:
         out += A[n:].t() @ B[n:]
     return out
+
+
+# ---------------------------------------------------------------------------- 16-bit NT (autocast)
+# The half-precision nn.Linear of the autocast path (forward x W^T + b, input gradient dY W) on the
+# native 16-bit MFMA kernel (``sir_gemm_nt16``): fp32 A is rounded to the 16-bit type on load (the
+# X.to(dt) cast fused in), the result is rounded once from the fp32 accumulator (or kept in fp32
+# for the fp32 input's gradient).  Below MIN_ROWS_16 rows, or for shapes the kernel does not take,
+# the same dataflow runs on torch's half-precision GEMM.
+NT16_K = (128, 256, 512)
+
+
+def _nt16_ok(A, K, N, dt):
+    return (USE_NATIVE and A.is_cuda and A.dim() == 2 and A.stride(1) == 1 and A.dtype in (dt, torch.float32)
+            and A.shape[0] >= MIN_ROWS_16 and K in NT16_K and N <= 512 and N % 4 == 0
+            and A.stride(0) % (4 if A.dtype == torch.float32 else 8) == 0 and A.stride(0) <= MAX_LD
+            and A.data_ptr() % 16 == 0)
+
+
+def mm16_wt(A, W, bias, dt, out_dtype=None, acopy=None):
+    """F.linear(A.to(dt), W.to(dt), bias.to(dt)) (autocast's nn.Linear), result in ``out_dtype``
+    (default dt).  ``acopy``: a [M, K] dt tensor that receives A.to(dt) when A is fp32."""
+    N, K = W.shape
+    od = out_dtype or dt
+    if _nt16_ok(A, K, N, dt) and (acopy is None or (A.dtype == torch.float32 and acopy.stride(1) == 1
+                                                     and acopy.data_ptr() % 16 == 0)):
+        b = bias.to(dt).float().contiguous() if bias is not None else None
+        return _native.gemm_nt16(A, _native.gemm_pack16(W.contiguous().float(), dt), b, od, acopy)
+    Ah = A.to(dt)
+    if acopy is not None:
+        acopy.copy_(Ah)
+    out = torch.nn.functional.linear(Ah, W.to(dt), bias.to(dt) if bias is not None else None)
+    return out if out.dtype == od else out.to(od)
+
+
+def mm16_w(A, W, dt, out_dtype=None):
+    """(A.to(dt) @ W.to(dt)) in ``out_dtype`` (default dt): the input gradient of autocast's
+    nn.Linear; W [K, N]."""
+    K, N = W.shape
+    od = out_dtype or dt
+    if _nt16_ok(A, K, N, dt):
+        return _native.gemm_nt16(A, _native.gemm_pack16(W.contiguous().float(), dt, trans=True), None, od)
+    out = A.to(dt) @ W.to(dt)
+    return out if out.dtype == od else out.to(od)

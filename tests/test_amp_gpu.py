@@ -180,3 +180,47 @@ def test_amp_training_step_with_grad_scaler():
         assert e <= max(1e-2, AMP_SLACK * e_ref), (n, e, e_ref)
     scaler.step(opt)
     scaler.update()
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+def test_autocast_layer_native_nt16_large(dt, monkeypatch):
+    """Above linalg.MIN_ROWS_16 rows the autocast layer runs its four NT projections on the native
+    16-bit kernel (X.to(dt) fused into the QK GEMM's loads, dX straight from the fp32 accumulator):
+    every output and gradient within the AMP bar of the fp32 layer, and no worse than 1.25x the
+    reference's own AMP dataflow (oracle.SIRConvRef under the same autocast)."""
+    calls = []
+    real = _native.gemm_nt16
+    monkeypatch.setattr(_native, "gemm_nt16", lambda *a, **k: calls.append(1) or real(*a, **k))
+    V, E, H = 20000, 200000, 256
+    g = torch.Generator().manual_seed(21)
+    src, dst = torch.randint(0, V, (E,), generator=g), torch.randint(0, V, (E,), generator=g)
+    X = torch.randn(V, H, generator=g).to(DEV)
+    dY = torch.randn(V, H, generator=g).to(DEV)
+    torch.manual_seed(3)
+    m = SIRConv(H, H, H, nn.LeakyReLU(0.2), 0, agg_type="sum").to(DEV)
+    mr = oracle.SIRConvRef(H, H, H, nn.LeakyReLU(0.2), 0, agg_type="sum").to(DEV)
+    mr.load_state_dict(m.state_dict())
+    G = Graph(src, dst, V)
+
+    def run(mod, amp):
+        mod.zero_grad(set_to_none=True)
+        x = X.clone().requires_grad_(True)
+        if amp:
+            with torch.autocast("cuda", dtype=DT[dt]):
+                Y = mod(G, x)
+        else:
+            Y = mod(G, x)
+        Y.backward(dY.to(Y.dtype))
+        out = {"Y": Y, "dX": x.grad}
+        out.update({n: p.grad for n, p in mod.named_parameters()})
+        return {k: v.detach().double().cpu() for k, v in out.items()}
+
+    ref32 = run(m, False)
+    n0 = len(calls)
+    got = run(m, True)
+    assert len(calls) - n0 == 4, "QK, Y, G and dX on sir_gemm_nt16"
+    amp = run(mr, True)
+    tol = 2e-2 if dt == "bf16" else 1e-2
+    for k, v in got.items():
+        e, e_amp = rel_err(v, ref32[k]), rel_err(amp[k], ref32[k])
+        assert e <= max(tol, AMP_SLACK * e_amp), f"{k}: relL2 {e:.3e} vs fp32 (reference AMP {e_amp:.3e})"

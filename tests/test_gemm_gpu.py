@@ -197,3 +197,71 @@ def test_gemm_errors_are_loud():
     pk = _native.gemm_pack(torch.randn(8, 6, device=DEV))
     with pytest.raises(RuntimeError, match="multiples of 4"):
         _native.gemm_nt(A, pk)
+
+
+# ---------------------------------------------------------------------------- 16-bit NT (autocast)
+def _nt16_ref(A, W, bias, dt, trans):
+    """fp64 of autocast's half-precision nn.Linear on the rounded operands: A.to(dt), W.to(dt),
+    bias.to(dt) (each 16-bit product exact; fp64 sums)."""
+    Wd = W.to(dt).double()
+    B = Wd.t() if trans else Wd
+    ref = A.to(dt).double() @ B.t()
+    if bias is not None:
+        ref = ref + bias.to(dt).double()
+    return ref
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("a32", [False, True])
+@pytest.mark.parametrize("M,K,N,trans,with_bias", [(4133, 256, 512, False, True), (2000, 256, 256, False, True),
+                                                   (517, 512, 256, True, False), (300, 256, 256, True, False),
+                                                   (1000, 128, 100, False, True), (70, 256, 4, False, False),
+                                                   (0, 256, 256, False, True), (33000, 256, 256, False, True)])
+def test_gemm_nt16_vs_fp64(dt, a32, M, K, N, trans, with_bias):
+    """sir_gemm_nt16 (the autocast forward projections and input gradients) against fp64 of the
+    same rounded operands: the fp32-output result within the fp32 accumulation bound, the 16-bit
+    output within one unit of its last place of the correctly rounded value (the fp32 sum may sit
+    on the other side of a rounding boundary), and — for an fp32 A — the rounded copy equal to
+    A.to(dt) bit for bit."""
+    g = torch.Generator(device=DEV).manual_seed(M + 3 * K + N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    if not a32:
+        A = A.to(dt)
+    W = torch.randn(K, N, device=DEV, generator=g) if trans else torch.randn(N, K, device=DEV, generator=g)
+    W *= K ** -0.5
+    bias = torch.randn(N, device=DEV, generator=g) if with_bias else None
+    pk = _native.gemm_pack16(W, dt, trans=trans)
+    b = bias.to(dt).float() if bias is not None else None
+    acopy = torch.full((M, K), 7.0, device=DEV, dtype=dt) if a32 else None
+    C32 = _native.gemm_nt16(A, pk, b, torch.float32, acopy)
+    C16 = _native.gemm_nt16(A, pk, b)
+    assert C16.dtype == dt and C32.dtype == torch.float32
+    if M == 0:
+        return
+    if a32:
+        assert torch.equal(acopy, A.to(dt)), "rounded copy of A"
+    ref = _nt16_ref(A, W, bias, dt, trans)
+    absum = A.to(dt).double().abs() @ (W.to(dt).double().t() if trans else W.to(dt).double()).abs().t()
+    err = (C32.double() - ref).abs()
+    assert torch.all(err <= 4 * K * 2.0 ** -24 * absum + 1e-30), f"nt16 fp32 out: max err {err.max().item():.3e}"
+    # 16-bit output: within 1 ulp of the correctly rounded reference
+    r16 = ref.to(dt)
+    ulp = (r16.double().abs() * 2.0 ** (-7 if dt == torch.bfloat16 else -10)).clamp_min(2.0 ** -126)
+    d16 = (C16.double() - r16.double()).abs()
+    assert torch.all(d16 <= ulp + 4 * K * 2.0 ** -24 * absum), f"nt16 16-bit out: max diff {d16.max().item():.3e}"
+    assert torch.equal(C16, _native.gemm_nt16(A, pk, b)), "deterministic"
+
+
+def test_gemm_nt16_strided_rows_and_errors():
+    """lda > K (a column slice of a wider 16-bit tensor), ldc > N, and loud errors."""
+    g = torch.Generator(device=DEV).manual_seed(12)
+    A0 = torch.randn(5000, 640, device=DEV, generator=g).to(torch.bfloat16)
+    A = A0[:, 64:320]
+    W = torch.randn(256, 256, device=DEV, generator=g) * 0.0625
+    pk = _native.gemm_pack16(W, torch.bfloat16)
+    C = _native.gemm_nt16(A, pk, None, torch.float32)
+    ref = A.double() @ W.to(torch.bfloat16).double().t()
+    assert _rel(C.double(), ref) < 1e-6
+    with pytest.raises(RuntimeError, match="bad shape"):
+        _native.gemm_nt16(torch.zeros(10, 96, device=DEV, dtype=torch.bfloat16),
+                          _native.gemm_pack16(torch.zeros(8, 96, device=DEV), torch.bfloat16))
