@@ -346,8 +346,9 @@ int sir_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_
  * SIR_DTYPE_F32 (A rounded to dtype on load: the autocast cast fused into the GEMM; with
  * Acopy != NULL the rounded A is also written to Acopy [M, K] (ldac)); c_dtype = dtype (RNE of the
  * fp32 accumulator) or SIR_DTYPE_F32.  bias [N] fp32 (the caller passes the dtype-rounded bias of
- * autocast) or NULL.  K in {128, 256, 512}; N <= 512, N and lda multiples of 8 (16-bit A) / 4;
- * ldc >= N; A, C, Acopy, packed 16-B aligned.  One 16-bit MFMA per step, fp32 accumulation. */
+ * autocast) or NULL.  K in {128, 256, 512}; N <= 512; lda, N and ldc multiples of 16 bytes of
+ * A / C (8 16-bit or 4 fp32 elements); ldc >= N; A, C, Acopy, packed 16-B aligned.  One 16-bit
+ * MFMA per step, fp32 accumulation. */
 int64_t sir_gemm_pack16_bytes(int64_t N, int64_t K);
 int sir_gemm_pack16(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, int dtype, void* packed, void* stream);
 int sir_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int64_t K, const void* packed, int64_t N,

@@ -582,8 +582,9 @@ int sir_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int64_t K,
     if (M < 0 || N <= 0 || N > 512 || (K != 128 && K != 256 && K != 512)) return fail(SIR_EINVAL, fn, "bad shape");
     if ((M + 255) / 256 * ((N + 255) / 256) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
     const int64_t av = a_dtype == SIR_DTYPE_F32 ? 4 : 8;     // elements per 16 B of A
-    if (N % 4 != 0 || lda % av != 0 || lda < K || ldc < N || ldc % 4 != 0)
-        return fail(SIR_EINVAL, fn, "N, ldc multiples of 4, lda a multiple of 16 B, lda >= K, ldc >= N");
+    const int64_t cv = c_dtype == SIR_DTYPE_F32 ? 4 : 8;     // elements per 16 B of C
+    if (N % cv != 0 || lda % av != 0 || lda < K || ldc < N || ldc % cv != 0)
+        return fail(SIR_EINVAL, fn, "N, ldc multiples of 16 B of C, lda a multiple of 16 B, lda >= K, ldc >= N");
     if (lda > SIR_GEMM_MAX_LD || ldc > SIR_GEMM_MAX_LD) return fail(SIR_EINVAL, fn, "lda/ldc too large");
     if (Acopy != nullptr && (a_dtype != SIR_DTYPE_F32 || ldac < K || ldac % 8 != 0 || ldac > SIR_GEMM_MAX_LD))
         return fail(SIR_EINVAL, fn, "Acopy needs an fp32 A and ldac >= K, a multiple of 8");

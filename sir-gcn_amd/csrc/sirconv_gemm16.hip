@@ -228,6 +228,9 @@ k_gemm_tn16(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
 // Chunks of KC k-values: a thread loads half of one row's chunk (KC/2 values) and the same
 // number of packed weight bytes into a register set, two sets alternate (two chunks in flight
 // while one is multiplied out of LDS), and the pipeline runs on across tile boundaries.
+#ifndef SIR_NT16_EPI
+#define SIR_NT16_EPI 1          // 16-bit NT epilogue through LDS with whole-row stores (1) or fragment stores (0)
+#endif
 #ifndef SIR_NT16_ABL
 #define SIR_NT16_ABL 0          // timing-only ablations: 1 = A loads dropped, 2 = C stores dropped, 4 = no MFMAs
 #endif
@@ -263,8 +266,11 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
     static_assert(KC == 32 || KC == 64, "chunk");
     static_assert(WV >= 1, "weight loader");
     static_assert(NS >= 2 && NS <= NC && NC % NS == 0, "register sets: a tile's chunks map to sets the same way");
-    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 512 * 4];
+    constexpr int EPITCH = BFT * EC + 16;             // epilogue image row pitch (bytes)
+    constexpr int EPI_BYTES = SIR_NT16_EPI ? 64 * EPITCH : 0;
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 512 * 4 + EPI_BYTES];
     float* const bias_l = reinterpret_cast<float*>(lds + 2 * STAGE);
+    char* const epi = lds + 2 * STAGE + 512 * 4;
 
     const int t = threadIdx.x;
     const int tb = blockIdx.x * tiles_per_block;
@@ -369,6 +375,64 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
     // C[m][n] = acc + bias[n]; rows past M fall outside the store's range, columns past N are
     // sent past its end (dropped).  Lane indices re-derived from an opaque threadIdx copy so that
     // they do not hold VGPRs through the steps.
+#if SIR_NT16_EPI
+    // Epilogue through LDS: per round b, every wave writes its 32-row band b (bias added, rounded
+    // to the output type) into a row-major image of 64 tile rows, then the block stores whole
+    // output rows — each wave-instruction writes 1 KiB of contiguous row bytes (2 bf16 / 1 fp32
+    // rows) instead of 32 rows x 16 B (the fragment-order stores made the 16-bit Y GEMM spend 45 %
+    // of its time on its stores: timing ablation, profiles/r02_ab_nt16.txt).
+    auto epilogue = [&](const TileP& p) {
+        int tq = threadIdx.x;
+        asm volatile("" : "+v"(tq));
+        const int lq = tq & 63, rq = lq & 31, hq = lq >> 5, wq = tq >> 6;
+        const int f_wq = (wq % WF) * TFT * 32;
+        const uint32_t ldcb = (uint32_t)ldc * EC;
+        const uint32_t nrec = (uint32_t)p.rows * ldcb;
+        const rsrc_t crs = mk_rsrc(static_cast<char*>(C) + p.d0 * ldc * EC, (SIR_NT16_ABL & 2) ? 0u : nrec);
+        char* const wrow = epi + ((wq / WF) * 32 + rq) * EPITCH + (f_wq + 4 * hq) * EC;
+#pragma unroll
+        for (int b = 0; b < TDT; ++b) {
+#pragma unroll
+            for (int a = 0; a < TFT; ++a) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int nl = f_wq + 32 * a + 8 * g + 4 * hq;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_l + p.f0 + nl);
+                    const float o0 = acc[a][b][4 * g + 0] + bb.x, o1 = acc[a][b][4 * g + 1] + bb.y;
+                    const float o2 = acc[a][b][4 * g + 2] + bb.z, o3 = acc[a][b][4 * g + 3] + bb.w;
+                    char* d = wrow + (32 * a + 8 * g) * EC;
+                    if constexpr (C32) {
+                        *reinterpret_cast<float4*>(d) = make_float4(o0, o1, o2, o3);
+                    } else {
+                        typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+                        u2v ov;
+                        ov.x = pack2(o0, o1, BF);
+                        ov.y = pack2(o2, o3, BF);
+                        *reinterpret_cast<u2v*>(d) = ov;
+                    }
+                }
+            }
+            __syncthreads();
+            constexpr int PR = BFT * EC / 16;                 // 16-B pieces per image row
+#pragma unroll
+            for (int i = 0; i < 64 * PR / 512; ++i) {
+                const int q = tq + 512 * i;
+                const int ir = q / PR, c16 = q % PR;
+                const u4v v = *reinterpret_cast<const u4v*>(epi + ir * EPITCH + c16 * 16);
+                const int ml = (ir >> 5) * (TDT * 32) + 32 * b + (ir & 31);      // row within the tile
+                const int n = p.f0 + c16 * (16 / EC);
+                const uint32_t off = (n < N) ? (uint32_t)ml * ldcb + (uint32_t)c16 * 16u : nrec;
+                __builtin_amdgcn_raw_buffer_store_b128(v, crs, off, p.f0 * EC, 0);
+                // the store reads its data VGPRs over several cycles: keep the next writes of
+                // them away (see k_gemm_nt_p's epilogue)
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_nop 1" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+        }
+    };
+#else
     auto epilogue = [&](const TileP& p) {
         int tq = threadIdx.x;
         asm volatile("" : "+v"(tq));
@@ -412,6 +476,8 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
             }
         }
     };
+
+#endif
 
     // step c: chunk c is multiplied out of LDS buffer c & 1, chunks c+1 .. c+NS are in flight in
     // register sets (c+1) % NS .. c % NS; chunk c+NS is issued into set c % NS (chunk c's, already

@@ -114,7 +114,7 @@ NT16_K = (128, 256, 512)
 
 def _nt16_ok(A, K, N, dt):
     return (USE_NATIVE and A.is_cuda and A.dim() == 2 and A.stride(1) == 1 and A.dtype in (dt, torch.float32)
-            and A.shape[0] >= MIN_ROWS_16 and K in NT16_K and N <= 512 and N % 4 == 0
+            and A.shape[0] >= MIN_ROWS_16 and K in NT16_K and N <= 512 and N % 8 == 0
             and A.stride(0) % (4 if A.dtype == torch.float32 else 8) == 0 and A.stride(0) <= MAX_LD
             and A.data_ptr() % 16 == 0)
 

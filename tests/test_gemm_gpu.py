@@ -215,7 +215,7 @@ def _nt16_ref(A, W, bias, dt, trans):
 @pytest.mark.parametrize("a32", [False, True])
 @pytest.mark.parametrize("M,K,N,trans,with_bias", [(4133, 256, 512, False, True), (2000, 256, 256, False, True),
                                                    (517, 512, 256, True, False), (300, 256, 256, True, False),
-                                                   (1000, 128, 100, False, True), (70, 256, 4, False, False),
+                                                   (1000, 128, 104, False, True), (70, 256, 8, False, False),
                                                    (0, 256, 256, False, True), (33000, 256, 256, False, True)])
 def test_gemm_nt16_vs_fp64(dt, a32, M, K, N, trans, with_bias):
     """sir_gemm_nt16 (the autocast forward projections and input gradients) against fp64 of the
@@ -265,3 +265,6 @@ def test_gemm_nt16_strided_rows_and_errors():
     with pytest.raises(RuntimeError, match="bad shape"):
         _native.gemm_nt16(torch.zeros(10, 96, device=DEV, dtype=torch.bfloat16),
                           _native.gemm_pack16(torch.zeros(8, 96, device=DEV), torch.bfloat16))
+    with pytest.raises(RuntimeError, match="multiples of 16 B"):     # 16-bit C rows in 16-B pieces
+        _native.gemm_nt16(torch.zeros(10, 256, device=DEV, dtype=torch.bfloat16),
+                          _native.gemm_pack16(torch.zeros(12, 256, device=DEV), torch.bfloat16))
