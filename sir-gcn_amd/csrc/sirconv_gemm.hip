@@ -482,6 +482,9 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #ifndef SIR_NT_P_KSB
 #define SIR_NT_P_KSB 1
 #endif
+#ifndef SIR_NT_P_EPI
+#define SIR_NT_P_EPI 1          // persistent NT epilogue through LDS with whole-row stores (1) or fragment stores (0)
+#endif
 constexpr int NT_P_NMAX = 512;
 
 template <int NCT>
@@ -657,6 +660,62 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
     // re-derived from an opaque copy of threadIdx.x inside the epilogue: hoisted out of the tile
     // loop, its addresses and offsets would hold VGPRs through every step and force spills
     // (whose reloads, vector-memory ops, drain the load queue).
+#if SIR_NT_P_EPI
+    // Epilogue through LDS (stage 1: free after a tile's last step — the next tile's first chunk
+    // is in stage 0 — and the 64-row image of pitch BF*4 + 16 is exactly STAGE bytes): per round b
+    // every wave writes its 32-row band b, then the block stores whole output rows (one 1-KiB row
+    // per wave-instruction instead of 32 rows x 32 B; the 16-bit kernel's timing ablation put 45 %
+    // of a GEMM on the fragment-order stores).  Called after the tile's last step; it ends with a
+    // barrier, so the next tile's first split into stage 1 follows it.
+    auto epilogue = [&](const TileP& p, int slot) {
+        int tq = threadIdx.x;
+        asm volatile("" : "+v"(tq));
+        const int lq = tq & 63, rq = lq & 31, hq = lq >> 5, wq = tq >> 6;
+        const int d_wq = (wq / WF) * TDT * 32, f_wq = (wq % WF) * TFT * 32;
+        constexpr int PITCH = BF * 4 + 16;
+        static_assert(64 * PITCH <= STAGE, "epilogue image fits the free stage");
+        char* const img = lds + STAGE;
+        const uint32_t ldc4 = (uint32_t)ldc * 4u;
+        const uint32_t nrec = (uint32_t)p.rows * ldc4;
+        const rsrc_t crs = mk_rsrc(C + p.d0 * ldc, (SIR_ABL_NT & 2) ? 0u : nrec);
+        const float* sc = fin + slot * BD;
+        char* const wrow = img + ((wq / WF) * 32 + rq) * PITCH + (f_wq + 4 * hq) * 4;
+#pragma unroll
+        for (int b = 0; b < TDT; ++b) {
+            const float is = sc[d_wq + 32 * b + rq];
+#pragma unroll
+            for (int a = 0; a < TFT; ++a) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = p.f0 + f_wq + 32 * a + 8 * g + 4 * hq;
+                    const float4 it = *reinterpret_cast<const float4*>(inv_l + n);
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_l + n);   // -0 without bias
+                    float4 o;
+                    o.x = acc[a][b][4 * g + 0] * is * it.x + bb.x;
+                    o.y = acc[a][b][4 * g + 1] * is * it.y + bb.y;
+                    o.z = acc[a][b][4 * g + 2] * is * it.z + bb.z;
+                    o.w = acc[a][b][4 * g + 3] * is * it.w + bb.w;
+                    *reinterpret_cast<float4*>(wrow + (32 * a + 8 * g) * 4) = o;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int ir = wq + 8 * i, c16 = lq;                 // image row, 16-B piece of it
+                const u4v v = *reinterpret_cast<const u4v*>(img + ir * PITCH + c16 * 16);
+                const int ml = (ir >> 5) * (TDT * 32) + 32 * b + (ir & 31);
+                const int n = p.f0 + 4 * c16;
+                const uint32_t off = (n < N) ? (uint32_t)ml * ldc4 + (uint32_t)c16 * 16u : nrec;
+                __builtin_amdgcn_raw_buffer_store_b128(v, crs, off, p.f0 * 4, 0);
+                // a 16-byte store reads its data VGPRs over several cycles (see below)
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_nop 1" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+        }
+    };
+#else
     auto epilogue = [&](const TileP& p, int slot) {
         int tq = threadIdx.x;
         asm volatile("" : "+v"(tq));
@@ -702,6 +761,8 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
             }
         }
     };
+
+#endif
 
 #if SIR_NT_PRIO == 2
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
