@@ -829,6 +829,69 @@ __device__ __forceinline__ void mask_item_dst_wide(int e0, int e1, const int* __
     }
 }
 
+#ifndef SIR_DQ_SMEM
+#define SIR_DQ_SMEM 0           // 1: dQ pass (sum / mean, H <= 256) mask words by prefetched scalar loads (+13 %: rejected, profiles/r02_ab_dq_smem2.txt)
+#endif
+
+// dQ pass, scalar form (sum / mean, NV = 1: 4 words per edge): the mask words of a 4-edge
+// sub-batch (128 B, contiguous) come by two s_load_dwordx16 straight into SGPRs — the selects'
+// lane-mask operands — so no v_readlane is needed (8 per edge in the vector forms: the pass was
+// VALU-bound on them).  Scalar loads may return out of order (one lgkmcnt for all), so the next
+// sub-batch's loads are issued only after the current one's words have arrived, then overlap
+// its selects and adds.  Same per-column edge order as the other forms: bit-identical.
+template <int ST, int ACT, int AGG>
+__device__ __forceinline__ void mask_item_dst_smem(int e0, int e1, const uint64_t* __restrict__ mask, float slope,
+                                                   int HC, int lane, const float (&gv)[1][4], float (&acc)[1][4]) {
+    struct W16 { uint64_t w[16]; };
+    auto load = [&](int eb) {
+        W16 x;
+        const uint64_t* p = mask + (int64_t)__builtin_amdgcn_readfirstlane(eb) * 4;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x.w[k] = p[k];
+        return x;
+    };
+    auto arrived = [&](const W16& x) {       // wait for x (and nothing else is in flight)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("" :: "s"(x.w[k]) : "memory");
+    };
+    const bool ok = lane < HC;
+    auto compute = [&](const W16& x, int n) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < n && ok) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) acc[0][w] += sel_mask<ACT>(x.w[4 * i + w], gv[0][w], slope);
+            }
+        }
+    };
+    int e = e0;
+    if (e + 4 <= e1) {
+        W16 a = load(e);
+        for (; e + 8 <= e1; e += 8) {
+            arrived(a);
+            const W16 b = load(e + 4);
+            compute(a, 4);
+            arrived(b);
+            if (e + 12 <= e1) a = load(e + 8);
+            compute(b, 4);
+        }
+        if (e + 4 <= e1) {
+            arrived(a);
+            compute(a, 4);
+            e += 4;
+        }
+    }
+    for (; e < e1; ++e) {                    // 0 .. 3 edges
+        uint64_t wd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wd[k] = uniform64(mask[(int64_t)e * 4 + k]);
+        if (ok) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) acc[0][w] += sel_mask<ACT>(wd[w], gv[0][w], slope);
+        }
+    }
+}
+
 __device__ __forceinline__ int4 uniform_item(const int4* __restrict__ items, int64_t i) {
     int4 it = items[i];
     it.x = __builtin_amdgcn_readfirstlane(it.x);
@@ -882,7 +945,9 @@ mask_pass_item(int64_t wave, const int* __restrict__ rowptr, const int* __restri
     }
     float nr = 1.f;
     if constexpr (AGG == AGG_SYM) nr = norm_row[row];
-    if constexpr (SIR_DQ_WIDE && MODE == MODE_BWD_DST)
+    if constexpr (SIR_DQ_SMEM && MODE == MODE_BWD_DST && AGG != AGG_SYM && NV == 1)
+        mask_item_dst_smem<ST, ACT, AGG>(e0, e1, mask, slope, HC, lane, gv, acc);
+    else if constexpr (SIR_DQ_WIDE && MODE == MODE_BWD_DST)
         mask_item_dst_wide<ST, ACT, AGG, NV>(e0, e1, col, mask, norm_col, nr, slope, lane, HC, gv, acc);
     else if constexpr (SIR_DQ_PF && MODE == MODE_BWD_DST && AGG != AGG_SYM && U * NV * 4 <= 64)
         mask_item_dst<ST, ACT, AGG, NV, U>(e0, e1, col, mask, norm_col, nr, slope, lane, HC, gv, acc);
