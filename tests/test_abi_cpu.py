@@ -77,6 +77,35 @@ def test_argument_checks_are_synchronous_and_reported():
     assert rc == 1 and b"perm" in lib.sir_last_error()
 
 
+def test_gemm16_argument_checks():
+    """sir_gemm_pack16 / sir_gemm_nt16 (the autocast projections): bad dtypes, shapes and
+    alignments are rejected synchronously with a message; sizing returns 0 for bad shapes."""
+    lib = _native.load()
+    n = _null()
+    assert lib.sir_gemm_pack16_bytes(256, 256) == 256 * 256 * 2
+    assert lib.sir_gemm_pack16_bytes(100, 256) == 256 * 256 * 2          # N padded to 256 rows
+    assert lib.sir_gemm_pack16_bytes(256, 100) == 0                      # K % 16 != 0
+    assert lib.sir_gemm_pack16(n, 256, 256, 256, 0, 0, n, n) == 1 and b"BF16 or F16" in lib.sir_last_error()
+    BF, F32 = 1, 0
+    # K must be 128 / 256 / 512, N <= 512
+    assert lib.sir_gemm_nt16(n, 300, BF, 10, 300, n, 256, BF, n, n, 256, BF, n, 0, n) == 1
+    assert b"bad shape" in lib.sir_last_error()
+    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 1024, BF, n, n, 1024, BF, n, 0, n) == 1
+    # a_dtype / c_dtype must be the MFMA type or F32
+    assert lib.sir_gemm_nt16(n, 256, 2, 10, 256, n, 256, BF, n, n, 256, BF, n, 0, n) == 1
+    assert b"a_dtype" in lib.sir_last_error()
+    # 16-bit C: N a multiple of 8
+    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 12, BF, n, n, 12, BF, n, 0, n) == 1
+    assert b"multiples of 16 B" in lib.sir_last_error()
+    # the rounded copy of A needs an fp32 A
+    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 256, BF, n, n, 256, BF, ctypes.c_void_p(16), 256, n) == 1
+    assert b"Acopy" in lib.sir_last_error()
+    # NULL buffers with work; an empty M is a no-op
+    assert lib.sir_gemm_nt16(n, 256, F32, 10, 256, n, 256, BF, n, n, 256, F32, n, 0, n) == 1
+    assert b"NULL" in lib.sir_last_error()
+    assert lib.sir_gemm_nt16(n, 256, F32, 0, 256, n, 256, BF, n, n, 256, F32, n, 0, n) == 0
+
+
 def test_mask_words_contract():
     lib = _native.load()
     assert lib.sir_mask_words(256, 2) == 4 and lib.sir_mask_words(256, 1) == 4
