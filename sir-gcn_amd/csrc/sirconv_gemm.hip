@@ -1098,12 +1098,23 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     }
 }
 
+// Partials added in split order; the loads are issued 16 at a time ahead of the (sequential,
+// same-order) adds — a dependent one-load-per-add loop kept one load in flight per thread and
+// took ~50 us per call at P = 256 (and longer for the many-split small shapes).
 __global__ void __launch_bounds__(256)
 k_gemm_reduce(const float* __restrict__ part, int P, int64_t count, int Nc, float* __restrict__ C, int64_t ldc) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= count) return;
     float s = 0.f;
-    for (int q = 0; q < P; ++q) s += part[(int64_t)q * count + i];
+    int q = 0;
+    for (; q + 16 <= P; q += 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = part[(int64_t)(q + j) * count + i];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    for (; q < P; ++q) s += part[(int64_t)q * count + i];
     C[(i / Nc) * ldc + i % Nc] = s;
 }
 
@@ -1178,10 +1189,13 @@ hipError_t run_gemm_reduce(const float* part, int P, int64_t count, int Nc, floa
     return hipGetLastError();
 }
 
+#ifndef SIR_TN_MINROWS
+#define SIR_TN_MINROWS 1024     // fewest node rows per split of the TN GEMMs (1024: cfg2 TN16 -30 %, profiles/r02_ab_tn_reduce.txt)
+#endif
 int gemm_tn_splits(int64_t R, int64_t Mc, int64_t Nc) {
     const int64_t tiles = ((Mc + 255) / 256) * ((Nc + 255) / 256);
     int64_t P = (256 + tiles - 1) / tiles;
-    const int64_t pmax = (R + 2047) / 2048;      // >= 2048 rows per split
+    const int64_t pmax = (R + SIR_TN_MINROWS - 1) / SIR_TN_MINROWS;      // >= SIR_TN_MINROWS rows per split
     if (P > pmax) P = pmax;
     if (P < 1) P = 1;
     return (int)P;

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--H", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--tn", nargs="*", default=[], help="also time sir_gemm_tn16 at R,M,N (e.g. 229532,256,128)")
+    ap.add_argument("--no-nt", action="store_true")
     a = ap.parse_args()
     V, H, dev, dt = a.V, a.H, "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
@@ -69,7 +71,21 @@ def main():
             ("dX K=2H f32", lambda: lib.sir_gemm_nt16(P(dQK), 2 * H, BF, V, 2 * H, P(p2t), H, BF, None, P(dX), H, F32, None, 0, st), dX),
         ]
 
-    runs = {n: shapes(lib) for n, lib in libs}
+    def tn_shapes(lib):
+        out = []
+        g.manual_seed(1)          # the same operands for every library
+        for spec in a.tn:
+            R, M, N = (int(x) for x in spec.split(","))
+            At = torch.randn(R, M, device=dev, generator=g).to(dt)
+            Bt = torch.randn(R, N, device=dev, generator=g).to(dt)
+            C = torch.empty(M, N, device=dev)
+            cs = torch.empty(M, device=dev)
+            ws = torch.empty((max(lib.sir_gemm_tn_workspace(R, M, N), 4),), dtype=torch.uint8, device=dev)
+            out.append((f"tn16 {R}x{M}x{N}", (lambda At=At, Bt=Bt, C=C, cs=cs, ws=ws, R=R, M=M, N=N:
+                        lib.sir_gemm_tn16(P(At), M, P(Bt), N, R, M, N, BF, P(C), N, P(cs), P(ws), ws.numel(), st)), C))
+        return out
+
+    runs = {n: ([] if a.no_nt else shapes(lib)) + tn_shapes(lib) for n, lib in libs}
     times = {}
     for r in range(a.rounds):
         for n, _ in libs:
