@@ -222,8 +222,8 @@ def kernel_table(timing, rows_of, edges, H, agg, masked, s):
         if not name.startswith("sir_edge_agg"):
             kernels[name] = {"ms": round(t, 4), "launches": len(evs)}
             continue
-        if name == "sir_edge_agg_bwd":         # both backward passes in one launch
-            b = sum(edge_pass_bytes(n, rows_of(n), edges, H, agg, masked, s=s)
+        if name == "sir_edge_agg_bwd":         # both backward passes in one launch (MEAN: on G / deg)
+            b = sum(edge_pass_bytes(n, rows_of(n), edges, H, "sum" if agg == "mean" else agg, masked, s=s)
                     for n in ("sir_edge_agg_bwd_dst", "sir_edge_agg_bwd_src"))
         else:
             b = edge_pass_bytes(name, rows_of(name), edges, H, agg, masked, s=s)

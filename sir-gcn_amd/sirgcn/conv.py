@@ -121,10 +121,21 @@ def _slots(csr, H, device):
 
 def edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK):
     """dQ -> dQK[:, :H], dK -> dQK[:, H:] (the backward of ``update_all``, conv.py:45,63).  Sign-mask
-    mode with SUM / SYM runs both passes in one launch (``sir_edge_agg_bwd``); MEAN (the source
-    pass reads the destination pass's G / deg) and recompute mode run them one after the other."""
+    mode runs both passes in one launch (``sir_edge_agg_bwd``; MEAN on G / deg formed first);
+    recompute mode runs them one after the other (MEAN: the source pass reads the destination
+    pass's G / deg)."""
     in_norm, out_norm = plan.norms(agg)
-    if mask is not None and agg != "mean" and EdgeAggregate.dual:
+    if mask is not None and EdgeAggregate.dual:
+        if agg == "mean":
+            # both passes of MEAN read g = G / deg(v) (the reference's DivBackward, rounded once to
+            # the storage dtype): form it first, then the one-launch SUM backward on it is the MEAN
+            # backward (bit-identical to the two-launch form, which divides inside the dQ pass)
+            deg = getattr(plan, "_deg_f", None)
+            if deg is None:
+                rp = plan.dst.rowptr
+                deg = plan._deg_f = (rp[1:] - rp[:-1]).clamp(min=1).to(torch.float32)[:, None]
+            G = (G.float() / deg).to(G.dtype) if G.dtype != torch.float32 else G / deg
+            agg = "sum"
         _native.edge_agg_bwd(plan.dst, plan.src, G, mask, in_norm, out_norm, agg, act, slope, dQK[:, :H],
                              dQK[:, H:], _slots(plan.dst, H, G.device), _slots(plan.src, H, G.device))
         return

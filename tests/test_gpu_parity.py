@@ -646,10 +646,12 @@ def test_native_plan_build_batched_molecules_speed():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-@pytest.mark.parametrize("agg", ["sum", "sym"])
+@pytest.mark.parametrize("agg", ["sum", "sym", "mean"])
 @pytest.mark.parametrize("chunk", [256, 4])
 def test_one_launch_backward_bit_identical_to_two_passes(agg, dtype, chunk):
-    """sir_edge_agg_bwd (dQ pass || dK pass in one launch) == sir_edge_agg_bwd_dst + _src, bit for bit."""
+    """sir_edge_agg_bwd (dQ pass || dK pass in one launch; MEAN on G / deg formed first) ==
+    sir_edge_agg_bwd_dst + _src (MEAN: the dst pass divides and writes G / deg for the src pass),
+    bit for bit."""
     from sirgcn.conv import edge_backward
     gen = torch.Generator().manual_seed(21)
     V, E, H = 3000, 60000, 256
