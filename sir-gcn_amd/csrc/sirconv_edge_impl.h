@@ -1020,10 +1020,13 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
                                                            out_norm, in_norm, slope, H, dK, lddk, partial_s, nullptr, H);
 }
 
+#ifndef SIR_COMBINE_PF
+#define SIR_COMBINE_PF 4        // partial rows in flight per thread in k_combine (8: +0..1 %, rejected)
+#endif
 // Combine the partial rows of split rows (deterministic, no atomics).  One 1024-thread block
 // per split row: threads cover the row's columns (VW floats each); the remaining thread
-// dimension takes slices of the partial slots (slot s -> slice s % nslice, 4 loads in
-// flight); the slices are added in slice order through LDS.  MEAN_DIV divides by the degree.
+// dimension takes slices of the partial slots (slot s -> slice s % nslice, SIR_COMBINE_PF
+// loads in flight); the slices are added in slice order through LDS.  MEAN_DIV divides by the degree.
 template <int ST, bool MEAN_DIV, int VW>
 __global__ void __launch_bounds__(1024)
 k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
@@ -1044,12 +1047,12 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
         if (slice < nslice && c < HC) {
             const float* base = partial + (int64_t)sp.y * H + c * VW;
             int s = slice;
-            for (; s + 3 * nslice < sp.z; s += 4 * nslice) {
-                float v[4][VW];
+            for (; s + (SIR_COMBINE_PF - 1) * nslice < sp.z; s += SIR_COMBINE_PF * nslice) {
+                float v[SIR_COMBINE_PF][VW];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) vload<VW>(v[i], base + (int64_t)(s + i * nslice) * H);
+                for (int i = 0; i < SIR_COMBINE_PF; ++i) vload<VW>(v[i], base + (int64_t)(s + i * nslice) * H);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < SIR_COMBINE_PF; ++i)
 #pragma unroll
                     for (int w = 0; w < VW; ++w) acc[w] += v[i][w];
             }
