@@ -984,6 +984,9 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
                                               out, ldo, partial, Gm, ldgm);
 }
 
+#ifndef SIR_DUAL_PRIO
+#define SIR_DUAL_PRIO 0         // one-launch backward wave priority: 1 = dK waves first, 2 = dQ waves first
+#endif
 // Both sign-mask backward passes in ONE launch (SUM / SYM: the dK pass does not need the dQ pass's
 // Gm).  The dQ pass is VALU-bound (v_readlane + select + add per element and edge) and reads 32 B
 // per edge; the dK pass is HBM-bound (one gathered G row per edge).  Interleaving their waves
@@ -1012,6 +1015,11 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
         idx = nmin + (w - 2 * nmin);
         if (idx >= (dst ? n_items : n_items_s)) return;
     }
+#if SIR_DUAL_PRIO == 1
+    if (!dst) __builtin_amdgcn_s_setprio(1);       // dK waves (memory-bound) issue first
+#elif SIR_DUAL_PRIO == 2
+    if (dst) __builtin_amdgcn_s_setprio(1);        // dQ waves (VALU-bound) issue first
+#endif
     if (dst)
         mask_pass_item<ST, MODE_BWD_DST, ACT, AGG, NV, UD>(idx, rowptr, col, nullptr, items, G, ldg, mask, in_norm,
                                                            out_norm, slope, H, dQ, lddq, partial, nullptr, H);
