@@ -1112,7 +1112,7 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 #define SIR_UNROLL_DST_H 6
 #endif
 #ifndef SIR_UNROLL_SRC_H
-#define SIR_UNROLL_SRC_H 8
+#define SIR_UNROLL_SRC_H 4       // with the prefetched indices: one-launch bf16 backward 5.50 -> 4.86 ms (profiles/r02_ab_unroll_src.txt)
 #endif
 #if SIR_UNROLL_FWD > 16 || SIR_UNROLL_DST > 16 || SIR_UNROLL_SRC > 16 || SIR_UNROLL_FWD_H > 16 || \
     SIR_UNROLL_DST_H > 16 || SIR_UNROLL_SRC_H > 16
