@@ -1095,7 +1095,7 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 // Gathered rows in flight per wave for NV == 1 shapes, per pass (A/B-tuned on MI355X with
 // tools/edge_ab.py: more rows in flight per wave than this only adds cache pressure).
 #ifndef SIR_UNROLL_FWD
-#define SIR_UNROLL_FWD 4
+#define SIR_UNROLL_FWD 6         // with the buffer-load gathers + col prefetch: S2 forward 5.86 -> 5.61 ms (profiles/r02_ab_unroll_fwd.txt)
 #endif
 #ifndef SIR_UNROLL_DST
 #define SIR_UNROLL_DST 6
