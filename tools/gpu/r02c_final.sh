@@ -1,8 +1,8 @@
 # Round-2 (session 3) measurement set from one build on one box: bench lines (S2 headline with cpu_baseline,
 # S1, controls, BASELINE configs), rocprofv3 kernel-trace stats and PMC traffic for S2 and S1.
 set -o pipefail
-mkdir -p gpurun_out/final4
-O=gpurun_out/final4
+mkdir -p gpurun_out/final5
+O=gpurun_out/final5
 run() { name=$1; shift; timeout -k 10 420 python -u bench.py "$@" > $O/b_$name.json 2> $O/b_$name.err; r=$?; echo "$name rc=$r $(tail -c 300 $O/b_$name.json | tr -d '\n' | cut -c1-120)"; return $r; }
 run S2 --steps 20 --warmup 5 || exit $?
 run S1 --graph S1 --steps 20 --warmup 5 --no-cpu-baseline || exit $?
