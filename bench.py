@@ -207,12 +207,16 @@ def kernel_table(timing, rows_of, edges, H, agg, masked, s):
     kernels, gemm = {}, {}
     for name, evs in timing.items():
         t = sum(a.elapsed_time(b) for a, b, _ in evs) / len(evs)    # ms per launch
-        if name.startswith("sir_gemm_"):       # MFMA-bound projections: flops per launch
-            if name == "sir_gemm_pack":
+        if name.startswith("sir_gemm_"):       # MFMA-bound projections: flops (and HBM bytes) per launch
+            if name.startswith("sir_gemm_pack"):
                 continue
-            fl = sum(w for _, _, w in evs) / len(evs)
+            fl = sum(w[0] for _, _, w in evs) / len(evs)
+            by = sum(w[1] for _, _, w in evs) / len(evs)
             gemm[name] = {"ms": round(t, 4), "launches": len(evs), "flops": fl,
-                          "TFLOPs": round(fl / (t * 1e-3) / 1e12, 1)}
+                          "TFLOPs": round(fl / (t * 1e-3) / 1e12, 1), "hbm_bytes": by,
+                          "GBps": round(by / (t * 1e-3) / 1e9, 1),
+                          # fp16/bf16 MFMAs issued per product: 3 for the two-term split, 1 for 16-bit operands
+                          "mfma_per_product": 1 if name.endswith("16") else 3}
             continue
         if name == "sir_edge_mlp_fwd":         # fused per-edge dense layer: fp32 MFMA flops per launch
             fl = sum(w for _, _, w in evs) / len(evs)
@@ -232,7 +236,12 @@ def kernel_table(timing, rows_of, edges, H, agg, masked, s):
     return kernels, gemm
 
 
+STEP_MS = []       # per-step times (ms) of the last timed_loop, from HIP events between steps
+
+
 def timed_loop(step, steps, warmup, world, dist, dev):
+    """Time EXACTLY ``steps`` steps between barrier + synchronize; per-step HIP events on the
+    current stream (no host sync inside the loop) give the median beside the mean."""
     import torch
     from sirgcn import _native
     for _ in range(warmup):
@@ -241,15 +250,25 @@ def timed_loop(step, steps, warmup, world, dist, dev):
     if world > 1:
         dist.barrier()
     timing = _native.enable_timing(True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(steps):
+    evs[0].record()
+    for i in range(steps):
         step()
+        evs[i + 1].record()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     _native.enable_timing(False)
+    STEP_MS[:] = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
     return el, timing
+
+
+def median(xs):
+    xs = sorted(xs)
+    n = len(xs)
+    return (xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])) if n else None
 
 
 def max_over_ranks(x, world, dist, dev):
@@ -366,6 +385,8 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
     else:
         el, timing = timed_loop(step, args.steps, args.warmup, world, dist, dev)
     el = max_over_ranks(el, world, dist, dev if args.dist_backend == "nccl" and not rehearsal else "cpu")
+    med = None if rehearsal else max_over_ranks(median(STEP_MS), world, dist,
+                                                dev if args.dist_backend == "nccl" else "cpu")
     ms = 1e3 * el / args.steps
     out = {"metric": METRIC, "value": round(E / (el / args.steps), 1), "unit": "edges/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
@@ -382,6 +403,10 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
         out["n_gpus"] = world
         return out
 
+    # the median of the per-step HIP-event times; value / ms_per_step stay the mean over
+    # the bracketed K steps (the bench contract)
+    out["ms_per_step_median"] = round(med, 3)
+    out["value_median"] = round(E / (med * 1e-3), 1)
     from sirgcn.conv import EdgeAggregate
     s = SIZEOF[dtn]
     masked = bool(EdgeAggregate.use_mask and _native.mask_words(H, _native.ACT_LEAKY)) and args.agg != "max"
@@ -399,6 +424,7 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
     out["roofline"]["all_kernels"] = kernels
     if gemm:
         out["projections"] = projections(gemm, args.steps)
+    out["design_bytes_per_step"] = design_bytes(kernels, gemm, args.steps, ms)
     if dconv is not None:     # halo exchange volume per rank (rows of H), max over ranks
         ex = torch.tensor([dg.n_halo, int(dg.send_idx.numel()), edges_local], dtype=torch.float64,
                           device=dev if args.dist_backend == "nccl" else "cpu")
@@ -451,30 +477,48 @@ def roofline_fwd(args, kernels, V, E, V_src, H, s, world):
             traffic = rec["hbm_bytes_per_launch"]      # L2<->fabric bytes (Infinity-Cache hits included)
     except (OSError, ValueError):
         pass
-    frac = ach / HBM_PEAK_GBS
-    if frac > 1.0:   # algorithmic bytes charge every gathered row to HBM; hub rows hit the caches
-        frac_note = "algorithmic rate above the HBM peak: cache-served gathers (see frac_unique / frac_counter)"
-    else:
-        frac_note = None
+    frac_alg = ach / HBM_PEAK_GBS
+    # The physical figure is the HBM-side one: counter bytes (PMC FETCH_SIZE x2 + WRITE_SIZE, a
+    # separate profiled run of this build: profiles/pmc_traffic_<graph>.json) / this launch time.
+    # Without it, the algorithmic figure is reported as is — never capped: on power-law graphs the
+    # hub rows are served by L2 / Infinity Cache, so the algorithmic rate can exceed the HBM peak.
+    phys = traffic / t / 1e9 if traffic else None
     out = {"bound": "hbm", "kernel": "sir_edge_agg_fwd (k_edge<FWD> + k_combine)",
-           "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(min(frac, 1.0), 4),
+           "achieved": round(phys if phys else ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round((phys if phys else ach) / HBM_PEAK_GBS, 4),
+           "frac_basis": "counter (HBM-side bytes from PMC)" if phys else "algorithmic (no PMC file for this config)",
            "traffic": traffic, "algorithmic_bytes": alg, "ms_per_launch": k["ms"],
+           "achieved_algorithmic": round(ach, 1), "frac_algorithmic": round(frac_alg, 4),
            "bytes_formula": "SURVEY 8(d): E*(s_i + H*s) + V*(2*H*s + s_i)",
            "unique_bytes": uniq, "frac_unique": round(uniq / t / 1e9 / HBM_PEAK_GBS, 4),
-           "frac_counter": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4) if traffic else None}
-    if frac_note:
-        out["note"] = frac_note
+           "frac_counter": round(phys / HBM_PEAK_GBS, 4) if phys else None}
+    if frac_alg > 1.0:
+        out["note"] = "algorithmic rate above the HBM peak: cache-served gathers (see frac_unique / frac_counter)"
     return out
 
 
 def projections(gemm, steps):
+    """``fp16_mfma_util``: the 16-bit MFMA work actually issued (flops x MFMAs per product: 3 for the
+    split-fp16 fp32 kernels, 1 for the bf16 / fp16 kernels) / time / the dense fp16 peak."""
     fl = sum(g["flops"] * g["launches"] for g in gemm.values()) / steps
+    fl16 = sum(g["flops"] * g["launches"] * g["mfma_per_product"] for g in gemm.values()) / steps
+    by = sum(g["hbm_bytes"] * g["launches"] for g in gemm.values()) / steps
     tg = sum(g["ms"] * g["launches"] for g in gemm.values()) / steps
     return {"bound": "mfma", "ms_per_step": round(tg, 3), "flops_per_step": fl,
             "achieved_fp32_equiv_TFLOPs": round(fl / (tg * 1e-3) / 1e12, 1),
-            "fp16_mfma_util": round(3 * fl / (tg * 1e-3) / FP16_PEAK_FLOPS, 4),
+            "fp16_mfma_util": round(fl16 / (tg * 1e-3) / FP16_PEAK_FLOPS, 4),
             "vs_fp32_peak": round(fl / (tg * 1e-3) / (FP32_PEAK_TFLOPS * 1e12), 3),
+            "hbm_bytes_per_step": by, "hbm_frac": round(by / (tg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "kernels": gemm}
+
+
+def design_bytes(kernels, gemm, steps, ms):
+    """Bytes one step moves in THIS design: edge passes (incl. the sign mask) + the
+    projection GEMMs' A, B and C; ÷ the step time = the whole step's HBM rate."""
+    e = sum(k.get("design_bytes", 0) * k["launches"] for k in kernels.values()) / steps
+    g = sum(k["hbm_bytes"] * k["launches"] for k in gemm.values()) / steps
+    return {"edge_passes": e, "projections": g, "total": e + g,
+            "GBps_over_step": round((e + g) / (ms * 1e-3) / 1e9, 1)}
 
 
 def run_stack(args, world, rank, dev, torch, dist):
@@ -528,6 +572,7 @@ def run_stack(args, world, rank, dev, torch, dist):
     else:
         el, timing = timed_loop(step, args.steps, args.warmup, world, dist, dev)
     el = max_over_ranks(el, world, dist, dev)
+    med = max_over_ranks(median(STEP_MS), world, dist, dev)
     L, H, E, V = c["layers"], c["hidden"], g.num_edges(), g.num_nodes()
     tot = torch.tensor([E, V, g.batch_size], dtype=torch.float64, device=dev)
     if world > 1:
@@ -546,7 +591,7 @@ def run_stack(args, world, rank, dev, torch, dist):
                                   f"{' per rank, DDP over RCCL' if world > 1 else ''}",
                       "graphs_per_s": round(B_all / (el / args.steps), 1), "V_total": V_all, "E_total": E_all,
                       "parallelism": f"data-parallel x{world}" if world > 1 else "single GPU"},
-           "kernels": kernels, "hip_graph": captured is not None}
+           "ms_per_step_median": round(med, 3), "kernels": kernels, "hip_graph": captured is not None}
     if captured is not None:
         out["kernels_note"] = "per-kernel times from 3 eager steps; value / ms_per_step from the replayed HIP graph"
     if gemm:

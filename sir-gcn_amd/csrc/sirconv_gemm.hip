@@ -486,6 +486,9 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #define SIR_NT_P_EPI 1          // persistent NT epilogue through LDS with whole-row stores (1) or fragment stores (0)
 #endif
 constexpr int NT_P_NMAX = 512;
+#ifndef SIR_NT_W_MINROWS
+#define SIR_NT_W_MINROWS 0      // fewest rows for the weight-resident kernel (sirconv_gemm_w.hip)
+#endif
 
 template <int NCT>
 __global__ void __launch_bounds__(512)
@@ -1121,9 +1124,14 @@ k_gemm_reduce(const float* __restrict__ part, int P, int64_t count, int Nc, floa
 }  // namespace
 
 int64_t gemm_pack_npad(int64_t N) { return (N + 255) / 256 * 256; }
-int64_t gemm_pack_bytes(int64_t N, int64_t K) {
+// the packed weight holds the k_gemm_nt / k_gemm_nt_p image and, for the shapes the
+// weight-resident kernel takes (sirconv_gemm_w.hip), its slice images after it (16-B aligned)
+static int64_t gemm_pack_base_bytes(int64_t N, int64_t K) {
     const int64_t np = gemm_pack_npad(N), kc = (K + KC - 1) / KC;
-    return kc * 4 * np * 32 + np * 4;
+    return (kc * 4 * np * 32 + np * 4 + 15) / 16 * 16;
+}
+int64_t gemm_pack_bytes(int64_t N, int64_t K) {
+    return gemm_pack_base_bytes(N, K) + gemm_pack_w_bytes((int)N, (int)K);
 }
 
 hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st) {
@@ -1131,6 +1139,11 @@ hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, v
     _Float16* out = static_cast<_Float16*>(packed);
     float* inv = reinterpret_cast<float*>(static_cast<char*>(packed) + (int64_t)kc * 4 * np * 32);
     hipLaunchKernelGGL(k_pack_weight, dim3(np), dim3(64), 0, st, W, ldw, N, K, trans, np, kc, out, inv);
+    if (gemm_nt_w_ok(N, K)) {
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return run_gemm_pack_w(W, ldw, N, K, trans, static_cast<char*>(packed) + gemm_pack_base_bytes(N, K), st);
+    }
     return hipGetLastError();
 }
 
@@ -1141,6 +1154,9 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     const u4v* wp = static_cast<const u4v*>(packed);
     const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
     const bool kfull = K % KC == 0;
+    if (gemm_nt_w_ok(N, K) && M >= SIR_NT_W_MINROWS)
+        return run_gemm_nt_w(A, lda, M, K, static_cast<const char*>(packed) + gemm_pack_base_bytes(N, K), N, bias, C,
+                             ldc, st);
     if (SIR_NT_PERSIST && N > 128 && np <= NT_P_NMAX && kfull && (kc == 4 || kc == 8 || kc == 16)) {
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;

@@ -82,7 +82,8 @@ def enable_timing(on=True):
 
 
 class _Timed:
-    """Records (start, end, work) on the launching stream; ``work`` = flops for the GEMMs."""
+    """Records (start, end, work) on the launching stream; ``work`` = (flops, algorithmic HBM bytes)
+    for the GEMMs (A, B read once, C written once; the packed weights are L2-resident)."""
     __slots__ = ("name", "dev", "ev", "work")
 
     def __init__(self, name, dev, work=0):
@@ -363,7 +364,7 @@ def gemm_nt(A, packed, bias=None, out=None):
     assert A.dim() == 2 and A.shape[1] == K and A.stride(1) == 1
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    with _Timed("sir_gemm_nt", A.device, 2 * M * N * K):
+    with _Timed("sir_gemm_nt", A.device, (2 * M * N * K, 4 * M * (K + N))):
         rc = lib.sir_gemm_nt(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(bias), _ptr(out), out.stride(0),
                              _stream(A.device))
     _check(rc, lib)
@@ -383,7 +384,7 @@ def gemm_tn(A, B, out=None, colsum=False):
     cs = torch.empty((M,), dtype=torch.float32, device=A.device) if colsum else None
     ws_bytes = lib.sir_gemm_tn_workspace(R, M, N)
     ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=A.device)
-    with _Timed("sir_gemm_tn", A.device, 2 * R * M * N):
+    with _Timed("sir_gemm_tn", A.device, (2 * R * M * N, 4 * R * (M + N))):
         rc = lib.sir_gemm_tn(_ptr(A), A.stride(0), _ptr(B), B.stride(0), R, M, N, _ptr(out), out.stride(0),
                              _ptr(cs), _ptr(ws), ws.numel(), _stream(A.device))
     _check(rc, lib)
@@ -406,7 +407,7 @@ def gemm_tn16(A, B, out=None, colsum=False):
     cs = torch.empty((M,), dtype=torch.float32, device=A.device) if colsum else None
     ws_bytes = lib.sir_gemm_tn_workspace(R, M, N)
     ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=A.device)
-    with _Timed("sir_gemm_tn16", A.device, 2 * R * M * N):
+    with _Timed("sir_gemm_tn16", A.device, (2 * R * M * N, A.element_size() * R * (M + N))):
         rc = lib.sir_gemm_tn16(_ptr(A), A.stride(0), _ptr(B), B.stride(0), R, M, N, _DT16[A.dtype], _ptr(out),
                                out.stride(0), _ptr(cs), _ptr(ws), ws.numel(), _stream(A.device))
     _check(rc, lib)
@@ -443,7 +444,8 @@ def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None):
     out = torch.empty((M, N), dtype=od, device=A.device)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
-    with _Timed("sir_gemm_nt16", A.device, 2 * M * N * K):
+    with _Timed("sir_gemm_nt16", A.device, (2 * M * N * K, A.element_size() * M * K + out.element_size() * M * N
+                                            + (acopy.element_size() * M * K if acopy is not None else 0))):
         rc = lib.sir_gemm_nt16(_ptr(A), A.stride(0), STORAGE[A.dtype], M, K, _ptr(pk), N, _DT16[dt], _ptr(bias),
                                _ptr(out), out.stride(0), STORAGE[od], _ptr(acopy),
                                acopy.stride(0) if acopy is not None else 0, _stream(A.device))

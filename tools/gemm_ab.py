@@ -63,7 +63,8 @@ def main():
         "dW  tn": (D2, X),
     }
     if a.only:
-        shapes = {k: v for k, v in shapes.items() if k.startswith(a.only)}
+        pre = a.only.split(",")
+        shapes = {k: v for k, v in shapes.items() if any(k.startswith(x) for x in pre)}
     packs = {(n, s): pack(lib, v[1], v[2]) for n, lib in libs for s, v in shapes.items() if len(v) == 4}
     outs = {}
     ws = torch.empty(max(lib.sir_gemm_tn_workspace(V, 2 * H, H) for _, lib in libs), dtype=torch.uint8, device=dev)
