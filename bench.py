@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--dtype", default=None, choices=["f32", "bf16", "f16"],
                     help="feature dtype (16-bit = the autocast path); default f32 (cfg2: bf16)")
     ap.add_argument("--chunk", type=int, default=None)
+    ap.add_argument("--dropout", type=float, default=None,
+                    help="SIRConv feat_dropout (Q/K dropout, conv.py:60-61) in training mode; default: 0 for cfg4, "
+                         "the reference's trained value for the stack workloads (cfg3 / cfg5: 0.2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-graph", default="S1", help="graph of the reference CPU dataflow baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat CPU baseline steps until this long")
@@ -335,7 +338,8 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
     src, dst = powerlaw_edges(V, E, alpha, seed=0)
 
     torch.manual_seed(4)
-    conv = SIRConv(H, H, H, nn.LeakyReLU(0.2, inplace=True), 0, agg_type=args.agg).to(dev)
+    p_drop = args.dropout or 0.0
+    conv = SIRConv(H, H, H, nn.LeakyReLU(0.2, inplace=True), p_drop, agg_type=args.agg).to(dev)
     if args.chunk:
         conv.chunk = args.chunk
     X_full = torch.randn(V, H, generator=torch.Generator().manual_seed(3))
@@ -392,7 +396,7 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
            "scaling": "strong", "vs_baseline": None, "dtype": dtn, "data": "synthetic",
            "config": {"workload": f"cfg4 {args.graph}: Chung-Lu power-law V={V} E={E} alpha={alpha}; 1 SIRConv layer "
-                                  f"d_in=H=d_out={H}, agg={args.agg}, LeakyReLU(0.2), {dtn}"
+                                  f"d_in=H=d_out={H}, agg={args.agg}, LeakyReLU(0.2), {dtn}, feat_dropout={p_drop}"
                                   f"{' (autocast)' if dtn != 'f32' else ''}; fwd+bwd incl. projections",
                       "graph": args.graph, "V": V, "E": E, "hidden": H, "agg": args.agg,
                       "parallelism": f"edge-cut dst-range x{world}, sparse halo all-to-all" if world > 1
@@ -532,7 +536,8 @@ def run_stack(args, world, rank, dev, torch, dist):
     if world > 1 and name != "cfg5":
         raise SystemExit(f"{name} is a single-GPU workload (cfg5 is the data-parallel one, cfg4 the edge-cut)")
     g = make_graph(name, rank=rank)
-    stack = make_stack(name, SIRConv, GraphNorm).to(dev)
+    p_drop = c["feat_dropout"] if args.dropout is None else args.dropout
+    stack = make_stack(name, SIRConv, GraphNorm, feat_dropout=p_drop).to(dev)
     model = stack
     if world > 1:           # DP replicas: a different batch per rank, RCCL gradient all-reduce
         model = torch.nn.parallel.DistributedDataParallel(stack, device_ids=[dev.index])
@@ -587,7 +592,7 @@ def run_stack(args, world, rank, dev, torch, dist):
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
            "higher_is_better": True, "scaling": "weak" if name == "cfg5" else "strong", "vs_baseline": None,
            "dtype": dtn, "data": "synthetic",
-           "config": {"workload": f"{name}: {CONFIGS[name]} V={V} E={E} graphs={g.batch_size}"
+           "config": {"workload": f"{name}: {dict(CONFIGS[name], feat_dropout=p_drop)} V={V} E={E} graphs={g.batch_size}"
                                   f"{' per rank, DDP over RCCL' if world > 1 else ''}",
                       "graphs_per_s": round(B_all / (el / args.steps), 1), "V_total": V_all, "E_total": E_all,
                       "parallelism": f"data-parallel x{world}" if world > 1 else "single GPU"},

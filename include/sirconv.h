@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 7
+#define SIR_ABI_VERSION 8
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -56,6 +56,27 @@ enum { SIR_OK = 0, SIR_EINVAL = 1, SIR_EUNSUPPORTED = 2, SIR_ELAUNCH = 3 };
 
 int sir_abi_version(void);
 const char* sir_last_error(void);
+
+/*
+ * Feature dropout on Q and K — conv.py:35,60-61: K = Dropout(p)(X W_K^T), Q = Dropout(p)(X W_Q^T + b_Q),
+ * two independent nn.Dropout masks (the reference trains with p = 0.1-0.2, e.g. ogbn-arxiv/train.py:303).
+ * Element (row, col) of QK = [Q | K] (col < H: Q, col >= H: K) is kept iff a counter-based hash of
+ * (seed, row, col) is >= round(p * 2^32); kept elements are scaled by 1 / (1 - p) (fp32).  No mask
+ * is stored: the QK GEMM applies it to its output (sir_gemm_nt / sir_gemm_nt16, C column = QK
+ * column), the backward edge passes apply the same bits to dQ (columns 0..H-1) and dK (H..2H-1)
+ * before storing them — the dropout's backward (grad * mask * scale).  16-bit outputs scale the value
+ * rounded to the 16-bit type and round again (the reference's Dropout of a half-precision tensor).
+ * A NULL pointer, or p <= 0, means no dropout; p >= 1 drops everything.
+ */
+typedef struct {
+    uint64_t seed;
+    double p;
+} sir_dropout_t;
+
+/* In place: X[m][n] = keep(m, col0 + n) ? X[m][n] * scale : 0 for an [M, N] block of QK (ldx
+ * elements per row, dtype SIR_DTYPE_*) — the forward dropout of a QK computed by another GEMM. */
+int sir_dropout_apply(void* X, int64_t ldx, int64_t M, int64_t N, int dtype, int64_t col0,
+                      const sir_dropout_t* drop, void* stream);
 
 /*
  * Per-edge sign-mask size (64-bit words) for hidden size H and activation `act`, or 0 when
@@ -124,7 +145,7 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
                          void* dQ, int64_t lddq, void* Gm, int64_t ldgm,
-                         float* partial, void* stream);
+                         float* partial, const sir_dropout_t* drop, void* stream);
 
 /*
  * Backward, source pass — the K half (replaces the index_add of conv.py:45's src gather).
@@ -144,7 +165,7 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          const void* Gd, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
-                         void* dK, int64_t lddk, float* partial, void* stream);
+                         void* dK, int64_t lddk, float* partial, const sir_dropout_t* drop, void* stream);
 
 /*
  * Both backward passes in ONE launch — sign-mask mode, SUM or SYM (MEAN's source pass needs the
@@ -162,7 +183,7 @@ int sir_edge_agg_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
                      int64_t H, int dtype, const uint64_t* mask, const void* G, int64_t ldg,
                      const float* in_norm, const float* out_norm, int agg, int act, float slope,
                      void* dQ, int64_t lddq, void* dK, int64_t lddk, float* partial, float* partial_s,
-                     void* stream);
+                     const sir_dropout_t* drop, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Edge-materialised path: agg_type='max' (conv.py:46-47 + DGL max reduce) and sigma callables the
@@ -316,7 +337,7 @@ int sir_gemm_pack(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, 
 /* C[M, N] = A[M, K] B^T + bias  (bias [N] or NULL).  A, C row-major; K, N, lda, ldc multiples of
  * 4; A, C, bias 16-B aligned.  Replaces addmm(b, X, W^T) / mm(X, W). */
 int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
-                const float* bias, float* C, int64_t ldc, void* stream);
+                const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream);
 
 /* C[M, N] = A^T B with A [R, M] (lda), B [R, N] (ldb): the weight gradients (contraction over the
  * R node rows, split over row ranges; the partial products are added in a fixed order, so the
@@ -353,7 +374,7 @@ int64_t sir_gemm_pack16_bytes(int64_t N, int64_t K);
 int sir_gemm_pack16(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, int dtype, void* packed, void* stream);
 int sir_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int64_t K, const void* packed, int64_t N,
                   int dtype, const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac,
-                  void* stream);
+                  const sir_dropout_t* drop, void* stream);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,12 @@ int check_mask(const char* fn, int64_t H, int act) {
     return SIR_OK;
 }
 
+// the kernels' Drop of an ABI dropout argument (NULL / p <= 0: none); col0 = first QK column written
+sir::Drop to_drop(const sir_dropout_t* d, int64_t col0) {
+    if (d == nullptr || !(d->p > 0.0)) return sir::Drop();
+    return sir::make_drop(d->p, d->seed, (int)col0);
+}
+
 int finish(const char* fn, hipError_t err, const char* why) {
     if (err == hipSuccess) return SIR_OK;
     if (err == hipErrorInvalidValue && why) return fail(SIR_EUNSUPPORTED, fn, why);
@@ -132,7 +138,7 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
                          void* dQ, int64_t lddq, void* Gm, int64_t ldgm,
-                         float* partial, void* stream) {
+                         float* partial, const sir_dropout_t* drop, void* stream) {
     const char* fn = "sir_edge_agg_bwd_dst";
     int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, dQ, partial);
@@ -155,6 +161,7 @@ int sir_edge_agg_bwd_dst(const int32_t* rowptr, const int32_t* col,
     a.out = dQ; a.ldo = lddq; a.partial = partial;
     a.Gm = (agg == SIR_AGG_MEAN) ? Gm : nullptr; a.ldgm = Gm ? ldgm : H;
     a.mask_in = mask;
+    a.drop = to_drop(drop, 0);              // dQ = QK columns 0 .. H-1
     const char* why = nullptr;
     hipError_t err = sir::run_edge(sir::MODE_BWD_DST, dtype, a, agg, act, splits, n_splits, dQ, lddq, false,
                                    static_cast<hipStream_t>(stream), &why);
@@ -170,7 +177,7 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          const void* Gd, int64_t ldg,
                          const float* norm_row, const float* norm_col,
                          int agg, int act, float slope,
-                         void* dK, int64_t lddk, float* partial, void* stream) {
+                         void* dK, int64_t lddk, float* partial, const sir_dropout_t* drop, void* stream) {
     const char* fn = "sir_edge_agg_bwd_src";
     int rc = check_common(fn, rowptr_s, col_s, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, dK, partial);
@@ -192,6 +199,7 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = dK; a.ldo = lddk; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
     a.mask_in = mask; a.perm = perm_s;
+    a.drop = to_drop(drop, H);              // dK = QK columns H .. 2H-1
     const char* why = nullptr;
     hipError_t err = sir::run_edge(sir::MODE_BWD_SRC, dtype, a, agg, act, splits, n_splits, dK, lddk, false,
                                    static_cast<hipStream_t>(stream), &why);
@@ -205,7 +213,7 @@ int sir_edge_agg_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
                      int64_t H, int dtype, const uint64_t* mask, const void* G, int64_t ldg,
                      const float* in_norm, const float* out_norm, int agg, int act, float slope,
                      void* dQ, int64_t lddq, void* dK, int64_t lddk, float* partial, float* partial_s,
-                     void* stream) {
+                     const sir_dropout_t* drop, void* stream) {
     const char* fn = "sir_edge_agg_bwd";
     int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act, in_norm, out_norm,
                           dQ, partial);
@@ -230,6 +238,8 @@ int sir_edge_agg_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
     b.rowptr = rowptr_s; b.col = col_s; b.perm = perm_s; b.items = items_s; b.n_items = n_items_s;
     b.G = G; b.ldg = ldg; b.norm_row = out_norm; b.norm_col = in_norm; b.slope = slope; b.H = (int)H;
     b.out = dK; b.ldo = lddk; b.partial = partial_s; b.mask_in = mask; b.ldr = H; b.ldc = H; b.ldgm = H;
+    a.drop = to_drop(drop, 0);
+    b.drop = to_drop(drop, H);
     const char* why = nullptr;
     hipError_t err = sir::run_edge_dual(dtype, a, splits, n_splits, b, splits_s, n_splits_s, agg, act,
                                         static_cast<hipStream_t>(stream), &why);
@@ -499,7 +509,7 @@ int sir_gemm_pack(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, 
 }
 
 int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
-                const float* bias, float* C, int64_t ldc, void* stream) {
+                const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream) {
     const char* fn = "sir_gemm_nt";
     if (M < 0 || N <= 0 || K <= 0 || N > 65536 || K > 65536) return fail(SIR_EINVAL, fn, "bad shape");
     if ((M + 255) / 256 * ((N + 127) / 128) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
@@ -511,7 +521,8 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
     if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(bias) |
           reinterpret_cast<uintptr_t>(packed)) & 15u) != 0)
         return fail(SIR_EINVAL, fn, "A, C, bias and packed must be 16-B aligned");
-    hipError_t err = sir::run_gemm_nt(A, lda, M, (int)K, packed, (int)N, bias, C, ldc, static_cast<hipStream_t>(stream));
+    hipError_t err = sir::run_gemm_nt(A, lda, M, (int)K, packed, (int)N, bias, C, ldc, static_cast<hipStream_t>(stream),
+                                      to_drop(drop, 0));
     return finish(fn, err, nullptr);
 }
 
@@ -574,7 +585,7 @@ int sir_gemm_pack16(const float* W, int64_t ldw, int64_t N, int64_t K, int trans
 
 int sir_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int64_t K, const void* packed, int64_t N,
                   int dtype, const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac,
-                  void* stream) {
+                  const sir_dropout_t* drop, void* stream) {
     const char* fn = "sir_gemm_nt16";
     if (dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "dtype must be BF16 or F16");
     if (a_dtype != dtype && a_dtype != SIR_DTYPE_F32) return fail(SIR_EINVAL, fn, "a_dtype must be dtype or F32");
@@ -593,8 +604,20 @@ int sir_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int64_t K,
           reinterpret_cast<uintptr_t>(packed)) & 15u) != 0)
         return fail(SIR_EINVAL, fn, "A, C, Acopy and packed must be 16-B aligned");
     hipError_t err = sir::run_gemm_nt16(A, lda, a_dtype, M, (int)K, packed, (int)N, dtype, bias, C, ldc, c_dtype, Acopy,
-                                        ldac, static_cast<hipStream_t>(stream));
+                                        ldac, static_cast<hipStream_t>(stream), to_drop(drop, 0));
     return finish(fn, err, nullptr);
+}
+
+int sir_dropout_apply(void* X, int64_t ldx, int64_t M, int64_t N, int dtype, int64_t col0,
+                      const sir_dropout_t* drop, void* stream) {
+    const char* fn = "sir_dropout_apply";
+    if (dtype != SIR_DTYPE_F32 && dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16)
+        return fail(SIR_EINVAL, fn, "dtype must be SIR_DTYPE_F32, _BF16 or _F16");
+    if (M < 0 || N < 0 || N > (1 << 24) || M > INT32_MAX || ldx < N || col0 < 0 || col0 > (1 << 24))
+        return fail(SIR_EINVAL, fn, "bad shape");
+    if (M > 0 && N > 0 && X == nullptr) return fail(SIR_EINVAL, fn, "NULL X");
+    return finish(fn, sir::run_dropout_apply(X, ldx, M, (int)N, dtype, to_drop(drop, col0), static_cast<hipStream_t>(stream)),
+                  nullptr);
 }
 
 }  // extern "C"

@@ -104,15 +104,15 @@ hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, fl
 
 template <int ST, bool MEAN_DIV>
 static hipError_t launch_combine(const int32_t* splits, int64_t n, const float* partial, int H,
-                                 void* out, int64_t ldo, int vw, hipStream_t st) {
+                                 void* out, int64_t ldo, int vw, hipStream_t st, const Drop& drop) {
     if (n == 0) return hipSuccess;
     TP<ST>* o = static_cast<TP<ST>*>(out);
     if (vw == 4)
         hipLaunchKernelGGL((k_combine<ST, MEAN_DIV, 4>), dim3((unsigned)n), dim3(1024), 0, st,
-                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo);
+                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo, drop);
     else
         hipLaunchKernelGGL((k_combine<ST, MEAN_DIV, 1>), dim3((unsigned)n), dim3(1024), 0, st,
-                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo);
+                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo, drop);
     return hipGetLastError();
 }
 
@@ -127,8 +127,8 @@ static hipError_t run_edge_t(int mode, const EdgeArgs& a, int agg, int act, Shap
         default: err = launch_edge_pass<ST, MODE_BWD_SRC>(a, agg, act, s, st); break;
     }
     if (err != hipSuccess || n_splits == 0) return err;
-    return mean_div ? launch_combine<ST, true>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st)
-                    : launch_combine<ST, false>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st);
+    return mean_div ? launch_combine<ST, true>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st, a.drop)
+                    : launch_combine<ST, false>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st, a.drop);
 }
 
 hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
@@ -212,9 +212,9 @@ hipError_t run_edge_dual(int dtype, const EdgeArgs& a, const int32_t* splits, in
     auto combine = [&](const int32_t* sp, int64_t n, const EdgeArgs& x) -> hipError_t {
         if (n == 0) return hipSuccess;
         switch (dtype) {
-            case ST_BF16: return launch_combine<ST_BF16, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st);
-            case ST_F16: return launch_combine<ST_F16, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st);
-            default: return launch_combine<ST_F32, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st);
+            case ST_BF16: return launch_combine<ST_BF16, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st, x.drop);
+            case ST_F16: return launch_combine<ST_F16, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st, x.drop);
+            default: return launch_combine<ST_F32, false>(sp, n, x.partial, x.H, x.out, x.ldo, 4, st, x.drop);
         }
     };
     if ((err = combine(splits, n_splits, a)) != hipSuccess) return err;

@@ -108,6 +108,16 @@ __device__ __forceinline__ float round_st(float x) {
     else return h2f<ST>(f2h<ST>(x));
 }
 
+// backward of the feature dropout on Q / K (sirconv_dropout.h): row `row`, features c0 .. c0+VW-1 of
+// dQ (drop.col0 = 0) or dK (drop.col0 = H); 16-bit storage scales the value rounded to it (the
+// reference's grad is the half-precision tensor), the store rounds again
+template <int ST, int VW>
+__device__ __forceinline__ void drop_vec(const Drop& d, int64_t row, int c0, float (&v)[VW]) {
+    const uint32_t rh = drop_row_hash(d, row);
+#pragma unroll
+    for (int w = 0; w < VW; ++w) v[w] = drop_keep(d, rh, d.col0 + c0 + w) ? round_st<ST>(v[w]) * d.scale : 0.f;
+}
+
 // ------------------------------------------------------------------------------ vectors
 // Cache-policy experiment knobs (tools/edge_ab.py builds them as separate libraries):
 //   SIR_NT_STREAM = 1: non-temporal loads/stores for the once-touched row-side streams
@@ -383,7 +393,7 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
        const float* __restrict__ norm_row, const float* __restrict__ norm_col,
        float slope, int H,
        typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-       typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask) {
+       typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask, Drop drop) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LPR;
@@ -497,6 +507,12 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
                 for (int w = 0; w < VW; ++w) acc[j][w] = acc[j][w] / degf;
         }
         auto* op = out + (int64_t)row * ldo;
+        if constexpr (MODE != MODE_FWD) {
+            if (drop.on()) {
+#pragma unroll
+                for (int j = 0; j < NV; ++j) drop_vec<ST, VW>(drop, row, (li + LPR * j) * VW, acc[j]);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = li + LPR * j;
@@ -909,7 +925,7 @@ mask_pass_item(int64_t wave, const int* __restrict__ rowptr, const int* __restri
                const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
                const float* __restrict__ norm_row, const float* __restrict__ norm_col,
                float slope, int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-               typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm) {
+               typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, const Drop& drop) {
     const int lane = threadIdx.x & 63;
     const int4 it = uniform_item(items, wave);
     const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
@@ -955,6 +971,10 @@ mask_pass_item(int64_t wave, const int* __restrict__ rowptr, const int* __restri
         mask_item<ST, MODE, ACT, AGG, NV, U>(e0, e1, col, perm, G, ldg, mask, norm_col, nr, slope, lane, HC, gv, acc);
     if (slot < 0) {
         auto* op = out + (int64_t)row * ldo;
+        if (drop.on()) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) drop_vec<ST, 4>(drop, row, (lane + 64 * j) * 4, acc[j]);
+        }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int c = lane + 64 * j;
@@ -977,11 +997,11 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
             const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
             const float* __restrict__ norm_row, const float* __restrict__ norm_col,
             float slope, int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-            typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm) {
+            typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, Drop drop) {
     const int64_t wave = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     if (wave >= n_items) return;
     mask_pass_item<ST, MODE, ACT, AGG, NV, U>(wave, rowptr, col, perm, items, G, ldg, mask, norm_row, norm_col, slope, H,
-                                              out, ldo, partial, Gm, ldgm);
+                                              out, ldo, partial, Gm, ldgm, drop);
 }
 
 #ifndef SIR_DUAL_PRIO
@@ -1002,7 +1022,8 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
                  const int4* __restrict__ items_s, int64_t n_items_s, float* __restrict__ partial_s,
                  typename Stor<ST>::T* __restrict__ dK, int64_t lddk,
                  const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
-                 const float* __restrict__ in_norm, const float* __restrict__ out_norm, float slope, int H) {
+                 const float* __restrict__ in_norm, const float* __restrict__ out_norm, float slope, int H,
+                 Drop drop_q, Drop drop_k) {
     const int64_t w = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int64_t nmin = n_items < n_items_s ? n_items : n_items_s;
     bool dst;
@@ -1022,10 +1043,11 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
 #endif
     if (dst)
         mask_pass_item<ST, MODE_BWD_DST, ACT, AGG, NV, UD>(idx, rowptr, col, nullptr, items, G, ldg, mask, in_norm,
-                                                           out_norm, slope, H, dQ, lddq, partial, nullptr, H);
+                                                           out_norm, slope, H, dQ, lddq, partial, nullptr, H, drop_q);
     else
         mask_pass_item<ST, MODE_BWD_SRC, ACT, AGG, NV, US>(idx, rowptr_s, col_s, perm_s, items_s, G, ldg, mask,
-                                                           out_norm, in_norm, slope, H, dK, lddk, partial_s, nullptr, H);
+                                                           out_norm, in_norm, slope, H, dK, lddk, partial_s, nullptr, H,
+                                                           drop_k);
 }
 
 #ifndef SIR_COMBINE_PF
@@ -1038,7 +1060,7 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
 template <int ST, bool MEAN_DIV, int VW>
 __global__ void __launch_bounds__(1024)
 k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
-          int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo) {
+          int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, Drop drop) {
     __shared__ float red[1024 * VW];
     const int4 sp = splits[blockIdx.x];
     const int HC = H / VW;
@@ -1085,6 +1107,7 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
 #pragma unroll
                 for (int w = 0; w < VW; ++w) r[w] = r[w] / degf;
             }
+            if (drop.on()) drop_vec<ST, VW>(drop, sp.x, c * VW, r);      // backward passes only (host)
             tstore_p<ST, VW, false>(out + (int64_t)sp.x * ldo + c * VW, r);
         }
         __syncthreads();
@@ -1144,7 +1167,7 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
             hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, true>), dim3((unsigned)blocks), dim3(256), 0, st,
                                a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
                                cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
-                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out);
+                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out, a.drop);
             return hipGetLastError();
         }
     } else {
@@ -1153,7 +1176,7 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, false>), dim3((unsigned)blocks), dim3(256), 0, st,
                        a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
                        cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
-                       a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr);
+                       a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr, a.drop);
     return hipGetLastError();
 }
 
@@ -1165,7 +1188,7 @@ static hipError_t launch_mask_t(const EdgeArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_edge_mask<ST, MODE, ACT, AGG, NV, U>), dim3((unsigned)blocks), dim3(256), 0, st,
                        a.rowptr, a.col, a.perm, reinterpret_cast<const int4*>(a.items), a.n_items,
                        cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H,
-                       mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm);
+                       mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.drop);
     return hipGetLastError();
 }
 
@@ -1180,7 +1203,8 @@ static hipError_t launch_dual_t(const EdgeArgs& a, const EdgeArgs& b, hipStream_
                        a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items, a.partial,
                        mp_<ST>(a.out), a.ldo,
                        b.rowptr, b.col, b.perm, reinterpret_cast<const int4*>(b.items), b.n_items, b.partial,
-                       mp_<ST>(b.out), b.ldo, cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H);
+                       mp_<ST>(b.out), b.ldo, cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H,
+                       a.drop, b.drop);
     return hipGetLastError();
 }
 

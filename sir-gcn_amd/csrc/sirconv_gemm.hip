@@ -32,6 +32,7 @@
 
 #include "sirconv_internal.h"
 #include "sirconv_gemm_util.h"
+#include "sirconv_dropout.h"
 
 namespace sir {
 namespace {
@@ -84,6 +85,15 @@ __device__ inline int next_se(int se_old, int e_c) {
     return s > 126 ? 126 : s;
 }
 __device__ inline float pow2(int e) { e = e < -126 ? -126 : (e > 127 ? 127 : e); return __uint_as_float((uint32_t)(e + 127) << 23); }
+// feature dropout of QK (sirconv_dropout.h) on 4 consecutive output columns n .. n+3 of one row
+__device__ inline void drop4(const Drop& d, int64_t row, int n, float4& o) {
+    const uint32_t rh = drop_row_hash(d, row);
+    const int c = d.col0 + n;
+    o.x = drop_keep(d, rh, c + 0) ? o.x * d.scale : 0.f;
+    o.y = drop_keep(d, rh, c + 1) ? o.y * d.scale : 0.f;
+    o.z = drop_keep(d, rh, c + 2) ? o.z * d.scale : 0.f;
+    o.w = drop_keep(d, rh, c + 3) ? o.w * d.scale : 0.f;
+}
 
 // hi/lo fp16 split of 8 floats scaled by s (exact power of two)
 #define SIR_SPLIT1(x, i) { const float y_ = (x) * s; const _Float16 h_ = (_Float16)y_; hi[i] = h_; lo[i] = (_Float16)(y_ - (float)h_); }
@@ -133,7 +143,7 @@ template <int WD, int WF, int TDT, int TFT, bool KFULL>
 __global__ void __launch_bounds__(64 * WD * WF)
 k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
           const u4v* __restrict__ Wp, int Npad, const float* __restrict__ inv_t,
-          const float* __restrict__ bias, int N, float* __restrict__ C, int64_t ldc, int n_ftiles) {
+          const float* __restrict__ bias, int N, float* __restrict__ C, int64_t ldc, int n_ftiles, Drop drop) {
     constexpr int NT = 64 * WD * WF;
     constexpr int BD = 32 * TDT * WD;        // data rows per block
     constexpr int BF = 32 * TFT * WF;        // features per block
@@ -375,6 +385,9 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #endif
 
     // epilogue: C[m][n] = acc * 2^-se(m) * inv_t[n] + bias[n]
+#if SIR_NT_EPI != 1
+#error "the fragment-store NT epilogue has no dropout"
+#endif
 #if SIR_NT_EPI == 1
     // Through LDS, one 32-row band of every wave per round: the waves write their scaled float4
     // fragments into a row-major image (row pitch BF*4 + 16 B: conflict-free ds_write_b128), then
@@ -408,6 +421,7 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
                     const float4 bb = *reinterpret_cast<const float4*>(bias + n);
                     o.x += bb.x; o.y += bb.y; o.z += bb.z; o.w += bb.w;
                 }
+                if (drop.on()) drop4(drop, d0 + dl, n, o);
                 *reinterpret_cast<float4*>(rowp + nl * 4) = o;
             }
         }
@@ -494,7 +508,7 @@ template <int NCT>
 __global__ void __launch_bounds__(512)
 k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
-            int64_t ldc, int n_ftiles, int n_tiles, int tiles_per_block) {
+            int64_t ldc, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop) {
     constexpr int WF = 4, TDT = 4, TFT = 2;
     constexpr int NT = 512, BD = 256, BF = 256, TPR = NT / BD, FPT = KC / TPR, WPT = BF * 8 / NT;
     static_assert(TPR == 2 && WPT == 4 && NCT >= 4 && NCT % 2 == 0, "mapping");
@@ -663,6 +677,9 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
     // re-derived from an opaque copy of threadIdx.x inside the epilogue: hoisted out of the tile
     // loop, its addresses and offsets would hold VGPRs through every step and force spills
     // (whose reloads, vector-memory ops, drain the load queue).
+#if !SIR_NT_P_EPI
+#error "the fragment-store persistent NT epilogue has no dropout"
+#endif
 #if SIR_NT_P_EPI
     // Epilogue through LDS (stage 1: free after a tile's last step — the next tile's first chunk
     // is in stage 0 — and the 64-row image of pitch BF*4 + 16 is exactly STAGE bytes): per round b
@@ -698,6 +715,7 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
                     o.y = acc[a][b][4 * g + 1] * is * it.y + bb.y;
                     o.z = acc[a][b][4 * g + 2] * is * it.z + bb.z;
                     o.w = acc[a][b][4 * g + 3] * is * it.w + bb.w;
+                    if (drop.on()) drop4(drop, p.d0 + d_wq + 32 * b + rq, n, o);
                     *reinterpret_cast<float4*>(wrow + (32 * a + 8 * g) * 4) = o;
                 }
             }
@@ -1148,7 +1166,7 @@ hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, v
 }
 
 hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
-                       const float* bias, float* C, int64_t ldc, hipStream_t st) {
+                       const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
     if (M == 0 || N == 0) return hipSuccess;
     const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
     const u4v* wp = static_cast<const u4v*>(packed);
@@ -1156,7 +1174,7 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     const bool kfull = K % KC == 0;
     if (gemm_nt_w_ok(N, K) && M >= SIR_NT_W_MINROWS)
         return run_gemm_nt_w(A, lda, M, K, static_cast<const char*>(packed) + gemm_pack_base_bytes(N, K), N, bias, C,
-                             ldc, st);
+                             ldc, st, drop);
     if (SIR_NT_PERSIST && N > 128 && np <= NT_P_NMAX && kfull && (kc == 4 || kc == 8 || kc == 16)) {
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;
@@ -1170,7 +1188,7 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
             const int nblk = (int)((ntiles + tpb - 1) / tpb);
             auto kern = kc == 4 ? k_gemm_nt_p<4> : (kc == 8 ? k_gemm_nt_p<8> : k_gemm_nt_p<16>);
             hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, ldc,
-                               nft, (int)ntiles, tpb);
+                               nft, (int)ntiles, tpb, drop);
             return hipGetLastError();
         }
     }
@@ -1180,20 +1198,20 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
         const int64_t nblk = (M + BD - 1) / BD * nft;
         if (kfull)
             hipLaunchKernelGGL((k_gemm_nt<2, 4, 4, 2, true>), dim3((unsigned)nblk), dim3(512), 0, st,
-                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft, drop);
         else
             hipLaunchKernelGGL((k_gemm_nt<2, 4, 4, 2, false>), dim3((unsigned)nblk), dim3(512), 0, st,
-                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft, drop);
     } else {
         constexpr int BD = 256, BF = 128;
         const int nft = (N + BF - 1) / BF;
         const int64_t nblk = (M + BD - 1) / BD * nft;
         if (kfull)
             hipLaunchKernelGGL((k_gemm_nt<4, 2, 2, 2, true>), dim3((unsigned)nblk), dim3(512), 0, st,
-                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft, drop);
         else
             hipLaunchKernelGGL((k_gemm_nt<4, 2, 2, 2, false>), dim3((unsigned)nblk), dim3(512), 0, st,
-                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft);
+                               A, lda, M, K, wp, np, inv, bias, N, C, ldc, nft, drop);
     }
     return hipGetLastError();
 }

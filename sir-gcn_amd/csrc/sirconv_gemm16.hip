@@ -21,6 +21,7 @@
 #include "sirconv.h"
 #include "sirconv_internal.h"
 #include "sirconv_gemm_util.h"
+#include "sirconv_dropout.h"
 
 #include <type_traits>
 
@@ -42,6 +43,14 @@ __device__ inline f16v mfma16(u4v a, u4v b, f16v c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
     else
         return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
+
+// x rounded to the 16-bit output type (identity for an fp32 output)
+template <bool BF, bool C32>
+__device__ inline float rnd16(float x) {
+    if constexpr (C32) return x;
+    else if constexpr (BF) return (float)(__bf16)x;
+    else return (float)(_Float16)x;
 }
 
 template <bool BF>
@@ -254,7 +263,7 @@ template <bool BF, bool A32, bool C32, int KC, int NC, int NS>
 __global__ void __launch_bounds__(512)
 k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
             const float* __restrict__ bias, int N, void* __restrict__ C, int64_t ldc, unsigned short* __restrict__ Acopy,
-            int64_t ldac, int n_ftiles, int n_tiles, int tiles_per_block) {
+            int64_t ldac, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop) {
     constexpr int BD = 256, BFT = 256, WF = 4, TDT = 4, TFT = 2;
     constexpr int KS = KC / 16;                       // k16 planes per chunk
     constexpr int PLANE = 256 * 32;                   // one k16 plane of 256 rows
@@ -375,6 +384,9 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
     // C[m][n] = acc + bias[n]; rows past M fall outside the store's range, columns past N are
     // sent past its end (dropped).  Lane indices re-derived from an opaque threadIdx copy so that
     // they do not hold VGPRs through the steps.
+#if !SIR_NT16_EPI
+#error "the fragment-store 16-bit NT epilogue has no dropout"
+#endif
 #if SIR_NT16_EPI
     // Epilogue through LDS: per round b, every wave writes its 32-row band b (bias added, rounded
     // to the output type) into a row-major image of 64 tile rows, then the block stores whole
@@ -398,8 +410,18 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
                 for (int g = 0; g < 4; ++g) {
                     const int nl = f_wq + 32 * a + 8 * g + 4 * hq;
                     const float4 bb = *reinterpret_cast<const float4*>(bias_l + p.f0 + nl);
-                    const float o0 = acc[a][b][4 * g + 0] + bb.x, o1 = acc[a][b][4 * g + 1] + bb.y;
-                    const float o2 = acc[a][b][4 * g + 2] + bb.z, o3 = acc[a][b][4 * g + 3] + bb.w;
+                    float o0 = acc[a][b][4 * g + 0] + bb.x, o1 = acc[a][b][4 * g + 1] + bb.y;
+                    float o2 = acc[a][b][4 * g + 2] + bb.z, o3 = acc[a][b][4 * g + 3] + bb.w;
+                    if (drop.on()) {
+                        // dropout of autocast's dt output: round to dt, scale in fp32, round again
+                        // (the reference's Dropout on the half-precision Linear output)
+                        const uint32_t rh = drop_row_hash(drop, p.d0 + (wq / WF) * (TDT * 32) + 32 * b + rq);
+                        const int cc = drop.col0 + p.f0 + nl;
+                        o0 = drop_keep(drop, rh, cc + 0) ? rnd16<BF, C32>(o0) * drop.scale : 0.f;
+                        o1 = drop_keep(drop, rh, cc + 1) ? rnd16<BF, C32>(o1) * drop.scale : 0.f;
+                        o2 = drop_keep(drop, rh, cc + 2) ? rnd16<BF, C32>(o2) * drop.scale : 0.f;
+                        o3 = drop_keep(drop, rh, cc + 3) ? rnd16<BF, C32>(o3) * drop.scale : 0.f;
+                    }
                     char* d = wrow + (32 * a + 8 * g) * EC;
                     if constexpr (C32) {
                         *reinterpret_cast<float4*>(d) = make_float4(o0, o1, o2, o3);
@@ -545,6 +567,40 @@ hipError_t run_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb,
 }
 
 
+// ------------------------------------------------------------------------------------------
+// feature dropout in place on an [M, N] block (the QK of a path whose projection is not native)
+namespace {
+template <int DT>
+__global__ void __launch_bounds__(256)
+k_dropout_apply(void* __restrict__ X, int64_t ldx, int64_t M, int N, Drop drop) {
+    const int64_t m = blockIdx.y;
+    const uint32_t rh = drop_row_hash(drop, m);
+    for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+        const bool k = drop_keep(drop, rh, drop.col0 + n);
+        if constexpr (DT == SIR_DTYPE_F32) {
+            float* p = static_cast<float*>(X) + m * ldx + n;
+            *p = k ? *p * drop.scale : 0.f;
+        } else if constexpr (DT == SIR_DTYPE_BF16) {
+            __bf16* p = static_cast<__bf16*>(X) + m * ldx + n;
+            *p = k ? (__bf16)((float)*p * drop.scale) : (__bf16)0.f;
+        } else {
+            _Float16* p = static_cast<_Float16*>(X) + m * ldx + n;
+            *p = k ? (_Float16)((float)*p * drop.scale) : (_Float16)0.f;
+        }
+    }
+}
+}  // namespace
+
+hipError_t run_dropout_apply(void* X, int64_t ldx, int64_t M, int N, int dtype, const Drop& drop, hipStream_t st) {
+    if (M == 0 || N == 0 || !drop.on()) return hipSuccess;
+    if (M > 2147483647) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((N + 255) / 256 < 4 ? (N + 255) / 256 : 4), (unsigned)M);
+    if (dtype == SIR_DTYPE_F32) hipLaunchKernelGGL(k_dropout_apply<SIR_DTYPE_F32>, grid, dim3(256), 0, st, X, ldx, M, N, drop);
+    else if (dtype == SIR_DTYPE_BF16) hipLaunchKernelGGL(k_dropout_apply<SIR_DTYPE_BF16>, grid, dim3(256), 0, st, X, ldx, M, N, drop);
+    else hipLaunchKernelGGL(k_dropout_apply<SIR_DTYPE_F16>, grid, dim3(256), 0, st, X, ldx, M, N, drop);
+    return hipGetLastError();
+}
+
 int64_t gemm_pack16_bytes(int64_t N, int64_t K) { return (N + 255) / 256 * 256 * K * 2; }
 
 hipError_t run_gemm_pack16(const float* W, int64_t ldw, int N, int K, int trans, int dtype, void* packed, hipStream_t st) {
@@ -566,7 +622,7 @@ hipError_t run_gemm_pack16(const float* W, int64_t ldw, int N, int K, int trans,
 
 template <bool BF, bool A32, bool C32>
 static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, const void* packed, int N, const float* bias,
-                              void* C, int64_t ldc, unsigned short* Acopy, int64_t ldac, hipStream_t st) {
+                              void* C, int64_t ldc, unsigned short* Acopy, int64_t ldac, hipStream_t st, const Drop& drop) {
     const int np = (N + 255) / 256 * 256, nft = np / 256;
     const int64_t ntiles = (M + 255) / 256 * nft;
     int dev = 0, ncu = 256;
@@ -581,7 +637,7 @@ static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, cons
     const int nc = K / KC;
 #define SIR_NT16_L(NCV, NSV)                                                                                           \
     hipLaunchKernelGGL((k_gemm_nt16<BF, A32, C32, KC, NCV, NSV>), dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, \
-                       np, bias, N, C, ldc, Acopy, ldac, nft, (int)ntiles, tpb)
+                       np, bias, N, C, ldc, Acopy, ldac, nft, (int)ntiles, tpb, drop)
     if (nc == 256 / KC) SIR_NT16_L(256 / KC, (NS <= 256 / KC ? NS : 256 / KC));
     else if (nc == 512 / KC) SIR_NT16_L(512 / KC, NS);
     else if (nc == 128 / KC) SIR_NT16_L(128 / KC, (NS <= 128 / KC ? NS : 128 / KC));
@@ -591,12 +647,13 @@ static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, cons
 }
 
 hipError_t run_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int K, const void* packed, int N, int dtype,
-                         const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac, hipStream_t st) {
+                         const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac, hipStream_t st,
+                         const Drop& drop) {
     if (M == 0) return hipSuccess;
     const bool bf = dtype == SIR_DTYPE_BF16, a32 = a_dtype == SIR_DTYPE_F32, c32 = c_dtype == SIR_DTYPE_F32;
     auto* acp = static_cast<unsigned short*>(Acopy);
 #define SIR_NT16_D(B, A3, C3) \
-    if (bf == B && a32 == A3 && c32 == C3) return launch_nt16<B, A3, C3>(A, lda, M, K, packed, N, bias, C, ldc, acp, ldac, st)
+    if (bf == B && a32 == A3 && c32 == C3) return launch_nt16<B, A3, C3>(A, lda, M, K, packed, N, bias, C, ldc, acp, ldac, st, drop)
     SIR_NT16_D(true, false, false);
     SIR_NT16_D(true, false, true);
     SIR_NT16_D(true, true, false);

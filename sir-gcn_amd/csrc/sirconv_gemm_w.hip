@@ -28,6 +28,7 @@
 // so no barrier is needed (LDS operations of one wave complete in order).
 #include "sirconv_internal.h"
 #include "sirconv_gemm_util.h"
+#include "sirconv_dropout.h"
 
 namespace sir {
 namespace {
@@ -135,7 +136,7 @@ template <int K, int F>
 __global__ void __launch_bounds__(512)
 k_gemm_nt_w(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wimg,
             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
-            int64_t ldc, int nsl, int nrg, int ntiles) {
+            int64_t ldc, int nsl, int nrg, int ntiles, Drop drop) {
     constexpr int FT = F / 32, NCH = K / WKC, IMG = K * F * 4, SLOT = 4096;
     static_assert(NCH % WNS == 0, "chunk count must be a multiple of the register sets");
     static_assert(IMG + 8 * SLOT <= 160 * 1024, "slice image + wave slots fit LDS");
@@ -330,10 +331,19 @@ k_gemm_nt_w(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
                 for (int i = 0; i < 4; ++i) {
                     const float4 v = *reinterpret_cast<const float4*>(slot + slot_off(lr + 8 * i, lp));
                     u4v ov;
-                    ov.x = __float_as_uint(v.x * it.x + bb.x);
-                    ov.y = __float_as_uint(v.y * it.y + bb.y);
-                    ov.z = __float_as_uint(v.z * it.z + bb.z);
-                    ov.w = __float_as_uint(v.w * it.w + bb.w);
+                    float4 o = make_float4(v.x * it.x + bb.x, v.y * it.y + bb.y, v.z * it.z + bb.z, v.w * it.w + bb.w);
+                    if (drop.on()) {           // feature dropout of QK (sirconv_dropout.h)
+                        const uint32_t rh = drop_row_hash(drop, (int64_t)t * 32 + lr + 8 * i);
+                        const int cc = drop.col0 + fl;
+                        o.x = drop_keep(drop, rh, cc + 0) ? o.x * drop.scale : 0.f;
+                        o.y = drop_keep(drop, rh, cc + 1) ? o.y * drop.scale : 0.f;
+                        o.z = drop_keep(drop, rh, cc + 2) ? o.z * drop.scale : 0.f;
+                        o.w = drop_keep(drop, rh, cc + 3) ? o.w * drop.scale : 0.f;
+                    }
+                    ov.x = __float_as_uint(o.x);
+                    ov.y = __float_as_uint(o.y);
+                    ov.z = __float_as_uint(o.z);
+                    ov.w = __float_as_uint(o.w);
                     const uint32_t off = (fl < N) ? (uint32_t)(lr + 8 * i) * ldc4 + (uint32_t)(32 * a + 4 * lp) * 4u : nrec;
                     __builtin_amdgcn_raw_buffer_store_b128(ov, crs, off, f0 * 4, 0);
                     // a 16-byte store reads its data VGPRs over several cycles (sirconv_gemm.hip):
@@ -382,7 +392,7 @@ hipError_t run_gemm_pack_w(const float* W, int64_t ldw, int N, int K, int trans,
 }
 
 hipError_t run_gemm_nt_w(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
-                         const float* bias, float* C, int64_t ldc, hipStream_t st) {
+                         const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
     if (M == 0) return hipSuccess;
     const int F = ntw_feat(K);
     const int nsl = (N + F - 1) / F, np = nsl * F;
@@ -401,13 +411,13 @@ hipError_t run_gemm_nt_w(const float* A, int64_t lda, int64_t M, int K, const vo
     const dim3 grid((unsigned)(nsl * nrg)), blk(512);
     if (K == 256)
         hipLaunchKernelGGL((k_gemm_nt_w<256, 128>), grid, blk, 0, st, A, lda, M, img, inv, bias, N, C, ldc, nsl,
-                           (int)nrg, (int)ntiles);
+                           (int)nrg, (int)ntiles, drop);
     else if (K == 512)
         hipLaunchKernelGGL((k_gemm_nt_w<512, 64>), grid, blk, 0, st, A, lda, M, img, inv, bias, N, C, ldc, nsl,
-                           (int)nrg, (int)ntiles);
+                           (int)nrg, (int)ntiles, drop);
     else
         hipLaunchKernelGGL((k_gemm_nt_w<128, 128>), grid, blk, 0, st, A, lda, M, img, inv, bias, N, C, ldc, nsl,
-                           (int)nrg, (int)ntiles);
+                           (int)nrg, (int)ntiles, drop);
     return hipGetLastError();
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sirconv_dropout.h"
+
 namespace sir {
 
 enum { AGG_SUM = 0, AGG_MEAN = 1, AGG_SYM = 2 };
@@ -29,6 +31,7 @@ struct EdgeArgs {
     uint64_t* mask_out;          // forward: write the sign mask (ReLU family, full-wave rows)
     const uint64_t* mask_in;     // backward: sign-mask mode (Q/K not read)
     const int* perm;             // BWD_SRC mask mode: src-CSR position -> dst-CSR position
+    Drop drop;                   // backward passes: feature dropout on the output rows (sirconv_dropout.h)
 };
 
 struct Shape {
@@ -141,7 +144,7 @@ hipError_t run_mlp_bwd(const EdgeMlpArgs& a, bool dst, int red, int act1, int ac
 int64_t gemm_pack_bytes(int64_t N, int64_t K);
 hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st);
 hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
-                       const float* bias, float* C, int64_t ldc, hipStream_t st);
+                       const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop = Drop());
 int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc);
 hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
                        float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st);
@@ -151,7 +154,7 @@ bool gemm_nt_w_ok(int N, int K);
 int64_t gemm_pack_w_bytes(int N, int K);
 hipError_t run_gemm_pack_w(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st);
 hipError_t run_gemm_nt_w(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
-                         const float* bias, float* C, int64_t ldc, hipStream_t st);
+                         const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop = Drop());
 // C = sum_p part[p] (count elements of rows of Nc, C row stride ldc), p in order
 hipError_t run_gemm_reduce(const float* part, int P, int64_t count, int Nc, float* C, int64_t ldc, hipStream_t st);
 // 16-bit TN GEMM (sirconv_gemm16.hip): A, B bf16 (dtype SIR_DTYPE_BF16) or fp16, fp32 result
@@ -161,6 +164,10 @@ hipError_t run_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb,
 int64_t gemm_pack16_bytes(int64_t N, int64_t K);
 hipError_t run_gemm_pack16(const float* W, int64_t ldw, int N, int K, int trans, int dtype, void* packed, hipStream_t st);
 hipError_t run_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int K, const void* packed, int N, int dtype,
-                         const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac, hipStream_t st);
+                         const float* bias, void* C, int64_t ldc, int c_dtype, void* Acopy, int64_t ldac, hipStream_t st,
+                         const Drop& drop = Drop());
+// feature dropout applied in place to an [M, N] block of QK (the forward of paths whose QK GEMM
+// is not native): X[m][n] = keep(m, col0 + n) ? X[m][n] * scale : 0, storage dtype SIR_DTYPE_*
+hipError_t run_dropout_apply(void* X, int64_t ldx, int64_t M, int N, int dtype, const Drop& drop, hipStream_t st);
 
 }  // namespace sir

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -40,19 +40,20 @@ SIGNATURES = {
     "sir_csr_perm": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P]),
     "sir_gemm_pack_bytes": (ctypes.c_int64, [_I64, _I64]),
     "sir_gemm_pack": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _P, _P]),
-    "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
+    "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P, _P]),
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
     "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
     "sir_gemm_tn16": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _I, _P, _I64, _P, _P, _I64, _P]),
     "sir_gemm_pack16_bytes": (ctypes.c_int64, [_I64, _I64]),
     "sir_gemm_pack16": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _I, _P, _P]),
-    "sir_gemm_nt16": (ctypes.c_int, [_P, _I64, _I, _I64, _I64, _P, _I64, _I, _P, _P, _I64, _I, _P, _I64, _P]),
+    "sir_gemm_nt16": (ctypes.c_int, [_P, _I64, _I, _I64, _I64, _P, _I64, _I, _P, _P, _I64, _I, _P, _I64, _P, _P]),
+    "sir_dropout_apply": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _I64, _P, _P]),
     "sir_edge_agg_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64,
                                         _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
-                                            _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P]),
+                                            _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P, _P]),
     "sir_edge_agg_bwd_src": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
-                                            _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _P]),
+                                            _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _P, _P]),
     "sir_edge_mlp_pack_bytes": (ctypes.c_int64, [_I64, _I64]),
     "sir_edge_mlp_pack": (ctypes.c_int, [_P, _I64, _I64, _P, _P]),
     "sir_edge_mlp_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _I, _I,
@@ -63,8 +64,21 @@ SIGNATURES = {
     "sir_edge_mlp_bwd_src": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
                                             _P, _P, _I, _I, _F, _I, _P, _P, _P, _P, _I64, _P, _P]),
     "sir_edge_agg_bwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _P, _P, _P, _P, _I64, _P, _I64, _I64, _I, _P,
-                                        _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P, _P]),
+                                        _P, _I64, _P, _P, _I, _I, _F, _P, _I64, _P, _I64, _P, _P, _P, _P]),
 }
+
+class Dropout(ctypes.Structure):
+    """``sir_dropout_t`` (include/sirconv.h): the hashed feature-dropout mask of QK (seed, p)."""
+    _fields_ = [("seed", ctypes.c_uint64), ("p", ctypes.c_double)]
+
+
+def _drop(drop):
+    """ctypes pointer argument for an optional (seed, p) pair."""
+    if drop is None:
+        return None
+    seed, p = drop
+    return ctypes.byref(Dropout(int(seed) & (2 ** 64 - 1), float(p)))
+
 
 _lib = None
 _lock = threading.Lock()
@@ -190,7 +204,7 @@ def edge_agg_fwd(csr, Q, K, norm_row, norm_col, agg, act, slope, S, partial, mas
     _check(rc, lib)
 
 
-def edge_agg_bwd_dst(csr, Q, K, G, norm_row, norm_col, agg, act, slope, dQ, Gm, partial, mask=None):
+def edge_agg_bwd_dst(csr, Q, K, G, norm_row, norm_col, agg, act, slope, dQ, Gm, partial, mask=None, drop=None):
     lib = load()
     H = dQ.shape[1]
     with _Timed("sir_edge_agg_bwd_dst", dQ.device):
@@ -198,11 +212,11 @@ def edge_agg_bwd_dst(csr, Q, K, G, norm_row, norm_col, agg, act, slope, dQ, Gm, 
             _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
             H, _storage(Q, K, G, dQ, Gm), _ptr(Q), _ldx(Q, H), _ptr(K), _ldx(K, H), _ptr(mask), _ptr(G), _ld(G, H),
             _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
-            _ptr(dQ), _ld(dQ, H), _ptr(Gm), _ldx(Gm, H), _ptr(partial), _stream(dQ.device))
+            _ptr(dQ), _ld(dQ, H), _ptr(Gm), _ldx(Gm, H), _ptr(partial), _drop(drop), _stream(dQ.device))
     _check(rc, lib)
 
 
-def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, partial, mask=None):
+def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, partial, mask=None, drop=None):
     lib = load()
     H = dK.shape[1]
     with _Timed("sir_edge_agg_bwd_src", dK.device):
@@ -211,11 +225,11 @@ def edge_agg_bwd_src(csr_s, K, Q, Gd, norm_row, norm_col, agg, act, slope, dK, p
             _ptr(csr_s.items), csr_s.n_items, _ptr(csr_s.splits), csr_s.n_splits, H, _storage(K, Q, Gd, dK),
             _ptr(K), _ldx(K, H), _ptr(Q), _ldx(Q, H), _ptr(mask), _ptr(Gd), _ld(Gd, H),
             _ptr(norm_row), _ptr(norm_col), AGG[agg], act, float(slope),
-            _ptr(dK), _ld(dK, H), _ptr(partial), _stream(dK.device))
+            _ptr(dK), _ld(dK, H), _ptr(partial), _drop(drop), _stream(dK.device))
     _check(rc, lib)
 
 
-def edge_agg_bwd(csr, csr_s, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK, partial, partial_s):
+def edge_agg_bwd(csr, csr_s, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK, partial, partial_s, drop=None):
     """Both sign-mask backward passes in one launch (SUM / SYM); bit-identical to
     edge_agg_bwd_dst + edge_agg_bwd_src."""
     lib = load()
@@ -226,7 +240,7 @@ def edge_agg_bwd(csr, csr_s, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK
             _ptr(csr_s.rowptr), _ptr(csr_s.col), _ptr(csr_s.perm), _ptr(csr_s.items), csr_s.n_items,
             _ptr(csr_s.splits), csr_s.n_splits, H, _storage(G, dQ, dK), _ptr(mask), _ptr(G), _ld(G, H),
             _ptr(in_norm), _ptr(out_norm), AGG[agg], act, float(slope), _ptr(dQ), _ld(dQ, H), _ptr(dK), _ld(dK, H),
-            _ptr(partial), _ptr(partial_s), _stream(dQ.device))
+            _ptr(partial), _ptr(partial_s), _drop(drop), _stream(dQ.device))
     _check(rc, lib)
 
 
@@ -356,8 +370,9 @@ def gemm_pack(W, trans=False):
     return packed, N, K
 
 
-def gemm_nt(A, packed, bias=None, out=None):
-    """C = A B^T (+ bias) on the split-fp16 MFMA kernel; ``packed`` from gemm_pack."""
+def gemm_nt(A, packed, bias=None, out=None, drop=None):
+    """C = A B^T (+ bias) on the split-fp16 MFMA kernel; ``packed`` from gemm_pack.  ``drop``:
+    optional (seed, p) feature dropout of the output (C columns = QK columns)."""
     lib = load()
     pk, N, K = packed
     M = A.shape[0]
@@ -366,7 +381,7 @@ def gemm_nt(A, packed, bias=None, out=None):
         out = torch.empty((M, N), dtype=torch.float32, device=A.device)
     with _Timed("sir_gemm_nt", A.device, (2 * M * N * K, 4 * M * (K + N))):
         rc = lib.sir_gemm_nt(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(bias), _ptr(out), out.stride(0),
-                             _stream(A.device))
+                             _drop(drop), _stream(A.device))
     _check(rc, lib)
     return out
 
@@ -431,7 +446,7 @@ def gemm_pack16(W, dtype, trans=False):
     return packed, N, K, dtype
 
 
-def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None):
+def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None, drop=None):
     """C = A B^T (+ bias) on the 16-bit MFMA kernel (``packed`` from gemm_pack16).  A in the
     packed dtype or fp32 (rounded on load; ``acopy`` [M, K] of that dtype receives the rounded A);
     C in ``out_dtype`` (the packed dtype by default, or fp32).  ``bias`` fp32 [N] (pass autocast's
@@ -448,6 +463,17 @@ def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None):
                                             + (acopy.element_size() * M * K if acopy is not None else 0))):
         rc = lib.sir_gemm_nt16(_ptr(A), A.stride(0), STORAGE[A.dtype], M, K, _ptr(pk), N, _DT16[dt], _ptr(bias),
                                _ptr(out), out.stride(0), STORAGE[od], _ptr(acopy),
-                               acopy.stride(0) if acopy is not None else 0, _stream(A.device))
+                               acopy.stride(0) if acopy is not None else 0, _drop(drop), _stream(A.device))
     _check(rc, lib)
     return out
+
+
+def dropout_apply(X, drop, col0=0):
+    """In place: the hashed feature dropout (seed, p) of QK on the [M, N] block X (columns col0 ..)."""
+    lib = load()
+    M, N = X.shape
+    assert X.stride(1) == 1 and X.dtype in STORAGE
+    with _Timed("sir_dropout_apply", X.device):
+        rc = lib.sir_dropout_apply(_ptr(X), X.stride(0), M, N, STORAGE[X.dtype], col0, _drop(drop), _stream(X.device))
+    _check(rc, lib)
+    return X

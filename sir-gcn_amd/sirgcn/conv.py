@@ -119,11 +119,12 @@ def _slots(csr, H, device):
     return torch.empty((csr.n_slots * H,), device=device, dtype=torch.float32) if csr.n_slots else None
 
 
-def edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK):
+def edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK, drop=None):
     """dQ -> dQK[:, :H], dK -> dQK[:, H:] (the backward of ``update_all``, conv.py:45,63).  Sign-mask
     mode runs both passes in one launch (``sir_edge_agg_bwd``; MEAN on G / deg formed first);
     recompute mode runs them one after the other (MEAN: the source pass reads the destination
-    pass's G / deg)."""
+    pass's G / deg).  ``drop``: the (seed, p) feature dropout of the forward's QK — the passes
+    store dQK already multiplied by its mask and scale (the dropout's backward)."""
     in_norm, out_norm = plan.norms(agg)
     if mask is not None and EdgeAggregate.dual:
         if agg == "mean":
@@ -137,13 +138,14 @@ def edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK):
             G = (G.float() / deg).to(G.dtype) if G.dtype != torch.float32 else G / deg
             agg = "sum"
         _native.edge_agg_bwd(plan.dst, plan.src, G, mask, in_norm, out_norm, agg, act, slope, dQK[:, :H],
-                             dQK[:, H:], _slots(plan.dst, H, G.device), _slots(plan.src, H, G.device))
+                             dQK[:, H:], _slots(plan.dst, H, G.device), _slots(plan.src, H, G.device), drop=drop)
         return
     partial = _partial(plan, H, G.device)
     Gm = torch.empty((G.shape[0], H), device=G.device, dtype=G.dtype) if agg == "mean" else None
-    _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope, dQK[:, :H], Gm, partial, mask)
+    _native.edge_agg_bwd_dst(plan.dst, Q, K, G, in_norm, out_norm, agg, act, slope, dQK[:, :H], Gm, partial, mask,
+                             drop=drop)
     _native.edge_agg_bwd_src(plan.src, K, Q, Gm if Gm is not None else G, out_norm, in_norm,
-                             agg, act, slope, dQK[:, H:], partial, mask)
+                             agg, act, slope, dQK[:, H:], partial, mask, drop=drop)
 
 
 _tn = linalg.mm_tn
@@ -181,14 +183,17 @@ class SIRConvFunction(torch.autograd.Function):
     forward : QK = X [W_Q; W_K]^T + [b_Q; 0]  (one GEMM)  ->  S = edge kernels  ->  Y = S W_R^T + b_R
     backward: G = dY W_R, dW_R = dY^T S (split-K), db_R = sum dY, dQ/dK = edge passes,
               dX = [dQ dK] [W_Q; W_K], [dW_Q; dW_K] = [dQ dK]^T X (split-K), db_Q = sum dQ.
-    Used when dropout is inactive and inputs are fp32 (the modular path covers the rest)."""
+    Feature dropout on Q and K (conv.py:60-61, training with p > 0): ``drop`` = (seed, p); the QK
+    GEMM's epilogue applies the hashed mask and the backward edge passes apply the same mask to
+    dQK (``sirconv_dropout.h``) — no mask tensor, no extra pass.  Used for fp32 inputs (the
+    modular path covers the rest)."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on=True):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on=True, drop=None):
         H = W_Q.shape[0]
         X = X.contiguous()
         W_cat = torch.cat([W_Q, W_K], 0)
-        QK = linalg.mm_wt(X, W_cat, torch.cat([b_Q, b_Q.new_zeros(H)]) if b_Q is not None else None)
+        QK = linalg.mm_wt(X, W_cat, torch.cat([b_Q, b_Q.new_zeros(H)]) if b_Q is not None else None, drop=drop)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=torch.float32)
@@ -202,7 +207,7 @@ class SIRConvFunction(torch.autograd.Function):
         Y = linalg.mm_wt(S, W_R, b_R)
         ctx.save_for_backward(X, W_cat, W_R, S, mask if mask is not None else QK)
         ctx.masked = mask is not None
-        ctx.plan, ctx.agg, ctx.act, ctx.slope = plan, agg, act, slope
+        ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.drop = plan, agg, act, slope, drop
         ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
         return Y
 
@@ -222,7 +227,7 @@ class SIRConvFunction(torch.autograd.Function):
             Q, K = saved[:, :H], saved[:, H:]
             mask = None
         dQK = torch.empty((V, 2 * H), device=X.device, dtype=torch.float32)
-        edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK)
+        edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK, ctx.drop)
         dX = linalg.mm_w(dQK, W_cat) if ctx.needs_input_grad[0] else None
         dW_Q = dW_K = db_Q = None
         need_bq = ctx.has_bq and ctx.needs_input_grad[2]
@@ -232,7 +237,7 @@ class SIRConvFunction(torch.autograd.Function):
             db_Q = cs[:H] if need_bq else None
         elif need_bq:
             db_Q = _bias_grad(dQK[:, :H])
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None
 
 
 class SIRConvFunction16(torch.autograd.Function):
@@ -250,17 +255,17 @@ class SIRConvFunction16(torch.autograd.Function):
               half-precision GEMMs (``linalg.mm16_*``)."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on, dt):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on, dt, drop=None):
         H = W_Q.shape[0]
         W_cat = torch.cat([W_Q, W_K], 0)
         b_cat = torch.cat([b_Q, b_Q.new_zeros(H)]) if b_Q is not None else None
         X = X.contiguous()
         if X.dtype == dt:
             Xh = X
-            QK = linalg.mm16_wt(X, W_cat, b_cat, dt)
+            QK = linalg.mm16_wt(X, W_cat, b_cat, dt, drop=drop)
         else:       # X.to(dt) fused into the GEMM's loads; the rounded X (for dW) written by it
             Xh = torch.empty(X.shape, dtype=dt, device=X.device)
-            QK = linalg.mm16_wt(X, W_cat, b_cat, dt, acopy=Xh)
+            QK = linalg.mm16_wt(X, W_cat, b_cat, dt, acopy=Xh, drop=drop)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=dt)
@@ -272,7 +277,7 @@ class SIRConvFunction16(torch.autograd.Function):
         Y = linalg.mm16_wt(S, W_R, b_R, dt)
         ctx.save_for_backward(Xh, W_cat, W_R, S, mask if mask is not None else QK)
         ctx.masked = mask is not None
-        ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.x_dtype, ctx.dt = plan, agg, act, slope, X.dtype, dt
+        ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.x_dtype, ctx.dt, ctx.drop = plan, agg, act, slope, X.dtype, dt, drop
         ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
         return Y
 
@@ -295,7 +300,7 @@ class SIRConvFunction16(torch.autograd.Function):
             Q, K = saved[:, :H], saved[:, H:]
             mask = None
         dQK = torch.empty((V, 2 * H), device=Xh.device, dtype=dt)
-        edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK)
+        edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK, ctx.drop)
         # dX straight from the fp32 accumulator for an fp32 input (no 16-bit rounding, no cast pass)
         dX = linalg.mm16_w(dQK, W_cat, dt, out_dtype=ctx.x_dtype) if ctx.needs_input_grad[0] else None
         dW_Q = dW_K = db_Q = None
@@ -304,7 +309,7 @@ class SIRConvFunction16(torch.autograd.Function):
             dW, cs = _weight_and_bias_grad16(dQK, Xh, True, need_bq)
             dW_Q, dW_K = dW[:H], dW[H:]
             db_Q = cs[:H] if need_bq else None
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None
 
 
 class SIRConv(nn.Module):
@@ -334,6 +339,14 @@ class SIRConv(nn.Module):
         self.linear_relation = nn.Linear(hidden_dim, output_dim, bias=outer_bias)
         self._agg_type = agg_type
         self.chunk = DEFAULT_CHUNK
+
+    def _drop(self):
+        """(seed, p) of this forward's fused feature dropout (conv.py:35,60-61), or None (eval / p = 0).
+        The seed comes from torch's default CPU generator (reproducible under torch.manual_seed); a
+        forward captured into a HIP graph replays the mask drawn at capture time."""
+        if not (self.training and self.dropout.p > 0):
+            return None
+        return int(torch.randint(0, 2 ** 62, (1,)).item()), float(self.dropout.p)
 
     def _project(self, feat_key, feat_query):
         """K = drop(X W_K^T), Q = drop(X W_Q^T + b_Q) (``conv.py:60-61``) as ONE GEMM -> [V, 2H]."""
@@ -387,16 +400,14 @@ class SIRConv(nn.Module):
             from .generic import generic_forward       # edge-materialised native path
             return generic_forward(self, plan, feat_key, feat_query)
         fused = (self.use_fused and feat_key is feat_query and feat_query.dtype == torch.float32 and feat_query.is_cuda
-                 and not torch.is_autocast_enabled() and not (self.training and self.dropout.p > 0)
-                 and self.linear_query.weight.dtype == torch.float32)
+                 and not torch.is_autocast_enabled() and self.linear_query.weight.dtype == torch.float32)
         if fused:
             return SIRConvFunction.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
                                          self.linear_key.weight, self.linear_relation.weight,
                                          self.linear_relation.bias, plan, self._agg_type, act, slope,
-                                         torch.is_grad_enabled())
+                                         torch.is_grad_enabled(), self._drop())
         if (self.use_fused and feat_key is feat_query and torch.is_autocast_enabled() and H % 4 == 0
-                and not (self.training and self.dropout.p > 0) and feat_query.dtype in (torch.float32, torch.bfloat16,
-                                                                                      torch.float16)
+                and feat_query.dtype in (torch.float32, torch.bfloat16, torch.float16)
                 and self.linear_query.weight.dtype == torch.float32):
             dt = torch.get_autocast_dtype("cuda")
             if dt in (torch.bfloat16, torch.float16):
@@ -404,7 +415,7 @@ class SIRConv(nn.Module):
                     return SIRConvFunction16.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
                                                    self.linear_key.weight, self.linear_relation.weight,
                                                    self.linear_relation.bias, plan, self._agg_type, act, slope,
-                                                   torch.is_grad_enabled(), dt)
+                                                   torch.is_grad_enabled(), dt, self._drop())
         QK = self._project(feat_key, feat_query)
         S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope, torch.is_grad_enabled())
         return self.linear_relation(S)

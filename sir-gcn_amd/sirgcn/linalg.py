@@ -32,17 +32,23 @@ def _w_ok(W, n_out):
     return W.is_cuda and W.dtype == torch.float32 and n_out % 4 == 0 and n_out <= MAX_DIM
 
 
-def mm_wt(A, W, bias=None, out=None):
-    """A W^T + bias (nn.Linear); W [N, K]."""
+def mm_wt(A, W, bias=None, out=None, drop=None):
+    """A W^T + bias (nn.Linear); W [N, K].  ``drop``: (seed, p) feature dropout of the result
+    (the QK projection, conv.py:60-61), applied in the native GEMM's epilogue — or, on the torch
+    path, by ``sir_dropout_apply`` with the same hashed mask."""
     if (USE_NATIVE and _ok(A) and _w_ok(W, W.shape[0])
             and (bias is None or (bias.is_contiguous() and bias.data_ptr() % 16 == 0))
             and (out is None or _ok(out))):
-        return _native.gemm_nt(A, _native.gemm_pack(W.contiguous()), bias, out)
+        return _native.gemm_nt(A, _native.gemm_pack(W.contiguous()), bias, out, drop=drop)
     if out is None:
-        return torch.addmm(bias, A, W.t()) if bias is not None else torch.mm(A, W.t())
-    if bias is not None:
-        return torch.addmm(bias, A, W.t(), out=out)
-    return torch.mm(A, W.t(), out=out)
+        out = torch.addmm(bias, A, W.t()) if bias is not None else torch.mm(A, W.t())
+    elif bias is not None:
+        torch.addmm(bias, A, W.t(), out=out)
+    else:
+        torch.mm(A, W.t(), out=out)
+    if drop is not None:
+        _native.dropout_apply(out, drop)
+    return out
 
 
 def mm_w(A, W):
@@ -119,20 +125,24 @@ def _nt16_ok(A, K, N, dt):
             and A.data_ptr() % 16 == 0)
 
 
-def mm16_wt(A, W, bias, dt, out_dtype=None, acopy=None):
+def mm16_wt(A, W, bias, dt, out_dtype=None, acopy=None, drop=None):
     """F.linear(A.to(dt), W.to(dt), bias.to(dt)) (autocast's nn.Linear), result in ``out_dtype``
-    (default dt).  ``acopy``: a [M, K] dt tensor that receives A.to(dt) when A is fp32."""
+    (default dt).  ``acopy``: a [M, K] dt tensor that receives A.to(dt) when A is fp32.  ``drop``:
+    (seed, p) feature dropout of the result (see ``mm_wt``)."""
     N, K = W.shape
     od = out_dtype or dt
     if _nt16_ok(A, K, N, dt) and (acopy is None or (A.dtype == torch.float32 and acopy.stride(1) == 1
                                                      and acopy.data_ptr() % 16 == 0)):
         b = bias.to(dt).float().contiguous() if bias is not None else None
-        return _native.gemm_nt16(A, _native.gemm_pack16(W.contiguous().float(), dt), b, od, acopy)
+        return _native.gemm_nt16(A, _native.gemm_pack16(W.contiguous().float(), dt), b, od, acopy, drop=drop)
     Ah = A.to(dt)
     if acopy is not None:
         acopy.copy_(Ah)
     out = torch.nn.functional.linear(Ah, W.to(dt), bias.to(dt) if bias is not None else None)
-    return out if out.dtype == od else out.to(od)
+    out = out if out.dtype == od else out.to(od)
+    if drop is not None:
+        _native.dropout_apply(out, drop)
+    return out
 
 
 def mm16_w(A, W, dt, out_dtype=None):

@@ -21,14 +21,16 @@ from torch import nn
 
 class SIRStack(nn.Module):
     def __init__(self, conv_cls, hidden, num_layers, activation, agg_type="sum", order="arxiv",
-                 norm_cls=None, conv_activation=None):
+                 norm_cls=None, conv_activation=None, feat_dropout=0):
         super().__init__()
         if order not in ("arxiv", "zinc", "plain"):
             raise ValueError(order)
         self.order = order
         self.activation = activation
         sigma = conv_activation if conv_activation is not None else activation
-        self.convs = nn.ModuleList([conv_cls(hidden, hidden, hidden, sigma, 0, agg_type=agg_type)
+        # feat_dropout: the conv's own Dropout on Q and K, passed positionally as the reference's
+        # models do (ogbn-arxiv/model.py:57, ogbg-molhiv/model.py:66)
+        self.convs = nn.ModuleList([conv_cls(hidden, hidden, hidden, sigma, feat_dropout, agg_type=agg_type)
                                     for _ in range(num_layers)])
         self.norms = nn.ModuleList([norm_cls(hidden) for _ in range(num_layers)]) if norm_cls else None
 

@@ -25,11 +25,14 @@ from torch import nn
 from .stacks import SIRStack
 from .synth import NAMED, dictionary_lookup_batch, molecule_batch, powerlaw_graph
 
+# feat_dropout: the SIRConv dropout the reference trains each config's source with
+# (ogbn-arxiv/train.py:303 and ogbg-molhiv/train.py:249: 0.2; zinc/train.py:206: 0)
 CONFIGS = {
-    "cfg1": dict(hidden=64, layers=1, agg="sum", order="plain", dtype="f32", sigma="seq"),
-    "cfg2": dict(hidden=128, layers=4, agg="sym", order="zinc", dtype="bf16", sigma="leaky"),
-    "cfg3": dict(hidden=256, layers=3, agg="sym", order="arxiv", dtype="f32", sigma="leaky"),
-    "cfg5": dict(hidden=300, layers=5, agg="sum", order="arxiv", dtype="f32", sigma="leaky", norm=True),
+    "cfg1": dict(hidden=64, layers=1, agg="sum", order="plain", dtype="f32", sigma="seq", feat_dropout=0.0),
+    "cfg2": dict(hidden=128, layers=4, agg="sym", order="zinc", dtype="bf16", sigma="leaky", feat_dropout=0.0),
+    "cfg3": dict(hidden=256, layers=3, agg="sym", order="arxiv", dtype="f32", sigma="leaky", feat_dropout=0.2),
+    "cfg5": dict(hidden=300, layers=5, agg="sum", order="arxiv", dtype="f32", sigma="leaky", norm=True,
+                 feat_dropout=0.2),
 }
 DTYPES = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
 
@@ -48,8 +51,10 @@ def make_graph(name, seed=0, rank=0, small=False):
     raise KeyError(name)
 
 
-def make_stack(name, conv_cls, norm_cls=None, seed=4):
-    """The config's layer stack on ``conv_cls`` (and ``norm_cls`` for cfg5), seeded init."""
+def make_stack(name, conv_cls, norm_cls=None, seed=4, feat_dropout=0.0):
+    """The config's layer stack on ``conv_cls`` (and ``norm_cls`` for cfg5), seeded init.
+    ``feat_dropout``: the convs' Q/K dropout (0 for the parity tests; ``bench.py`` passes the
+    config's trained value, ``CONFIGS[name]["feat_dropout"]``)."""
     c = CONFIGS[name]
     H = c["hidden"]
     torch.manual_seed(seed)
@@ -58,7 +63,7 @@ def make_stack(name, conv_cls, norm_cls=None, seed=4):
     if c["sigma"] == "seq":          # dictionary-lookup/model.py:17 (shared by every layer)
         sigma = nn.Sequential(nn.ReLU(inplace=True), nn.Linear(H, H), nn.ReLU(inplace=True))
     return SIRStack(conv_cls, H, c["layers"], act, c["agg"], c["order"],
-                    norm_cls=norm_cls if c.get("norm") else None, conv_activation=sigma)
+                    norm_cls=norm_cls if c.get("norm") else None, conv_activation=sigma, feat_dropout=feat_dropout)
 
 
 def make_inputs(name, num_nodes, device, seed=3):

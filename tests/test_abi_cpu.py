@@ -53,11 +53,11 @@ def test_argument_checks_are_synchronous_and_reported():
     assert b"agg" in lib.sir_last_error()
     # H out of range
     rc = lib.sir_edge_agg_bwd_dst(n, n, n, 0, n, 0, 4096, 0, n, 4096, n, 4096, n, n, 4096, n, n, 0, 2, 0.2,
-                                  n, 4096, n, 4096, n, n)
+                                  n, 4096, n, 4096, n, n, n)
     assert rc == 1 and b"H must be" in lib.sir_last_error()
     # non-NULL requirements when there is work
     rc = lib.sir_edge_agg_bwd_src(n, n, n, n, 5, n, 0, 64, 0, n, 64, n, 64, n, n, 64, n, n, 0, 2, 0.2,
-                                  n, 64, n, n)
+                                  n, 64, n, n, n)
     assert rc == 1
     buf = ctypes.create_string_buffer(64)
     p = ctypes.cast(buf, ctypes.c_void_p)
@@ -73,7 +73,7 @@ def test_argument_checks_are_synchronous_and_reported():
     assert b"sign mask" in lib.sir_last_error()
     # mask-mode src pass needs the permutation
     rc = lib.sir_edge_agg_bwd_src(p, p, n, p, 1, n, 0, 256, 0, n, 256, n, 256, p, p, 256, n, n, 0, 2, 0.2,
-                                  p, 256, n, n)
+                                  p, 256, n, n, n)
     assert rc == 1 and b"perm" in lib.sir_last_error()
 
 
@@ -88,22 +88,22 @@ def test_gemm16_argument_checks():
     assert lib.sir_gemm_pack16(n, 256, 256, 256, 0, 0, n, n) == 1 and b"BF16 or F16" in lib.sir_last_error()
     BF, F32 = 1, 0
     # K must be 128 / 256 / 512, N <= 512
-    assert lib.sir_gemm_nt16(n, 300, BF, 10, 300, n, 256, BF, n, n, 256, BF, n, 0, n) == 1
+    assert lib.sir_gemm_nt16(n, 300, BF, 10, 300, n, 256, BF, n, n, 256, BF, n, 0, n, n) == 1
     assert b"bad shape" in lib.sir_last_error()
-    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 1024, BF, n, n, 1024, BF, n, 0, n) == 1
+    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 1024, BF, n, n, 1024, BF, n, 0, n, n) == 1
     # a_dtype / c_dtype must be the MFMA type or F32
-    assert lib.sir_gemm_nt16(n, 256, 2, 10, 256, n, 256, BF, n, n, 256, BF, n, 0, n) == 1
+    assert lib.sir_gemm_nt16(n, 256, 2, 10, 256, n, 256, BF, n, n, 256, BF, n, 0, n, n) == 1
     assert b"a_dtype" in lib.sir_last_error()
     # 16-bit C: N a multiple of 8
-    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 12, BF, n, n, 12, BF, n, 0, n) == 1
+    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 12, BF, n, n, 12, BF, n, 0, n, n) == 1
     assert b"multiples of 16 B" in lib.sir_last_error()
     # the rounded copy of A needs an fp32 A
-    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 256, BF, n, n, 256, BF, ctypes.c_void_p(16), 256, n) == 1
+    assert lib.sir_gemm_nt16(n, 256, BF, 10, 256, n, 256, BF, n, n, 256, BF, ctypes.c_void_p(16), 256, n, n) == 1
     assert b"Acopy" in lib.sir_last_error()
     # NULL buffers with work; an empty M is a no-op
-    assert lib.sir_gemm_nt16(n, 256, F32, 10, 256, n, 256, BF, n, n, 256, F32, n, 0, n) == 1
+    assert lib.sir_gemm_nt16(n, 256, F32, 10, 256, n, 256, BF, n, n, 256, F32, n, 0, n, n) == 1
     assert b"NULL" in lib.sir_last_error()
-    assert lib.sir_gemm_nt16(n, 256, F32, 0, 256, n, 256, BF, n, n, 256, F32, n, 0, n) == 0
+    assert lib.sir_gemm_nt16(n, 256, F32, 0, 256, n, 256, BF, n, n, 256, F32, n, 0, n, n) == 0
 
 
 def test_mask_words_contract():

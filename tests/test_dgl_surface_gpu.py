@@ -5,8 +5,8 @@
   ids in CSC order, eids), ``in_degrees`` / ``out_degrees`` / ``num_nodes`` / ``edges``;
 * ``forward(graph, (feat_src, feat_dst))`` — the tuple that ``expand_as_pair`` passes through
   (``conv.py:59``): keys from the source features, queries from the destination features;
-* ``dropout > 0`` (``conv.py:35,60-61``): independent masks on Q and K in train mode, identity in
-  eval mode.
+* ``dropout > 0`` (``conv.py:35,60-61``) on the modular path: independent masks on Q and K in train
+  mode, identity in eval mode (the fused layer's own dropout: ``tests/test_dropout_gpu.py``).
 """
 import numpy as np
 import pytest
@@ -147,6 +147,8 @@ def test_dropout_train_masks_and_eval_identity():
     m.dropout = _RecordingDropout(p)
     m0 = SIRConv(d, H, O, nn.LeakyReLU(0.2), 0, agg_type="sum").to(DEV)
     m0.load_state_dict(m.state_dict())
+    # the modular path (nn.Dropout on [Q | K]); the fused layer's hashed dropout: tests/test_dropout_gpu.py
+    m.use_fused = m0.use_fused = False
     g = Graph(src, dst, V)
     Xd = X.to(DEV)
     # train mode: the dropout sees [Q | K] (V x 2H): independent Bernoulli(1-p) masks, survivors / (1-p)

@@ -55,17 +55,17 @@ int main() {
                                                                256, nullptr, 256, nullptr, nullptr, 0, 2, 0.2f, nullptr,
                                                                256, nullptr, nullptr, nullptr), SIR_OK);
     expect("dst: NULL G", sir_edge_agg_bwd_dst(p, p, p, 1, nullptr, 0, 64, 0, v, 64, v, 64, nullptr, nullptr, 64, nullptr,
-                                               nullptr, 0, 2, 0.2f, v, 64, nullptr, 64, nullptr, nullptr), SIR_EINVAL, "G must");
+                                               nullptr, 0, 2, 0.2f, v, 64, nullptr, 64, nullptr, nullptr, nullptr), SIR_EINVAL, "G must");
     expect("src: mask without perm", sir_edge_agg_bwd_src(p, p, nullptr, p, 1, nullptr, 0, 256, 0, nullptr, 256, nullptr,
                                                           256, reinterpret_cast<uint64_t*>(v), v, 256, nullptr, nullptr,
-                                                          0, 2, 0.2f, v, 256, nullptr, nullptr), SIR_EINVAL, "perm");
+                                                          0, 2, 0.2f, v, 256, nullptr, nullptr, nullptr), SIR_EINVAL, "perm");
     expect("bwd (one launch): MEAN refused", sir_edge_agg_bwd(p, p, p, 1, nullptr, 0, p, p, p, p, 1, nullptr, 0, 256, 0,
                                                                reinterpret_cast<uint64_t*>(v), v, 256, nullptr, nullptr, 1,
-                                                               2, 0.2f, v, 256, v, 256, nullptr, nullptr, nullptr),
+                                                               2, 0.2f, v, 256, v, 256, nullptr, nullptr, nullptr, nullptr),
            SIR_EUNSUPPORTED, "MEAN");
     expect("bwd (one launch): needs mask", sir_edge_agg_bwd(p, p, p, 1, nullptr, 0, p, p, p, p, 1, nullptr, 0, 256, 0,
                                                              nullptr, v, 256, nullptr, nullptr, 0, 2, 0.2f, v, 256, v, 256,
-                                                             nullptr, nullptr, nullptr), SIR_EINVAL, "mask");
+                                                             nullptr, nullptr, nullptr, nullptr), SIR_EINVAL, "mask");
     expect("mask words", (int)sir_mask_words(300, SIR_ACT_LEAKY_RELU), 8);
     expect("mask words (GELU)", (int)sir_mask_words(256, SIR_ACT_GELU), 0);
     // generic path, GraphNorm, plan build
@@ -82,8 +82,8 @@ int main() {
                                                  nullptr, v, 64, nullptr), SIR_EINVAL, "2^31");
     expect("csr_build_workspace: negative", (int)sir_csr_build_workspace(-1, 4), -1);
     // GEMMs
-    expect("gemm_nt: K % 4", sir_gemm_nt(f, 6, 1, 6, v, 8, nullptr, f, 8, nullptr), SIR_EINVAL, "multiples");
-    expect("gemm_nt: lda overflow", sir_gemm_nt(f, (int64_t)1 << 21, 1, 16, v, 16, nullptr, f, 16, nullptr), SIR_EINVAL,
+    expect("gemm_nt: K % 4", sir_gemm_nt(f, 6, 1, 6, v, 8, nullptr, f, 8, nullptr, nullptr), SIR_EINVAL, "multiples");
+    expect("gemm_nt: lda overflow", sir_gemm_nt(f, (int64_t)1 << 21, 1, 16, v, 16, nullptr, f, 16, nullptr, nullptr), SIR_EINVAL,
            "lda too large");
     expect("gemm_tn: ldb overflow", sir_gemm_tn(f, 16, f, (int64_t)1 << 21, 1, 16, 16, f, 16, nullptr, v, 1 << 20,
                                                 nullptr), SIR_EINVAL, "too large");

@@ -27,7 +27,7 @@ for (M, K, N, kind) in [(255, 256, 256, "ones"), (255, 256, 256, "randn"), (600,
         pk = torch.empty(lib.sir_gemm_pack_bytes(N, K), dtype=torch.uint8, device=dev)
         assert lib.sir_gemm_pack(P(W), W.stride(0), N, K, 0, P(pk), st) == 0
         C = torch.full((M, N), float("nan"), device=dev)
-        assert lib.sir_gemm_nt(P(A), A.stride(0), M, K, P(pk), N, None, P(C), C.stride(0), st) == 0, lib.sir_last_error()
+        assert lib.sir_gemm_nt(P(A), A.stride(0), M, K, P(pk), N, None, P(C), C.stride(0), None, st) == 0, lib.sir_last_error()
         torch.cuda.synchronize()
         outs[n] = C.cpu()
     ref = (A @ W.t()).cpu()

@@ -77,12 +77,12 @@ def main():
         rc |= lib.sir_edge_agg_bwd_dst(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, dcode,
                                        None, H, None, H, P(mask), P(G), H, P(in_norm), P(out_norm),
                                        _native.AGG[a.agg], _native.ACT_LEAKY, 0.2, P(dQK), 2 * H, None, H,
-                                       P(partial), sp)
+                                       P(partial), None, sp)
         ev[2].record()
         rc |= lib.sir_edge_agg_bwd_src(P(s_.rowptr), P(s_.col), P(s_.perm), P(s_.items), s_.n_items, P(s_.splits),
                                        s_.n_splits, H, dcode, None, H, None, H, P(mask), P(G), H, P(out_norm),
                                        P(in_norm), _native.AGG[a.agg], _native.ACT_LEAKY, 0.2,
-                                       P(dQK[:, H:]), 2 * H, P(partial), sp)
+                                       P(dQK[:, H:]), 2 * H, P(partial), None, sp)
         ev[3].record()
         # the one-launch backward (sum / sym): both passes again, into a second dQK
         dQK2 = torch.empty(V, 2 * H, device=dev, dtype=tdt)
@@ -91,7 +91,7 @@ def main():
                                        P(s_.rowptr), P(s_.col), P(s_.perm), P(s_.items), s_.n_items, P(s_.splits),
                                        s_.n_splits, H, dcode, P(mask), P(G), H, P(in_norm), P(out_norm),
                                        _native.AGG[a.agg], _native.ACT_LEAKY, 0.2, P(dQK2), 2 * H, P(dQK2[:, H:]),
-                                       2 * H, P(partial), P(partial_s), sp)
+                                       2 * H, P(partial), P(partial_s), None, sp)
         ev[4].record()
         assert rc == 0, lib.sir_last_error()
         if a.agg in ("sum", "sym"):

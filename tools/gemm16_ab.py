@@ -65,10 +65,10 @@ def main():
         G = torch.empty(V, H, device=dev, dtype=dt)
         dX = torch.empty(V, H, device=dev, dtype=torch.float32)
         return [
-            ("QK x32 N=2H", lambda: lib.sir_gemm_nt16(P(X), H, F32, V, H, P(p2), 2 * H, BF, P(b2), P(QK), 2 * H, BF, P(Xh), H, st), QK),
-            ("Y  N=H", lambda: lib.sir_gemm_nt16(P(S), H, BF, V, H, P(p1), H, BF, None, P(Y), H, BF, None, 0, st), Y),
-            ("G  N=H (W^T)", lambda: lib.sir_gemm_nt16(P(S), H, BF, V, H, P(p1t), H, BF, None, P(G), H, BF, None, 0, st), G),
-            ("dX K=2H f32", lambda: lib.sir_gemm_nt16(P(dQK), 2 * H, BF, V, 2 * H, P(p2t), H, BF, None, P(dX), H, F32, None, 0, st), dX),
+            ("QK x32 N=2H", lambda: lib.sir_gemm_nt16(P(X), H, F32, V, H, P(p2), 2 * H, BF, P(b2), P(QK), 2 * H, BF, P(Xh), H, None, st), QK),
+            ("Y  N=H", lambda: lib.sir_gemm_nt16(P(S), H, BF, V, H, P(p1), H, BF, None, P(Y), H, BF, None, 0, None, st), Y),
+            ("G  N=H (W^T)", lambda: lib.sir_gemm_nt16(P(S), H, BF, V, H, P(p1t), H, BF, None, P(G), H, BF, None, 0, None, st), G),
+            ("dX K=2H f32", lambda: lib.sir_gemm_nt16(P(dQK), 2 * H, BF, V, 2 * H, P(p2t), H, BF, None, P(dX), H, F32, None, 0, None, st), dX),
         ]
 
     def tn_shapes(lib):

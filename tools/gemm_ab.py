@@ -75,7 +75,7 @@ def main():
             A, _, _, bias = v
             pk, N, K = packs[(n, s)]
             C = outs.setdefault((n, s), torch.empty(V, N, device=dev))
-            rc = lib.sir_gemm_nt(P(A), A.stride(0), V, K, P(pk), N, P(bias), P(C), C.stride(0), st)
+            rc = lib.sir_gemm_nt(P(A), A.stride(0), V, K, P(pk), N, P(bias), P(C), C.stride(0), None, st)
         else:
             A, B = v
             C = outs.setdefault((n, s), torch.empty(A.shape[1], B.shape[1], device=dev))

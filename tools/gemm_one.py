@@ -33,6 +33,6 @@ pk = torch.empty(lib.sir_gemm_pack_bytes(N, K), dtype=torch.uint8, device=dev)
 assert lib.sir_gemm_pack(P(W), W.stride(0), N, K, 0, P(pk), st) == 0
 C = torch.empty(V, N, device=dev)
 for _ in range(a.reps):
-    assert lib.sir_gemm_nt(P(A), A.stride(0), V, K, P(pk), N, None, P(C), C.stride(0), st) == 0
+    assert lib.sir_gemm_nt(P(A), A.stride(0), V, K, P(pk), N, None, P(C), C.stride(0), None, st) == 0
 torch.cuda.synchronize()
 print("ok", a.shape, a.lib)
