@@ -55,6 +55,9 @@ enum { SIR_DTYPE_F32 = 0, SIR_DTYPE_BF16 = 1, SIR_DTYPE_F16 = 2 };
 enum { SIR_OK = 0, SIR_EINVAL = 1, SIR_EUNSUPPORTED = 2, SIR_ELAUNCH = 3 };
 
 int sir_abi_version(void);
+/* First 16 hex digits of sha256 over the library's kernel and ABI sources (csrc/*.hip, *.h, *.cpp and
+ * include/*.h, concatenated in path order) at build time: lets a host detect a stale prebuilt library. */
+const char* sir_source_hash(void);
 const char* sir_last_error(void);
 
 /*

@@ -67,6 +67,11 @@ extern "C" {
 
 int sir_abi_version(void) { return SIR_ABI_VERSION; }
 
+#ifndef SIR_SRC_HASH
+#define SIR_SRC_HASH "unknown"
+#endif
+const char* sir_source_hash(void) { return SIR_SRC_HASH; }
+
 const char* sir_last_error(void) { return g_last_error.c_str(); }
 
 int64_t sir_mask_words(int64_t H, int act) {

@@ -22,6 +22,7 @@ STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: 
 _P, _I64, _I, _F = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
 SIGNATURES = {
     "sir_abi_version": (ctypes.c_int, []),
+    "sir_source_hash": (ctypes.c_char_p, []),
     "sir_last_error": (ctypes.c_char_p, []),
     "sir_mask_words": (ctypes.c_int64, [_I64, _I]),
     "sir_degree_norms": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P]),
@@ -115,6 +116,26 @@ class _Timed:
             _timing.setdefault(self.name, []).append((self.ev[0], self.ev[1], self.work))
 
 
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "include")
+
+
+def source_hash():
+    """The fingerprint the Makefile embeds (sha256 of csrc/*.hip, *.h, *.cpp and include/*.h in path
+    order, first 16 hex digits), or None when the sources are not in the tree."""
+    import glob
+    import hashlib
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h"))
+                   + glob.glob(os.path.join(CSRC, "*.cpp")) + glob.glob(os.path.join(INCLUDE, "*.h")))
+    if not files:
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load():
     """Load (once) and return the ctypes handle; raise loudly if absent."""
     global _lib
@@ -132,6 +153,11 @@ def load():
                 fn.argtypes = args
             if lib.sir_abi_version() != ABI_VERSION:
                 raise RuntimeError(f"sirgcn: ABI mismatch (library {lib.sir_abi_version()}, host {ABI_VERSION})")
+            want = source_hash()
+            got = lib.sir_source_hash().decode()
+            if want is not None and got != want:
+                raise RuntimeError(f"sirgcn: {LIB_PATH} was built from other sources (library {got}, tree {want}); "
+                                   "rebuild it with `make -C sir-gcn_amd/csrc`")
             _lib = lib
     return _lib
 

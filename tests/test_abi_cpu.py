@@ -138,3 +138,10 @@ def test_abi_argument_checks_under_asan_ubsan(tmp_path):
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "ok: 0 failure(s)" in r.stdout
+
+
+def test_library_built_from_these_sources():
+    """The library embeds a fingerprint of its sources (sir_source_hash); load() refuses a stale
+    build whose fingerprint differs from the tree's."""
+    lib = _native.load()
+    assert lib.sir_source_hash().decode() == _native.source_hash()

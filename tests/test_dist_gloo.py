@@ -1,5 +1,6 @@
-"""Multi-rank edge-cut (sirgcn.dist) on CPU with gloo, world_size 2 and 3: partition
-invariants, the all-gather / reduce-scatter / all-reduce exchange, and the assembled layer
+"""Multi-rank edge-cut (sirgcn.dist) on CPU with gloo, world sizes 2-4: partition invariants,
+the sparse halo all-to-all (forward K rows) and its transpose (backward dK rows), the weight-gradient
+all-reduce, and the assembled layer
 output + gradients against the single-process CPU oracle.  The per-rank edge math uses the
 test-only CPU backend (tests/cpu_edge_backend.py); the GPU path is covered by -m gpu tests."""
 import os
