@@ -219,7 +219,7 @@ def kernel_table(timing, rows_of, edges, H, agg, masked, s):
                           "TFLOPs": round(fl / (t * 1e-3) / 1e12, 1), "hbm_bytes": by,
                           "GBps": round(by / (t * 1e-3) / 1e9, 1),
                           # fp16/bf16 MFMAs issued per product: 3 for the two-term split, 1 for 16-bit operands
-                          "mfma_per_product": 1 if name.endswith("16") else 3}
+                          "mfma_per_product": 1 if name.split(" ")[0].endswith("16") else 3}
             continue
         if name == "sir_edge_mlp_fwd":         # fused per-edge dense layer: fp32 MFMA flops per launch
             fl = sum(w for _, _, w in evs) / len(evs)
@@ -528,20 +528,16 @@ def design_bytes(kernels, gemm, steps, ms):
 def run_stack(args, world, rank, dev, torch, dist):
     """BASELINE configs 1/2/3/5: the reference models' layer loops (sirgcn.workloads)."""
     from sirgcn import GraphNorm, SIRConv, _native
-    from sirgcn.workloads import CONFIGS, DTYPES, make_graph, make_inputs, make_stack
+    from sirgcn.workloads import CONFIGS, DTYPES, dp_replica
     name = args.workload
     c = CONFIGS[name]
     dtn = args.dtype or c["dtype"]
     dt = DTYPES[dtn]
     if world > 1 and name != "cfg5":
         raise SystemExit(f"{name} is a single-GPU workload (cfg5 is the data-parallel one, cfg4 the edge-cut)")
-    g = make_graph(name, rank=rank)
     p_drop = c["feat_dropout"] if args.dropout is None else args.dropout
-    stack = make_stack(name, SIRConv, GraphNorm, feat_dropout=p_drop).to(dev)
-    model = stack
-    if world > 1:           # DP replicas: a different batch per rank, RCCL gradient all-reduce
-        model = torch.nn.parallel.DistributedDataParallel(stack, device_ids=[dev.index])
-    X, dY = make_inputs(name, g.num_nodes(), dev, seed=3 + rank)
+    # DP replicas: a different batch per rank, RCCL gradient all-reduce (DDP)
+    model, stack, g, X, dY = dp_replica(name, rank, world, dev, SIRConv, GraphNorm, feat_dropout=p_drop)
     X.requires_grad_(True)
     dY_in = dY if dt == torch.float32 else dY.to(dt)      # cast outside the timed region (as in run_edge_cut)
 

@@ -1157,7 +1157,7 @@ hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, v
     _Float16* out = static_cast<_Float16*>(packed);
     float* inv = reinterpret_cast<float*>(static_cast<char*>(packed) + (int64_t)kc * 4 * np * 32);
     hipLaunchKernelGGL(k_pack_weight, dim3(np), dim3(64), 0, st, W, ldw, N, K, trans, np, kc, out, inv);
-    if (gemm_nt_w_ok(N, K)) {
+    if (gemm_pack_w_bytes(N, K) > 0) {     // the W image whenever the shape has one (route chosen per launch)
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         return run_gemm_pack_w(W, ldw, N, K, trans, static_cast<char*>(packed) + gemm_pack_base_bytes(N, K), st);

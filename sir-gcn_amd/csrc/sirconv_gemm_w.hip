@@ -30,6 +30,8 @@
 #include "sirconv_gemm_util.h"
 #include "sirconv_dropout.h"
 
+#include <cstdlib>
+
 namespace sir {
 namespace {
 using namespace gemm;
@@ -366,17 +368,29 @@ k_gemm_nt_w(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
 // ------------------------------------------------------------------------------------------
 static int ntw_feat(int K) { return K <= 256 ? 128 : 64; }
 
+// the shapes the kernel handles: Y, G (N <= 256: two slices) and K <= 256 only — with four slices
+// (QK at N = 512, dX at K = 512) the per-slice re-reads of A no longer hit in L2 and k_gemm_nt_p is
+// faster (r03 A/B).  The packed weight always carries the image for these shapes, whatever the
+// route switch says at pack time (the switch is read again at every launch).
+static bool gemm_nt_w_shape(int N, int K) {
+    return N > 0 && N % 4 == 0 && N <= 2 * ntw_feat(K) && (K == 128 || K == 256);
+}
+
 bool gemm_nt_w_ok(int N, int K) {
 #ifdef SIR_NT_W
     if (!SIR_NT_W) return false;
 #endif
-    // Y, G (N <= 256: two slices) and K <= 256 only: with four slices (QK at N = 512, dX at K = 512)
-    // the per-slice re-reads of A no longer hit in L2 and k_gemm_nt_p is faster (r03 A/B)
-    return N > 0 && N % 4 == 0 && N <= 2 * ntw_feat(K) && (K == 128 || K == 256);
+    // OPT-IN (SIR_NT_W=1 in the environment, read per call so a process can A/B it): stand-alone
+    // the kernel beats k_gemm_nt_p on Y / G (0.98 vs 1.04 ms at S2), but inside the S2 step it is
+    // slower (1.08-1.12 vs 0.95 ms; step 21.6 vs 21.3 ms, r03 A/B on one box), so the default
+    // route stays k_gemm_nt_p.
+    const char* e = getenv("SIR_NT_W");
+    if (e == nullptr || e[0] != '1') return false;
+    return gemm_nt_w_shape(N, K);
 }
 
 int64_t gemm_pack_w_bytes(int N, int K) {
-    if (!gemm_nt_w_ok(N, K)) return 0;
+    if (!gemm_nt_w_shape(N, K)) return 0;
     const int F = ntw_feat(K);
     const int64_t np = (int64_t)(N + F - 1) / F * F;
     return np * K * 4 + np * 4;

@@ -405,7 +405,7 @@ def gemm_nt(A, packed, bias=None, out=None, drop=None):
     assert A.dim() == 2 and A.shape[1] == K and A.stride(1) == 1
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    with _Timed("sir_gemm_nt", A.device, (2 * M * N * K, 4 * M * (K + N))):
+    with _Timed(f"sir_gemm_nt K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + N))):
         rc = lib.sir_gemm_nt(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(bias), _ptr(out), out.stride(0),
                              _drop(drop), _stream(A.device))
     _check(rc, lib)
@@ -425,7 +425,7 @@ def gemm_tn(A, B, out=None, colsum=False):
     cs = torch.empty((M,), dtype=torch.float32, device=A.device) if colsum else None
     ws_bytes = lib.sir_gemm_tn_workspace(R, M, N)
     ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=A.device)
-    with _Timed("sir_gemm_tn", A.device, (2 * R * M * N, 4 * R * (M + N))):
+    with _Timed(f"sir_gemm_tn M={M} N={N}", A.device, (2 * R * M * N, 4 * R * (M + N))):
         rc = lib.sir_gemm_tn(_ptr(A), A.stride(0), _ptr(B), B.stride(0), R, M, N, _ptr(out), out.stride(0),
                              _ptr(cs), _ptr(ws), ws.numel(), _stream(A.device))
     _check(rc, lib)
@@ -472,7 +472,7 @@ def gemm_pack16(W, dtype, trans=False):
     return packed, N, K, dtype
 
 
-def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None, drop=None):
+def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None, drop=None, out=None):
     """C = A B^T (+ bias) on the 16-bit MFMA kernel (``packed`` from gemm_pack16).  A in the
     packed dtype or fp32 (rounded on load; ``acopy`` [M, K] of that dtype receives the rounded A);
     C in ``out_dtype`` (the packed dtype by default, or fp32).  ``bias`` fp32 [N] (pass autocast's
@@ -482,7 +482,9 @@ def gemm_nt16(A, packed, bias=None, out_dtype=None, acopy=None, drop=None):
     M = A.shape[0]
     assert A.dim() == 2 and A.shape[1] == K and A.stride(1) == 1 and A.dtype in (dt, torch.float32)
     od = out_dtype or dt
-    out = torch.empty((M, N), dtype=od, device=A.device)
+    if out is None:
+        out = torch.empty((M, N), dtype=od, device=A.device)
+    assert out.dtype == od and out.shape == (M, N) and out.stride(1) == 1
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     with _Timed("sir_gemm_nt16", A.device, (2 * M * N * K, A.element_size() * M * K + out.element_size() * M * N

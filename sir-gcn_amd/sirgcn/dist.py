@@ -21,6 +21,10 @@ backend ``nccl``):
   goes back to the owners by the reverse all-to-all (overlapped with the dQ pass and the
   independent GEMMs) and is added in ascending peer order — deterministic.
 * **Weight gradients**: one all-reduce of a flat buffer (``allreduce_grads``).
+* **Backward edge passes**: in sign-mask mode ONE launch (dQ waves beside dK waves, as on one GPU;
+  MEAN on G / deg); the halo dK exchange follows it, under the independent GEMMs.
+* **Autocast** (``DistSIRConvFunction16``): 16-bit K_ext rows, edge passes and both exchanges in
+  the 16-bit type — half the wire bytes.
 * ``sym`` needs GLOBAL out-degrees: own-row out-degree histograms are completed by the same
   reverse exchange and forwarded to the halos (plan time, once).
 
@@ -31,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native, linalg
-from .conv import _tn, _weight_and_bias_grad, activation_code
+from .conv import EdgeAggregate, _slots, _tn, _weight_and_bias_grad, _weight_and_bias_grad16, activation_code
 from .graph import DEFAULT_CHUNK, build_plans_native, build_row_csr
 
 
@@ -144,6 +148,7 @@ class DistGraph:
         self.local_out_deg = (self.src.rowptr[1:] - self.src.rowptr[:-1]).to(torch.int64)
         self._out_deg = None
         self._norms = {}
+        self._deg_f = None       # fp32 in-degree of own rows (the one-launch MEAN backward)
 
     @classmethod
     def from_global(cls, src, dst, num_nodes, rank, world, device, chunk=DEFAULT_CHUNK, group=None):
@@ -213,6 +218,41 @@ def _workspace(plan, H, device):
     return torch.empty((max(n, 1) * H,), device=device, dtype=torch.float32) if n else None
 
 
+def _edge_backward_exchange(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recv):
+    """dQ (own rows) and dK_ext (own + halo sources) of the local edges, then the reverse
+    all-to-all of the halo dK rows into ``recv`` — started asynchronously and returned, so the
+    caller's independent GEMMs run under it.
+
+    Sign-mask mode on the native backend: both passes in ONE launch (``sir_edge_agg_bwd``, the
+    single-GPU layer's backward; MEAN on G / deg formed first — every in-edge of an own row is
+    local, so deg is the local CSR's), the exchange after it.  Recompute mode (other backends,
+    sigma without a mask): the dK pass first (MEAN: after the dQ pass, which writes G / deg) and
+    the dQ pass under the exchange."""
+    in_norm, out_norm = dg.norms(agg)
+    n = dg.n_rows
+    if mask is not None and backend is _native and EdgeAggregate.dual:
+        if agg == "mean":
+            if dg._deg_f is None:
+                rp = dg.dst.rowptr
+                dg._deg_f = (rp[1:] - rp[:-1]).clamp(min=1).to(torch.float32)[:, None]
+            G = (G.float() / dg._deg_f).to(G.dtype) if G.dtype != torch.float32 else G / dg._deg_f
+            agg = "sum"
+        _native.edge_agg_bwd(dg.dst, dg.src, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK_ext,
+                             _slots(dg.dst, H, G.device), _slots(dg.src, H, G.device))
+        return dg.scatter_halo(dK_ext[n:], recv, async_op=True)
+    partial = _workspace(dg, H, G.device)
+    Gm = None
+    if agg == "mean":     # the dK pass reads G / deg, written by the dQ pass
+        Gm = torch.empty((n, H), device=G.device, dtype=G.dtype)
+        backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, Gm, partial, mask)
+    backend.edge_agg_bwd_src(dg.src, K_ext, Q, Gm if Gm is not None else G, out_norm, in_norm,
+                             agg, act, slope, dK_ext, partial, mask)
+    work = dg.scatter_halo(dK_ext[n:], recv, async_op=True)
+    if agg != "mean":     # overlaps the reverse exchange
+        backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, None, partial, mask)
+    return work
+
+
 class DistSIRConvFunction(torch.autograd.Function):
     """One rank's share of the whole layer, hand-scheduled around the two exchanges.
 
@@ -265,21 +305,10 @@ class DistSIRConvFunction(torch.autograd.Function):
         dev = X.device
         dY = dY.contiguous()
         G = linalg.mm_w(dY, W_R)
-        in_norm, out_norm = dg.norms(agg)
-        partial = _workspace(dg, H, dev)
         dQ = torch.empty((n, H), device=dev, dtype=torch.float32)
         dK_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
-        Gm = None
-        if agg == "mean":     # the dK pass reads G / deg, written by the dQ pass
-            Gm = torch.empty((n, H), device=dev, dtype=torch.float32)
-            backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, Gm, partial, mask)
-        backend.edge_agg_bwd_src(dg.src, K_ext, Q, Gm if Gm is not None else G, out_norm, in_norm,
-                                 agg, act, slope, dK_ext, partial, mask)
         recv = torch.empty((dg.send_idx.numel(), H), device=dev, dtype=torch.float32)
-        work = dg.scatter_halo(dK_ext[n:], recv, async_op=True)
-        if agg != "mean":     # overlaps the reverse exchange
-            backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, None, partial,
-                                     mask)
+        work = _edge_backward_exchange(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recv)
         dW_R, db_R = _weight_and_bias_grad(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
         dX = linalg.mm_w(dQ, W_Q) if ctx.needs_input_grad[0] else None
         dW_Q, db_Q = _weight_and_bias_grad(dQ, X, ctx.needs_input_grad[1], ctx.has_bq and ctx.needs_input_grad[2])
@@ -292,6 +321,86 @@ class DistSIRConvFunction(torch.autograd.Function):
             dX += linalg.mm_w(dK, W_K)
         dW_K = _tn(dK, X) if ctx.needs_input_grad[3] else None
         return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None
+
+
+class DistSIRConvFunction16(torch.autograd.Function):
+    """:class:`DistSIRConvFunction` under autocast (bf16 / fp16 ``dt``, the reference's AMP path):
+    the single-GPU ``SIRConvFunction16`` dataflow per rank — 16-bit projections on the native
+    16-bit MFMA GEMMs (X.to(dt) fused into the first one), 16-bit ``K_ext`` rows and edge passes
+    (fp32 math inside) — with both halo exchanges in the 16-bit storage type: half the xGMI bytes
+    of the fp32 layer.  The received dK rows are added in that type (one more rounding per peer
+    than the single-GPU sum; within the AMP tolerance)."""
+
+    @staticmethod
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on, dt):
+        H = W_Q.shape[0]
+        n = dg.n_rows
+        dev = X.device
+        X = X.contiguous()
+        K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=dt)
+        if X.dtype == dt:
+            Xh = X
+            linalg.mm16_wt(X, W_K, None, dt, out=K_ext[:n])
+        else:       # X.to(dt) fused into the K GEMM's loads; the rounded X (for dW) written by it
+            Xh = torch.empty(X.shape, dtype=dt, device=dev)
+            linalg.mm16_wt(X, W_K, None, dt, acopy=Xh, out=K_ext[:n])
+        work = dg.gather_halo(K_ext[:n], K_ext[n:], async_op=True)
+        Q = linalg.mm16_wt(Xh, W_Q, b_Q, dt)
+        if work is not None:
+            work.wait()
+        in_norm, out_norm = dg.norms(agg)
+        S = torch.empty((n, H), device=dev, dtype=dt)
+        partial = _workspace(dg, H, dev)
+        training = grad_on and any(ctx.needs_input_grad[:6])
+        nw = _native.mask_words(H, act) if (use_mask and training and backend is _native) else 0
+        mask = torch.empty((max(dg.dst.col.numel(), 1) * nw,), device=dev, dtype=torch.int64) if nw else None
+        backend.edge_agg_fwd(dg.dst, Q, K_ext, in_norm, out_norm, agg, act, slope, S, partial, mask)
+        Y = linalg.mm16_wt(S, W_R, b_R, dt)
+        if mask is not None:
+            ctx.save_for_backward(Xh, W_Q, W_K, W_R, S, mask)
+        else:
+            ctx.save_for_backward(Xh, W_Q, W_K, W_R, S, Q, K_ext)
+        ctx.masked = mask is not None
+        ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend = dg, agg, act, slope, backend
+        ctx.x_dtype, ctx.dt = X.dtype, dt
+        ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        dg, agg, act, slope, backend, dt = ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend, ctx.dt
+        if ctx.masked:
+            Xh, W_Q, W_K, W_R, S, mask = ctx.saved_tensors
+            Q = K_ext = None
+        else:
+            Xh, W_Q, W_K, W_R, S, Q, K_ext = ctx.saved_tensors
+            mask = None
+        H = W_R.shape[1]
+        n = dg.n_rows
+        dev = Xh.device
+        dY = dY.contiguous().to(dt)
+        G = linalg.mm16_w(dY, W_R, dt)
+        dQ = torch.empty((n, H), device=dev, dtype=dt)
+        dK_ext = torch.empty((dg.n_ext, H), device=dev, dtype=dt)
+        recv = torch.empty((dg.send_idx.numel(), H), device=dev, dtype=dt)
+        work = _edge_backward_exchange(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recv)
+        dW_R = db_R = None
+        if ctx.needs_input_grad[4] or ctx.needs_input_grad[5]:
+            dW_R, db_R = _weight_and_bias_grad16(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
+        dX = linalg.mm16_w(dQ, W_Q, dt, out_dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        dW_Q = db_Q = None
+        if ctx.needs_input_grad[1] or (ctx.has_bq and ctx.needs_input_grad[2]):
+            dW_Q, db_Q = _weight_and_bias_grad16(dQ, Xh, True, ctx.has_bq and ctx.needs_input_grad[2])
+        if work is not None:
+            work.wait()
+        dK = dK_ext[:n]
+        if dg.world > 1:
+            dg.add_received(dK, recv)
+        if dX is not None:
+            dX += linalg.mm16_w(dK, W_K, dt, out_dtype=torch.float32)
+            dX = dX.to(ctx.x_dtype)
+        dW_K = _weight_and_bias_grad16(dK, Xh, True, False)[0] if ctx.needs_input_grad[3] else None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None
 
 
 class DistEdgeAggregate(torch.autograd.Function):
@@ -379,6 +488,16 @@ class DistSIRConv(torch.nn.Module):
                                              c.linear_relation.weight, c.linear_relation.bias, dgraph,
                                              c._agg_type, act, slope, self.backend, self.use_mask,
                                              torch.is_grad_enabled())
+        if (self.use_fused and feat.is_cuda and torch.is_autocast_enabled() and H % 4 == 0
+                and not (c.training and c.dropout.p > 0) and c.linear_query.weight.dtype == torch.float32
+                and feat.dtype in (torch.float32, torch.bfloat16, torch.float16)):
+            dt = torch.get_autocast_dtype("cuda")
+            if dt in (torch.bfloat16, torch.float16):
+                with torch.autocast("cuda", enabled=False):
+                    return DistSIRConvFunction16.apply(feat, c.linear_query.weight, c.linear_query.bias,
+                                                       c.linear_key.weight, c.linear_relation.weight,
+                                                       c.linear_relation.bias, dgraph, c._agg_type, act, slope,
+                                                       self.backend, self.use_mask, torch.is_grad_enabled(), dt)
         Q = c.dropout(c.linear_query(feat))
         K = c.dropout(c.linear_key(feat))
         S = DistEdgeAggregate.apply(Q, K, dgraph, H, c._agg_type, act, slope, self.backend, self.use_mask,

@@ -19,7 +19,8 @@ MAX_LD = 1 << 20         # SIR_GEMM_MAX_LD (include/sirconv.h)
 # Below this many node rows the native kernels (256-row tiles, split-K over rows) cannot fill the
 # 256 CUs and the call is launch-bound: small batches (config 5: ~1.6k nodes) use torch's fp32 GEMM
 # (hipBLASLt), which is also IEEE fp32.
-MIN_ROWS = 32768
+DEFAULT_MIN_ROWS = 32768
+MIN_ROWS = DEFAULT_MIN_ROWS
 
 
 def _ok(t):
@@ -80,7 +81,8 @@ def _tn16_ok(t):
 
 # The 16-bit TN kernel moves half the bytes and does a third of the MFMA work of the split one;
 # it still splits the rows over >= 2048-row ranges, so below this it cannot fill the chip.
-MIN_ROWS_16 = 16384
+DEFAULT_MIN_ROWS_16 = 16384
+MIN_ROWS_16 = DEFAULT_MIN_ROWS_16
 
 
 def mm_tn16(A, B, colsum=False):
@@ -118,31 +120,37 @@ def _tn_torch(A, B):
 NT16_K = (128, 256, 512)
 
 
-def _nt16_ok(A, K, N, dt):
+def _nt16_ok(A, K, N, dt, out=None):
+    if out is not None and not (out.stride(1) == 1 and out.stride(0) % 8 == 0 and out.data_ptr() % 16 == 0):
+        return False
     return (USE_NATIVE and A.is_cuda and A.dim() == 2 and A.stride(1) == 1 and A.dtype in (dt, torch.float32)
             and A.shape[0] >= MIN_ROWS_16 and K in NT16_K and N <= 512 and N % 8 == 0
             and A.stride(0) % (4 if A.dtype == torch.float32 else 8) == 0 and A.stride(0) <= MAX_LD
             and A.data_ptr() % 16 == 0)
 
 
-def mm16_wt(A, W, bias, dt, out_dtype=None, acopy=None, drop=None):
+def mm16_wt(A, W, bias, dt, out_dtype=None, acopy=None, drop=None, out=None):
     """F.linear(A.to(dt), W.to(dt), bias.to(dt)) (autocast's nn.Linear), result in ``out_dtype``
     (default dt).  ``acopy``: a [M, K] dt tensor that receives A.to(dt) when A is fp32.  ``drop``:
     (seed, p) feature dropout of the result (see ``mm_wt``)."""
     N, K = W.shape
     od = out_dtype or dt
-    if _nt16_ok(A, K, N, dt) and (acopy is None or (A.dtype == torch.float32 and acopy.stride(1) == 1
+    if _nt16_ok(A, K, N, dt, out) and (acopy is None or (A.dtype == torch.float32 and acopy.stride(1) == 1
                                                      and acopy.data_ptr() % 16 == 0)):
         b = bias.to(dt).float().contiguous() if bias is not None else None
-        return _native.gemm_nt16(A, _native.gemm_pack16(W.contiguous().float(), dt), b, od, acopy, drop=drop)
+        return _native.gemm_nt16(A, _native.gemm_pack16(W.contiguous().float(), dt), b, od, acopy, drop=drop,
+                                 out=out)
     Ah = A.to(dt)
     if acopy is not None:
         acopy.copy_(Ah)
-    out = torch.nn.functional.linear(Ah, W.to(dt), bias.to(dt) if bias is not None else None)
-    out = out if out.dtype == od else out.to(od)
+    res = torch.nn.functional.linear(Ah, W.to(dt), bias.to(dt) if bias is not None else None)
+    res = res if res.dtype == od else res.to(od)
     if drop is not None:
-        _native.dropout_apply(out, drop)
-    return out
+        _native.dropout_apply(res, drop)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
 
 
 def mm16_w(A, W, dt, out_dtype=None):

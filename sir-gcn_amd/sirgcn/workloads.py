@@ -73,3 +73,18 @@ def make_inputs(name, num_nodes, device, seed=3):
     X = torch.randn(num_nodes, H, generator=gen).to(device)
     dY = torch.randn(num_nodes, H, generator=gen).to(device)
     return X, dY
+
+
+def dp_replica(name, rank, world, device, conv_cls, norm_cls=None, feat_dropout=0.0, small=False):
+    """One rank of a data-parallel workload (cfg5: a different batch of molecules per rank, the
+    stack replicated with identical initial weights, gradients averaged by DDP's all-reduce —
+    RCCL in ``bench.py --gpus N``, gloo in tests/test_ddp_gloo.py).  Returns (model, stack,
+    graph, X, dY); ``model`` is the DDP wrapper when ``world > 1``."""
+    g = make_graph(name, rank=rank, small=small)
+    stack = make_stack(name, conv_cls, norm_cls, feat_dropout=feat_dropout).to(device)
+    model = stack
+    if world > 1:
+        ids = [device.index] if torch.device(device).type == "cuda" else None
+        model = torch.nn.parallel.DistributedDataParallel(stack, device_ids=ids)
+    X, dY = make_inputs(name, g.num_nodes(), device, seed=3 + rank)
+    return model, stack, g, X, dY

@@ -1,0 +1,167 @@
+"""Edge-cut layer (sirgcn.dist) on the GPU in one process, one thread per rank (tests/thread_comm.py):
+the one-launch backward (``sir_edge_agg_bwd``: dQ and dK waves in one grid, then the reverse halo
+exchange) and the autocast layer ``DistSIRConvFunction16`` (16-bit K_ext rows, edge passes and
+both exchanges in the 16-bit storage type).
+
+Tolerances: the one-launch backward is held BIT-EQUAL to the two-pass form (the same per-row
+fp32 sums in the same order; MEAN divides G by the local in-degree first, as the single-GPU layer
+does).  The 16-bit layer: relative L2 against the fp64 truth within 2e-2 (bf16) /
+1e-2 (fp16), or no worse than 1.25x the reference's own AMP dataflow (``oracle.SIRConvRef`` under
+the same autocast, single process) — the halo adds one 16-bit rounding per received dK row.
+"""
+import pytest
+import torch
+from torch import nn
+
+import oracle
+from conftest import rel_err
+
+from sirgcn import _native
+from sirgcn.conv import EdgeAggregate, SIRConv
+from sirgcn.dist import DistGraph, DistSIRConv, DistSIRConvFunction, DistSIRConvFunction16, partition_rows
+from sirgcn.graph import Graph
+from sirgcn.synth import powerlaw_edges
+from thread_comm import FakeCtx, ThreadComm, run_ranks
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DT = {"bf16": torch.bfloat16, "f16": torch.float16}
+TOL = {"bf16": 2e-2, "f16": 1e-2}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X box"
+    _native.load()
+
+
+def _problem(V, E, d, H, O, agg, seed=6):
+    src, dst = powerlaw_edges(V, E, 0.8, seed=seed)
+    X = torch.randn(V, d, generator=torch.Generator().manual_seed(1)).to(DEV)
+    dY = torch.randn(V, O, generator=torch.Generator().manual_seed(2)).to(DEV)
+    torch.manual_seed(3)
+    conv = SIRConv(d, H, O, nn.LeakyReLU(0.2), 0, agg_type=agg).to(DEV)
+    w = [conv.linear_query.weight.detach(), conv.linear_query.bias.detach(), conv.linear_key.weight.detach(),
+         conv.linear_relation.weight.detach(), conv.linear_relation.bias.detach()]
+    return src, dst, X, dY, conv, w
+
+
+def _ranks(world, src, dst, V, fn):
+    comms = ThreadComm.make(world)
+    bounds = partition_rows(torch.bincount(dst, minlength=V), world)
+    return run_ranks(world, lambda r: fn(r, DistGraph(src, dst, V, bounds, r, world, DEV, group=comms[r]),
+                                         comms[r]))
+
+
+@pytest.mark.parametrize("world,agg", [(2, "sum"), (3, "sym"), (2, "mean"), (4, "sum")])
+def test_one_launch_backward_bit_equal_to_two_pass(world, agg, monkeypatch):
+    V, E, H = 3000, 60000, 256   # sign-mask mode needs 128 < H (sir_mask_words)
+    src, dst, X, dY, conv, w = _problem(V, E, H, H, H, agg)
+    launches = []
+    orig = _native.edge_agg_bwd
+
+    def spy(*a, **k):
+        launches.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(_native, "edge_agg_bwd", spy)
+
+    def run(dual):
+        monkeypatch.setattr(EdgeAggregate, "dual", dual)
+
+        def fn(r, dg, comm):
+            ctx = FakeCtx((True,) * 6 + (False,) * 7)
+            sl = slice(dg.row_begin, dg.row_end)
+            with torch.no_grad():
+                Y = DistSIRConvFunction.forward(ctx, X[sl], *w, dg, agg, _native.ACT_LEAKY, 0.2, _native, True)
+                g = DistSIRConvFunction.backward(ctx, dY[sl])
+            torch.cuda.synchronize()
+            return Y, g
+        return _ranks(world, src, dst, V, fn)
+
+    one = run(True)
+    assert len(launches) == world                  # one sir_edge_agg_bwd per rank
+    two = run(False)
+    assert len(launches) == world
+    for a, b in zip(one, two):
+        assert torch.equal(a[0], b[0])
+        for ga, gb in zip(a[1], b[1]):
+            if ga is not None:
+                assert torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("world,agg", [(2, "sum"), (3, "sym"), (2, "mean")])
+def test_autocast_edge_cut_16bit_wire(world, agg, dt):
+    V, E, H = 3000, 60000, 256
+    src, dst, X, dY, conv, w = _problem(V, E, H, H, H, agg, seed=8)
+    wire = []
+
+    def fn(r, dg, comm):
+        orig = comm.all_to_all_rows
+
+        def spy(out, inp, *a, **k):
+            wire.append((out.dtype, inp.dtype))
+            return orig(out, inp, *a, **k)
+        comm.all_to_all_rows = spy
+        ctx = FakeCtx((True,) * 6 + (False,) * 8)
+        sl = slice(dg.row_begin, dg.row_end)
+        with torch.no_grad():
+            Y = DistSIRConvFunction16.forward(ctx, X[sl], *w, dg, agg, _native.ACT_LEAKY, 0.2, _native, True, True,
+                                              DT[dt])
+            g = DistSIRConvFunction16.backward(ctx, dY[sl])
+        torch.cuda.synchronize()
+        return dg.n_halo, Y, g
+
+    outs = _ranks(world, src, dst, V, fn)
+    assert all(o[0] > 0 for o in outs)
+    rows = [(a, b) for a, b in wire if a.is_floating_point]      # (sym's plan-time out-degrees are int64)
+    assert rows and all(a == DT[dt] and b == DT[dt] for a, b in rows)   # K rows out, dK rows back: 16-bit
+    assert all(o[1].dtype == DT[dt] for o in outs)
+    Y = torch.cat([o[1] for o in outs]).double().cpu()
+    dX = torch.cat([o[2][0] for o in outs]).double().cpu()
+    assert dX.dtype == torch.float64 and outs[0][2][0].dtype == torch.float32
+    grads = [sum(o[2][i].double() for o in outs).cpu() for i in range(1, 6)]
+    got = {"Y": Y, "dX": dX, **dict(zip(("dW_Q", "db_Q", "dW_K", "dW_R", "db_R"), grads))}
+    _vs_amp_reference(got, conv, src, dst, V, X, dY, w, agg, DT[dt], TOL[dt])
+
+
+def _vs_amp_reference(got, conv, src, dst, V, X, dY, w, agg, dt, tol):
+    """relL2 vs fp64 within ``tol`` or 1.25x the reference's own AMP dataflow's error."""
+    truth = oracle.layer_fwd_bwd(src, dst, V, X.cpu().double(), *[t.cpu().double() for t in w],
+                                 dY.cpu().double(), agg, "leaky", 0.2)
+    H = w[0].shape[0]
+    ref = oracle.SIRConvRef(X.shape[1], H, w[3].shape[0], nn.LeakyReLU(0.2), 0, agg_type=agg).to(DEV)
+    ref.load_state_dict(conv.state_dict())
+    xr = X.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=dt):
+        Yr = ref(Graph(src, dst, V), xr)
+    Yr.backward(dY.to(Yr.dtype))
+    amp = {"Y": Yr, "dX": xr.grad, "dW_Q": ref.linear_query.weight.grad, "db_Q": ref.linear_query.bias.grad,
+           "dW_K": ref.linear_key.weight.grad, "dW_R": ref.linear_relation.weight.grad,
+           "db_R": ref.linear_relation.bias.grad}
+    for k, v in got.items():
+        e, e_amp = rel_err(v.double().cpu(), truth[k]), rel_err(amp[k].double().cpu(), truth[k])
+        assert e <= max(tol, 1.25 * e_amp), (k, e, e_amp)
+
+
+def test_dist_layer_routes_autocast_to_the_16bit_function(monkeypatch):
+    """DistSIRConv.forward under autocast takes DistSIRConvFunction16 (world 1: no exchange) and
+    its gradients flow through Tensor.backward."""
+    V, E, H = 2000, 30000, 128
+    src, dst, X, dY, conv, w = _problem(V, E, H, H, H, "sym")
+    calls = []
+    orig = DistSIRConvFunction16.apply
+    monkeypatch.setattr(DistSIRConvFunction16, "apply", staticmethod(lambda *a: calls.append(1) or orig(*a)))
+    dg = DistGraph.from_global(src, dst, V, 0, 1, DEV)
+    layer = DistSIRConv(conv)
+    xr = X.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        Y = layer(dg, xr)
+    Y.backward(dY.to(Y.dtype))
+    assert calls == [1] and Y.dtype == torch.bfloat16 and xr.grad.dtype == torch.float32
+    got = {"Y": Y.detach(), "dX": xr.grad, "dW_Q": conv.linear_query.weight.grad,
+           "db_Q": conv.linear_query.bias.grad, "dW_K": conv.linear_key.weight.grad,
+           "dW_R": conv.linear_relation.weight.grad, "db_R": conv.linear_relation.bias.grad}
+    _vs_amp_reference({k: v.clone() for k, v in got.items()}, conv, src, dst, V, X, dY, w, "sym",
+                      torch.bfloat16, 2e-2)

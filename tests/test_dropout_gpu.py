@@ -59,11 +59,14 @@ def test_mask_statistics(p):
     assert torch.all(_mask(64, 64, 1, 1.0) == 0) and torch.all(_mask(64, 64, 1, 0.0) == 1)
 
 
-@pytest.mark.parametrize("M,K,N", [(70001, 256, 512), (3001, 128, 256), (5000, 256, 256), (2000, 300, 200),
-                                   (4099, 512, 256), (300, 64, 96)])
-def test_gemm_epilogue_applies_the_mask(M, K, N):
+@pytest.mark.parametrize("M,K,N,ntw", [(70001, 256, 512, "0"), (3001, 128, 256, "0"), (5000, 256, 256, "0"),
+                                       (2000, 300, 200, "0"), (4099, 512, 256, "0"), (300, 64, 96, "0"),
+                                       (3001, 128, 256, "1"), (5000, 256, 256, "1"), (70001, 256, 200, "1")])
+def test_gemm_epilogue_applies_the_mask(M, K, N, ntw, monkeypatch):
     """C = drop(A W^T + b) in the GEMM epilogue == sir_dropout_apply on the plain GEMM, bit for bit
-    (the shapes route to the persistent, tiled and weight-resident split-fp16 kernels)."""
+    (the shapes route to the persistent, tiled and — opted in with SIR_NT_W=1 — weight-resident
+    split-fp16 kernels)."""
+    monkeypatch.setenv("SIR_NT_W", ntw)
     g = torch.Generator(device=DEV).manual_seed(M + N)
     A = torch.randn(M, K, device=DEV, generator=g)
     W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5

@@ -268,3 +268,29 @@ def test_gemm_nt16_strided_rows_and_errors():
     with pytest.raises(RuntimeError, match="multiples of 16 B"):     # 16-bit C rows in 16-B pieces
         _native.gemm_nt16(torch.zeros(10, 256, device=DEV, dtype=torch.bfloat16),
                           _native.gemm_pack16(torch.zeros(12, 256, device=DEV), torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,K,N", [(70001, 256, 256), (3001, 128, 256), (513, 256, 200), (1, 128, 64),
+                                   (66000, 256, 128)])
+def test_gemm_nt_weight_resident_opt_in_bit_identical(M, K, N, monkeypatch):
+    """The weight-resident NT kernel (sirconv_gemm_w.hip, opt-in: SIR_NT_W=1) computes the same
+    split-fp16 products in the same order as k_gemm_nt_p: identical bits, incl. wide-range rows,
+    rows whose maximum grows along K (the exact-redo path), a strided C and a ragged last tile.
+    The weight is packed BEFORE the switch is flipped: the packed buffer carries the kernel's
+    weight image whatever the switch said at pack time."""
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-30, 30, (M, 1), device=DEV, generator=g).float())
+    if M > 300:
+        A[100:300] *= torch.exp2(torch.linspace(-20, 20, K, device=DEV))
+    W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g)
+    pk = _native.gemm_pack(W)
+    out = []
+    for w in ("0", "1"):
+        monkeypatch.setenv("SIR_NT_W", w)
+        wide = torch.full((M, N + 12), 7.0, device=DEV)
+        out.append((_native.gemm_nt(A, pk, b, out=wide[:, 4:4 + N]), wide))
+    assert torch.equal(out[0][0], out[1][0])
+    _check(out[1][0], A.double(), W.double().t(), torch.addmm(b, A, W.t()), b, f"nt_w M={M} K={K} N={N}")
+    assert torch.all(out[1][1][:, :4] == 7.0) and torch.all(out[1][1][:, 4 + N:] == 7.0)
