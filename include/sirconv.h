@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 8
+#define SIR_ABI_VERSION 9
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -250,13 +250,14 @@ int sir_edge_mlp_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
                      const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda,
                      float* pval, int32_t* parg, void* stream);
 
-/* Backward of the SUM / MEAN / SYM form (H, F <= 64): the destination pass writes dQ [rows, H] and one
- * partial [dW (FP x HP) | db (FP)] row per wave into wpart (FP = F rounded up to 32, HP = H rounded up to
- * 8; sir_edge_mlp_bwd_waves(n_items) rows of FP*HP + FP floats: sum them in row order, e.g. with
- * sir_col_sum); MEAN also writes Gm = G / deg [rows, F] for the source pass.  The source pass
+/* Backward of the SUM / MEAN / SYM form (H, F <= 256): the destination pass writes dQ [rows, H] and one
+ * partial [dW (FP x HP) | db (FP)] row per block into wpart (FP = F rounded up to 32, HP = H rounded up
+ * to 8; sir_edge_mlp_bwd_parts(n_items, H, F) rows of FP*HP + FP floats: sum them in row order, e.g.
+ * with sir_col_sum); MEAN also writes Gm = G / deg [rows, F] for the source pass.  The source pass
  * (rows = sources, col = destinations) writes dK [rows, H] from Gd (= Gm for MEAN, else G).
- * Split rows: partial = n_slots * H floats.  Deterministic (no atomics). */
-int64_t sir_edge_mlp_bwd_waves(int64_t n_items);
+ * Split rows: partial = n_slots * H floats.  Deterministic (no atomics).  (ABI 9: replaces
+ * sir_edge_mlp_bwd_waves(n_items), whose H, F <= 64 kernels these generalise.) */
+int64_t sir_edge_mlp_bwd_parts(int64_t n_items, int64_t H, int64_t F);
 int sir_edge_mlp_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
                          const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,
                          const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* G, int64_t ldg,

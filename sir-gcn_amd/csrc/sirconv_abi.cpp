@@ -344,8 +344,8 @@ static int check_mlp(const char* fn, const int32_t* rowptr, const int32_t* items
         return fail(SIR_EINVAL, fn, bwd ? "agg must be SUM, MEAN or SYM" : "agg must be SUM, MEAN, SYM or MAX");
     if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
     if (act2 != SIR_ACT_IDENTITY && act2 != SIR_ACT_RELU) return fail(SIR_EUNSUPPORTED, fn, "act2 must be IDENTITY or RELU");
-    if (H <= 0 || H % 4 != 0 || H > (bwd ? 64 : 512)) return fail(SIR_EUNSUPPORTED, fn, bwd ? "H % 4 == 0 and H <= 64" : "H % 4 == 0 and H <= 512");
-    if (F <= 0 || F > (bwd ? 64 : 256)) return fail(SIR_EUNSUPPORTED, fn, bwd ? "F <= 64" : "F <= 256");
+    if (H <= 0 || H % 4 != 0 || H > (bwd ? 256 : 512)) return fail(SIR_EUNSUPPORTED, fn, bwd ? "H % 4 == 0 and H <= 256" : "H % 4 == 0 and H <= 512");
+    if (F <= 0 || F > 256) return fail(SIR_EUNSUPPORTED, fn, "F <= 256");
     if (n_items < 0 || n_splits < 0 || n_items > INT32_MAX) return fail(SIR_EINVAL, fn, "bad item count");
     if (n_items > 0 && (rowptr == nullptr || items == nullptr || packed == nullptr || Q == nullptr || K == nullptr))
         return fail(SIR_EINVAL, fn, "NULL buffer");
@@ -391,7 +391,10 @@ int sir_edge_mlp_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
     return finish(fn, sir::run_mlp_fwd(a, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
 }
 
-int64_t sir_edge_mlp_bwd_waves(int64_t n_items) { return sir::mlp_bwd_waves(n_items); }
+int64_t sir_edge_mlp_bwd_parts(int64_t n_items, int64_t H, int64_t F) {
+    if (H <= 0 || F <= 0 || H > 256 || F > 256) return 0;
+    return sir::mlp_bwd_blocks(n_items, (int)H, (int)F);
+}
 
 int sir_edge_mlp_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
                          const int32_t* splits, int64_t n_splits, int64_t H, int64_t F,

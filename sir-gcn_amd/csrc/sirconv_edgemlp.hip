@@ -15,7 +15,7 @@
 // accumulation) with W streamed from L2 in fragment order, and reduces m_e in registers — no
 // [E, *] tensor in HBM.
 //
-// Backward of the sum family (H, F <= 64): a destination pass (dQ, and per-wave partial dW / db of
+// Backward of the sum family (H, F <= 256): a destination pass (dQ, and per-block partial dW / db of
 // the layer) and a source pass (dK), each recomputing z, a, h for its edges:
 //   dm_e = g[v] * c_e,  dh_e = act2'(h_e) dm_e,  da_e = dh_e W,  dz_e = act1'(z_e) da_e,
 //   dQ[v] = sum dz_e,  dK[u] = sum dz_e,  dW = sum dh_e (x) a_e,  db = sum dh_e.
@@ -228,10 +228,14 @@ __global__ void k_mlp_sum_combine(const int4* __restrict__ splits, int F, const 
 }
 
 // ------------------------------------------------------------------------------ backward (sum family)
-// LDS image of one 32-edge tile: z (pre-activation of act1), a = act1(z), g-rows (source pass: the
-// gathered G[v] rows; destination pass: unused) and dh.  HP, FP <= 64.
-template <int ACT1, int ACT2, int RED, bool DST>
-__global__ void __launch_bounds__(64)
+// One block of NW waves per work item (persistent over items) shares the LDS image of a 32-edge
+// tile: z (pre-activation of act1) and a = act1(z) [32 x 32 NW], dh [32 x 32 NW], and the g rows
+// (source pass: the gathered G[v] rows; destination pass: the one row g[v]).  H, F <= 32 NW.  The
+// waves split the work by 32-wide tiles — h / dh: feature tile w; da / dz and the dQ / dK columns:
+// a-column tile w; the block's partial dW: tiles (tf, th) = w, w + NW, ... — so no two waves ever
+// write the same accumulator and the per-block partials are summed in block order afterwards.
+template <int ACT1, int ACT2, int RED, bool DST, int NW>
+__global__ void __launch_bounds__(64 * NW)
 k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
           int64_t n_items, const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
           const float* __restrict__ G, int64_t ldg, const float* __restrict__ norm_row,
@@ -239,37 +243,33 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
           const float4* __restrict__ Wp, const float* __restrict__ W, const float* __restrict__ bias,
           float* __restrict__ out, int64_t ldo, float* __restrict__ partial, float* __restrict__ Gm,
           float* __restrict__ wpart) {
-    constexpr int NT = 2;                        // FP / 32 <= 2 and HP / 32 <= 2
-    __shared__ float sZ[32 * 65], sA[32 * 65], sG[32 * 65], sDH[32 * 65], sC[32];
-    const int pitch = 65;
-    const int l = threadIdx.x;
+    constexpr int P = 32 * NW + 1;               // row pitch of every LDS tile (odd: conflict-free columns)
+    constexpr int DWW = NW;                      // dW tiles per wave: (NW x NW tiles) / NW waves
+    __shared__ float sZ[32 * P], sA[32 * P], sDH[32 * P], sG[DST ? P : 32 * P], sC[32];
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nt = (F + 31) / 32, nh = (HP + 31) / 32;
     const int nq = HP / 8;
-    // per-wave partial dW [FP x HPad] (destination pass): tiles (tf, th) and db
-    mf16 dw[NT][NT];
-    float db[NT];
+    const int tf_own = w, th_own = w;            // this wave's h / dh tile and da / dz tile
+    mf16 dw[DWW];
+    float db = 0.f;
 #pragma unroll
-    for (int a = 0; a < NT; ++a) {
-        db[a] = 0.f;
+    for (int d = 0; d < DWW; ++d)
 #pragma unroll
-        for (int b = 0; b < NT; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) dw[a][b][r] = 0.f;
-    }
-    float bb[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int n = 32 * t + (l & 31);
-        bb[t] = (bias != nullptr && n < F) ? bias[n] : 0.f;
-    }
-    for (int64_t w = blockIdx.x; w < n_items; w += gridDim.x) {
-        const int4 it = uniform_item(items, w);
+        for (int r = 0; r < 16; ++r) dw[d][r] = 0.f;
+    const int nown = 32 * tf_own + (l & 31);     // this lane's feature column in the h / dh tile
+    const float bb = (bias != nullptr && nown < F) ? bias[nown] : 0.f;
+    const int kk = 32 * th_own + (l & 31);       // this lane's a column in the da / dz tile
+    for (int64_t wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
+        const int4 it = uniform_item(items, wi);
         const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
         const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
-        // row-side vector: destination pass: Q[v] and g = G[v] (mean: / deg); source pass: K[u]
+        // row-side vector: destination pass Q[v], source pass K[u]; 4 columns per lane
         const float* rp = DST ? Q + (int64_t)row * ldq : K + (int64_t)row * ldk;
-        float gl = 0.f;                          // destination pass: g[n] of column n = l (F <= 64)
-        if (DST) {
+        const int k4 = 4 * l;
+        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k4 < H) rv = *reinterpret_cast<const float4*>(rp + k4);
+        if (DST) {                               // g[v] (mean: / deg; the first chunk also writes Gm)
             float degf = 1.f;
             bool first = true;
             if (RED == AGG_MEAN) {
@@ -278,157 +278,146 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
                 degf = (float)(d > 1 ? d : 1);
                 first = (e0 == rs);
             }
-            if (l < F) {
-                gl = G[(int64_t)row * ldg + l];
-                if (RED == AGG_MEAN) {
-                    gl = gl / degf;
-                    if (Gm != nullptr && first) Gm[(int64_t)row * F + l] = gl;
+            for (int n = threadIdx.x; n < 32 * nt; n += 64 * NW) {
+                float g = 0.f;
+                if (n < F) {
+                    g = G[(int64_t)row * ldg + n];
+                    if (RED == AGG_MEAN) {
+                        g = g / degf;
+                        if (Gm != nullptr && first) Gm[(int64_t)row * F + n] = g;
+                    }
                 }
+                sG[n] = g;
             }
         }
-        float dacc[NT] = {0.f, 0.f};             // dQ / dK of column k = 32 t + l%32 (this lane's rows)
+        float dacc = 0.f;                        // dQ / dK of column kk (this lane's rows)
         for (int t0 = e0; t0 < e1; t0 += 32) {
             const int nv = (e1 - t0) < 32 ? (e1 - t0) : 32;
-            // ---- stage z, a (and the source pass's gathered g rows)
-            const int k = l;                     // HP <= 64: one column per lane
-            const float rv = (k < H) ? rp[k] : 0.f;
-            for (int i = 0; i < 32; ++i) {
-                float z = 0.f, gi = 0.f;
-                if (i < nv) {
-                    const int o = col[t0 + i];
-                    if (k < H) z = DST ? rv + K[(int64_t)o * ldk + k] : Q[(int64_t)o * ldq + k] + rv;
-                    if (!DST && k < F) gi = G[(int64_t)o * ldg + k];
+            // ---- stage z, a (rows w, w + NW, ...; columns past H and rows past nv: zeros)
+            if (k4 < 32 * nh) {
+                for (int i = w; i < 32; i += NW) {
+                    float4 z = make_float4(0.f, 0.f, 0.f, 0.f), a = z;
+                    if (i < nv && k4 < H) {
+                        const int o = col[t0 + i];
+                        const float4 ov = DST ? *reinterpret_cast<const float4*>(K + (int64_t)o * ldk + k4)
+                                              : *reinterpret_cast<const float4*>(Q + (int64_t)o * ldq + k4);
+                        // z = Q[v] + K[u] in the reference's operand order either way
+                        z = DST ? make_float4(rv.x + ov.x, rv.y + ov.y, rv.z + ov.z, rv.w + ov.w)
+                                : make_float4(ov.x + rv.x, ov.y + rv.y, ov.z + rv.z, ov.w + rv.w);
+                        a = make_float4(act_f<ACT1>(z.x, slope), act_f<ACT1>(z.y, slope), act_f<ACT1>(z.z, slope),
+                                        act_f<ACT1>(z.w, slope));
+                    }
+                    float* dz = sZ + i * P + k4;
+                    float* da = sA + i * P + k4;
+                    dz[0] = z.x; dz[1] = z.y; dz[2] = z.z; dz[3] = z.w;
+                    da[0] = a.x; da[1] = a.y; da[2] = a.z; da[3] = a.w;
                 }
-                if (k < HP) { sZ[i * pitch + k] = z; sA[i * pitch + k] = (i < nv) ? act_f<ACT1>(z, slope) : 0.f; }
-                if (!DST && k < 64) sG[i * pitch + k] = gi;
             }
-            if (l < 32) {
+            if (!DST) {                          // the gathered g rows of the tile's destinations
+                for (int i = w; i < 32; i += NW) {
+                    const int o = (i < nv) ? col[t0 + i] : 0;
+                    for (int n = l; n < 32 * nt; n += 64)
+                        sG[i * P + n] = (i < nv && n < F) ? G[(int64_t)o * ldg + n] : 0.f;
+                }
+            }
+            if (threadIdx.x < 32) {
                 float c = 0.f;
-                if (l < nv) {
+                if ((int)threadIdx.x < nv) {
                     if (RED == AGG_SYM) {
-                        const int o = col[t0 + l];
+                        const int o = col[t0 + threadIdx.x];
                         c = DST ? norm_col[o] * nr : nr * norm_col[o];     // out_norm[u] * in_norm[v]
                     } else {
                         c = 1.f;
                     }
                 }
-                sC[l] = c;
+                sC[threadIdx.x] = c;
             }
             __syncthreads();
-            // ---- h = a W^T + b (MFMA), dh = act2'(h) * (g * c), into sDH[i][n]
-            mf16 acc[NT];
+            // ---- h = a W^T + b (MFMA, this wave's feature tile), dh = act2'(h) * (g * c) -> sDH[i][n]
+            if (tf_own < nt) {
+                mf16 acc;
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-            const float* arow = sA + (l & 31) * pitch + (l >> 5);
-            for (int q = 0; q < nq; ++q) {
-                float av[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) av[j] = arow[8 * q + 2 * j];
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    if (t < nt) {
-                        const float4 b4 = Wp[(int64_t)(t * nq + q) * 64 + l];
-                        acc[t] = mfma32(av[0], b4.x, acc[t]);
-                        acc[t] = mfma32(av[1], b4.y, acc[t]);
-                        acc[t] = mfma32(av[2], b4.z, acc[t]);
-                        acc[t] = mfma32(av[3], b4.w, acc[t]);
-                    }
+                for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+                const float* arow = sA + (l & 31) * P + (l >> 5);
+                for (int q = 0; q < nq; ++q) {
+                    const float4 b4 = Wp[(int64_t)(tf_own * nq + q) * 64 + l];
+                    acc = mfma32(arow[8 * q + 0], b4.x, acc);
+                    acc = mfma32(arow[8 * q + 2], b4.y, acc);
+                    acc = mfma32(arow[8 * q + 4], b4.z, acc);
+                    acc = mfma32(arow[8 * q + 6], b4.w, acc);
                 }
-            }
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const int n = 32 * t + (l & 31);
-                // g of column n: destination pass from the row vector (lane n holds it), source pass per edge
-                const float gn = __shfl(gl, n & 63);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int i = drow(r, l);
                     float dh = 0.f;
-                    if (t < nt && i < nv && n < F) {
-                        const float gi = DST ? gn : sG[i * pitch + n];
+                    if (i < nv && nown < F) {
+                        const float gi = DST ? sG[nown] : sG[i * P + nown];
                         const float dm = gi * sC[i];                 // autograd of c * m: grad * c
-                        dh = dsig<ACT2>(acc[t][r] + bb[t], dm, slope);
+                        dh = dsig<ACT2>(acc[r] + bb, dm, slope);
                     }
-                    if (t < nt) sDH[i * pitch + n] = dh;
-                    if (DST) db[t] += dh;
+                    sDH[i * P + nown] = dh;
+                    if (DST) db += dh;
                 }
             }
             __syncthreads();
             // ---- destination pass: dW[n][k] += sum_i dh[i][n] a[i][k]  (K = edges, 2 per MFMA)
             if (DST) {
 #pragma unroll
-                for (int tf = 0; tf < NT; ++tf)
-#pragma unroll
-                    for (int th = 0; th < NT; ++th) {
-                        if (tf < nt && th < nh) {
-                            for (int s = 0; s < 16; ++s) {
-                                const int i = 2 * s + (l >> 5);
-                                const float av = sDH[i * pitch + 32 * tf + (l & 31)];
-                                const float bv = sA[i * pitch + 32 * th + (l & 31)];
-                                dw[tf][th] = mfma32(av, bv, dw[tf][th]);
-                            }
+                for (int d = 0; d < DWW; ++d) {
+                    const int idx = w + NW * d;
+                    const int tf = idx / NW, th = idx % NW;
+                    if (tf < nt && th < nh) {
+                        for (int s2 = 0; s2 < 16; ++s2) {
+                            const int i = 2 * s2 + (l >> 5);
+                            dw[d] = mfma32(sDH[i * P + 32 * tf + (l & 31)], sA[i * P + 32 * th + (l & 31)], dw[d]);
                         }
                     }
+                }
             }
             // ---- da[i][k] = sum_n dh[i][n] W[n][k]  (K = features), dz = act1'(z) da, summed per lane
+            if (th_own < nh) {
+                mf16 da;
 #pragma unroll
-            for (int th = 0; th < NT; ++th) {
-                if (th < nh) {
-                    mf16 da;
+                for (int r = 0; r < 16; ++r) da[r] = 0.f;
+                for (int s2 = 0; s2 < 16 * nt; ++s2) {
+                    const int n = 2 * s2 + (l >> 5);
+                    const float bv = (n < F && kk < H) ? W[(int64_t)n * H + kk] : 0.f;
+                    da = mfma32(sDH[(l & 31) * P + n], bv, da);
+                }
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) da[r] = 0.f;
-                    const int kk = 32 * th + (l & 31);
-                    for (int s = 0; s < (nt * 32) / 2; ++s) {
-                        const int n = 2 * s + (l >> 5);
-                        const float av = sDH[(l & 31) * pitch + n];
-                        const float bv = (n < F && kk < H) ? W[(int64_t)n * H + kk] : 0.f;
-                        da = mfma32(av, bv, da);
-                    }
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int i = drow(r, l);
-                        if (i < nv && kk < H) dacc[th] += dsig<ACT1>(sZ[i * pitch + kk], da[r], slope);
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    const int i = drow(r, l);
+                    if (i < nv && kk < H) dacc += dsig<ACT1>(sZ[i * P + kk], da[r], slope);
                 }
             }
             __syncthreads();
         }
         // ---- dQ[v] (destination pass) / dK[u] (source pass): combine the half-waves, store
-#pragma unroll
-        for (int th = 0; th < NT; ++th) {
-            const float other = __shfl_xor(dacc[th], 32);
-            const float v = dacc[th] + other;
-            const int kk = 32 * th + (l & 31);
-            if (th < nh && l < 32 && kk < H) {
-                if (slot < 0) out[(int64_t)row * ldo + kk] = v;
-                else partial[(int64_t)slot * H + kk] = v;
-            }
+        const float v = dacc + __shfl_xor(dacc, 32);
+        if (th_own < nh && l < 32 && kk < H) {
+            if (slot < 0) out[(int64_t)row * ldo + kk] = v;
+            else partial[(int64_t)slot * H + kk] = v;
         }
     }
-    if (DST) {   // this wave's partial dW [FP x HP] (row-major n, k) and db [FP]
+    if (DST) {   // this block's partial dW [FP x HP] (row-major n, k) and db [FP]
         const int FP = nt * 32;
         const int64_t stride = (int64_t)FP * HP + FP;
         float* wp = wpart + (int64_t)blockIdx.x * stride;
 #pragma unroll
-        for (int tf = 0; tf < NT; ++tf)
+        for (int d = 0; d < DWW; ++d) {
+            const int idx = w + NW * d;
+            const int tf = idx / NW, th = idx % NW;
+            if (tf < nt && th < nh) {
 #pragma unroll
-            for (int th = 0; th < NT; ++th) {
-                if (tf < nt && th < nh) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int n = 32 * tf + drow(r, l);      // MFMA rows = n, columns = k
-                        const int k = 32 * th + (l & 31);
-                        if (k < HP) wp[(int64_t)n * HP + k] = dw[tf][th][r];
-                    }
+                for (int r = 0; r < 16; ++r) {
+                    const int n = 32 * tf + drow(r, l);      // MFMA rows = n, columns = k
+                    const int k = 32 * th + (l & 31);
+                    if (k < HP) wp[(int64_t)n * HP + k] = dw[d][r];
                 }
             }
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const float v = db[t] + __shfl_xor(db[t], 32);
-            if (t < nt && l < 32) wp[(int64_t)FP * HP + 32 * t + l] = v;
         }
+        const float v = db + __shfl_xor(db, 32);
+        if (tf_own < nt && l < 32) wp[(int64_t)FP * HP + nown] = v;
     }
 }
 
@@ -458,12 +447,25 @@ hipError_t mlp_fwd_red(int red, int nt, dim3 grid, size_t lds, hipStream_t st, c
     }
 }
 
+// waves per block: the larger of the feature / a-column tile counts (H, F <= 32 NW)
+int mlp_bwd_nw(int H, int F) {
+    const int HP = (H + 7) / 8 * 8;
+    const int t = (F + 31) / 32 > (HP + 31) / 32 ? (F + 31) / 32 : (HP + 31) / 32;
+    return t <= 2 ? 2 : (t <= 4 ? 4 : 8);
+}
+
 template <int ACT1, int ACT2, int RED, bool DST>
 hipError_t mlp_bwd_launch(dim3 grid, hipStream_t st, const EdgeMlpArgs& a) {
-    hipLaunchKernelGGL((k_mlp_bwd<ACT1, ACT2, RED, DST>), grid, dim3(64), 0, st, a.rowptr, a.col,
-                       reinterpret_cast<const int4*>(a.items), a.n_items, a.Q, a.ldq, a.K, a.ldk, a.G, a.ldg,
-                       a.norm_row, a.norm_col, a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.W,
-                       a.bias, a.out, a.ldo, a.pval, a.Gm, a.wpart);
+#define SIR_MLP_BWD(NWV)                                                                                            \
+    hipLaunchKernelGGL((k_mlp_bwd<ACT1, ACT2, RED, DST, NWV>), grid, dim3(64 * NWV), 0, st, a.rowptr, a.col,           \
+                       reinterpret_cast<const int4*>(a.items), a.n_items, a.Q, a.ldq, a.K, a.ldk, a.G, a.ldg,          \
+                       a.norm_row, a.norm_col, a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.W,   \
+                       a.bias, a.out, a.ldo, a.pval, a.Gm, a.wpart)
+    const int nw = mlp_bwd_nw(a.H, a.F);
+    if (nw == 2) SIR_MLP_BWD(2);
+    else if (nw == 4) SIR_MLP_BWD(4);
+    else SIR_MLP_BWD(8);
+#undef SIR_MLP_BWD
     return hipGetLastError();
 }
 
@@ -533,11 +535,16 @@ hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStr
     return hipSuccess;
 }
 
-int mlp_bwd_waves(int64_t n_items) { return (int)(n_items < 2048 ? (n_items > 0 ? n_items : 1) : 2048); }
+// blocks of the backward grid = rows of the destination pass's dW partials: 2048 waves' worth of
+// blocks (about 8 waves per CU), fewer when there are fewer work items
+int mlp_bwd_blocks(int64_t n_items, int H, int F) {
+    const int cap = 2048 / mlp_bwd_nw(H, F);
+    return (int)(n_items < cap ? (n_items > 0 ? n_items : 1) : cap);
+}
 
 hipError_t run_mlp_bwd(const EdgeMlpArgs& a, bool dst, int red, int act1, int act2, hipStream_t st) {
     if (a.n_items > 0) {
-        const dim3 grid((unsigned)mlp_bwd_waves(a.n_items));
+        const dim3 grid((unsigned)mlp_bwd_blocks(a.n_items, a.H, a.F));
         hipError_t err = by_acts(act1, act2, [&](auto A1, auto A2) {
             return dst ? mlp_bwd_red<decltype(A1)::value, decltype(A2)::value, true>(red, grid, st, a)
                        : mlp_bwd_red<decltype(A1)::value, decltype(A2)::value, false>(red, grid, st, a);

@@ -137,7 +137,7 @@ struct EdgeMlpArgs {
 int64_t mlp_pack_floats(int H, int F);
 hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t st);
 hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st);
-int mlp_bwd_waves(int64_t n_items);
+int mlp_bwd_blocks(int64_t n_items, int H, int F);
 hipError_t run_mlp_bwd(const EdgeMlpArgs& a, bool dst, int red, int act1, int act2, hipStream_t st);
 
 // projection GEMMs, sirconv_gemm.hip

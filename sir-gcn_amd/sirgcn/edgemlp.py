@@ -2,8 +2,9 @@
 whose message runs a Linear on every edge, without any [E, *] tensor in the forward.
 
 * ``Sequential(act1, Linear(H, F), act2)`` sigma (``dictionary-lookup/model.py:17``, used through
-  ``conv.py:45``) with sum / mean / sym: :class:`EdgeMLPSum` — forward and backward fused (the
-  backward kernels cover H, F <= 64; the config-1 shape is H = F = 64).
+  ``conv.py:45``) with sum / mean / sym: :class:`EdgeMLPSum` — forward and backward fused for
+  H, F <= 256 (the config-1 shape is H = F = 64; the DictionaryLookup sweep reaches H = F = 200,
+  ``dictionary-lookup/README.md:8``).
 * ``agg_type='max'`` (``conv.py:46-47``: ``linear_relation`` per edge, DGL ``fn.max``):
   :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge); the backward
   recomputes the edge activations once (the gradient needs the arg edges' activations, dW_R is an
@@ -46,7 +47,7 @@ def seq_sigma(act, H):
     c2 = _elementwise_code(a2)
     if c1 is None or c2 is None or c2[0] not in (_native.ACT_RELU, _native.ACT_IDENTITY):
         return None
-    if not isinstance(lin, nn.Linear) or lin.in_features != H or H % 4 or H > 64 or lin.out_features > 64:
+    if not isinstance(lin, nn.Linear) or lin.in_features != H or H % 4 or H > 256 or lin.out_features > 256:
         return None
     return c1[0], c1[1], lin, c2[0]
 
@@ -116,7 +117,7 @@ class EdgeMLPSum(torch.autograd.Function):
         Q, K = QK[:, :H], QK[:, H:]
         dQK = torch.empty_like(QK)
         d, s = plan.dst, plan.src
-        waves = lib.sir_edge_mlp_bwd_waves(d.n_items)
+        waves = lib.sir_edge_mlp_bwd_parts(d.n_items, H, Fo)
         FP, HP = (Fo + 31) // 32 * 32, (H + 7) // 8 * 8
         wpart = torch.empty((waves, FP * HP + FP), device=dev, dtype=torch.float32)
         part = torch.empty((max(d.n_slots, s.n_slots, 1) * H,), device=dev, dtype=torch.float32)

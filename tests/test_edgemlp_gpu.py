@@ -62,10 +62,22 @@ def _oracle(m, src, dst, V, X, dY, agg, act, dtype):
     return r
 
 
+def _no_generic(monkeypatch):
+    """Make the edge-materialised path (sirgcn.generic) fail if the layer reaches it."""
+    import sirgcn.generic
+
+    def boom(*a, **k):
+        raise AssertionError("generic_forward reached: the fused edge-MLP kernels should serve this shape")
+    monkeypatch.setattr(sirgcn.generic, "generic_forward", boom)
+
+
 @pytest.mark.parametrize("chunk", [256, 4])
 @pytest.mark.parametrize("agg", ["sum", "mean", "sym"])
-@pytest.mark.parametrize("H,Fo", [(64, 64), (32, 48), (16, 16)])
-def test_seq_sigma_fused_vs_oracle(agg, H, Fo, chunk):
+@pytest.mark.parametrize("H,Fo", [(64, 64), (32, 48), (16, 16), (200, 200), (128, 96), (100, 140), (256, 256)])
+def test_seq_sigma_fused_vs_oracle(agg, H, Fo, chunk, monkeypatch):
+    """H, F up to 256 (the DictionaryLookup sweep's nhidden = 4n reaches 200 at n = 50,
+    dictionary-lookup/README.md:8) on the fused kernels — one to eight waves per block."""
+    _no_generic(monkeypatch)
     src, dst, V, gen = _graph(H + Fo + len(agg))
     d, O = 24, 20
     X, dY = torch.randn(V, d, generator=gen), torch.randn(V, O, generator=gen)
@@ -145,3 +157,28 @@ def test_fused_max_s1_scale_fits_and_is_deterministic():
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     assert torch.isfinite(outs[0]).all()
+
+
+@pytest.mark.parametrize("n", [10, 17, 50])
+def test_dictionary_lookup_sweep_shapes_fused(n, monkeypatch):
+    """The DictionaryLookup model at nhidden = 4n (dictionary-lookup/README.md:8, model.py:17,20:
+    SIRConv(H, H, H) with sigma = Sequential(ReLU, Linear(H, H), ReLU), sum) on its own bipartite
+    batch graph: fused forward and backward (no generic path) against the fp32 / fp64 oracle."""
+    from sirgcn.synth import dictionary_lookup_batch
+    _no_generic(monkeypatch)
+    H = 4 * n
+    g = dictionary_lookup_batch(n, 4)
+    V = g.num_nodes()
+    src, dst = g.edges()
+    gen = torch.Generator().manual_seed(n)
+    X, dY = torch.randn(V, H, generator=gen), torch.randn(V, H, generator=gen)
+    torch.manual_seed(n)
+    sigma = nn.Sequential(nn.ReLU(inplace=True), nn.Linear(H, H), nn.ReLU(inplace=True))
+    m = SIRConv(H, H, H, sigma, 0, agg_type="sum").to(DEV)
+    got = _run(m, g, X, dY)
+    r32 = _oracle(m, src, dst, V, X, dY, "sum", m.activation, torch.float32)
+    r64 = _oracle(m, src, dst, V, X, dY, "sum", m.activation, torch.float64)
+    for k, kr in (("Y", "Y"), ("dX", "dX"), ("linear_query.weight", "dW_Q"), ("linear_key.weight", "dW_K"),
+                  ("linear_relation.weight", "dW_R"), ("activation.1.weight", "act.1.weight"),
+                  ("activation.1.bias", "act.1.bias")):
+        assert_parity(got[k], r32[kr], r64[kr], 1e-5, f"dictionary n={n} {k}", strict=(k == "Y"))

@@ -96,9 +96,10 @@ int main() {
     expect("mlp_fwd: MAX needs arg", sir_edge_mlp_fwd(p, p, p, 1, nullptr, 0, 64, 64, f, 64, f, 64, nullptr, nullptr,
                                                       SIR_AGG_MAX, 1, 0.f, 0, v, nullptr, f, 64, nullptr, 64, nullptr,
                                                       nullptr, nullptr), SIR_EINVAL, "arg");
-    expect("mlp_bwd_dst: H > 64", sir_edge_mlp_bwd_dst(p, p, p, 1, nullptr, 0, 128, 64, f, 128, f, 128, f, 64, nullptr,
-                                                       nullptr, 0, 1, 0.f, 1, v, f, nullptr, f, 128, nullptr, nullptr,
-                                                       f, nullptr), SIR_EUNSUPPORTED, "H");
+    expect("mlp_bwd_dst: H > 256", sir_edge_mlp_bwd_dst(p, p, p, 1, nullptr, 0, 260, 64, f, 260, f, 260, f, 64, nullptr,
+                                                        nullptr, 0, 1, 0.f, 1, v, f, nullptr, f, 260, nullptr, nullptr,
+                                                        f, nullptr), SIR_EUNSUPPORTED, "H");
+    expect("mlp_bwd_parts: range", (int)sir_edge_mlp_bwd_parts(100, 64, 300), 0);
     expect("mlp_bwd_src: MAX refused", sir_edge_mlp_bwd_src(p, p, p, 1, nullptr, 0, 64, 64, f, 64, f, 64, f, 64, nullptr,
                                                             nullptr, SIR_AGG_MAX, 1, 0.f, 1, v, f, nullptr, f, 64,
                                                             nullptr, nullptr), SIR_EINVAL, "agg");
