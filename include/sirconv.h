@@ -237,7 +237,7 @@ int sir_segment_max_bwd(const int32_t* items, int64_t n_items, int64_t F, const 
  * Linear(H, F), act2) (dictionary-lookup/model.py:17) and conv.py:46-47 (agg_type='max': W = W_R,
  * act2 = identity).  No per-edge tensor is written.  fp32 throughout (MFMA fp32 products).
  * W: [F, H] row-major (an nn.Linear weight), packed once by sir_edge_mlp_pack.  Limits: H % 4 == 0,
- * H <= 512, F <= 256, Q/K 16-B aligned rows.  act2 in {IDENTITY, RELU}.  Split rows: pval
+ * H <= 512, F <= 512, Q/K 16-B aligned rows.  act2 in {IDENTITY, RELU}.  Split rows: pval
  * (n_slots * F floats) and, for MAX, parg (n_slots * F ints).
  * ------------------------------------------------------------------------------------------- */
 #define SIR_AGG_MAX 3
@@ -270,6 +270,25 @@ int sir_edge_mlp_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          const float* norm_row, const float* norm_col, int agg, int act1, float slope, int act2,
                          const void* packed, const float* W, const float* bias, float* dK, int64_t lddk,
                          float* partial, void* stream);
+
+/* Backward of the SIR_AGG_MAX form (conv.py:46-47, act2 = identity, W = W_R [O, H]) for H, O <= 256,
+ * without any [E, *] tensor: dm_e[o] = dY[v][o] if edge e is the first arg-max edge of (v, o) (arg
+ * from sir_edge_mlp_fwd: dst-CSR positions, -1 for empty rows), else 0; then, recomputing z and a
+ * per edge, da = dm W, dz = act1'(z) da.  The destination pass writes dQ [rows, H] and one partial
+ * [dW_R (OP x HP) | db_R (OP)] row per block into wpart (sir_edge_mlp_bwd_parts(n_items, H, O) rows,
+ * OP = O rounded up to 32, HP = H rounded up to 8: sum them in row order).  The source pass (rows =
+ * sources, col = destinations, perm = the source CSR's dst-CSR positions) writes dK [rows, H].
+ * Split rows: partial = n_slots * H floats.  Deterministic (no atomics). */
+int sir_edge_max_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits, int64_t H, int64_t O,
+                         const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* dY, int64_t ldy,
+                         const int32_t* arg, int64_t lda, int act1, float slope, const float* W,
+                         float* dQ, int64_t lddq, float* partial, float* wpart, void* stream);
+int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
+                         const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
+                         int64_t H, int64_t O, const float* K, int64_t ldk, const float* Q, int64_t ldq,
+                         const float* dY, int64_t ldy, const int32_t* arg, int64_t lda, int act1, float slope,
+                         const float* W, float* dK, int64_t lddk, float* partial, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * GraphNorm (models/norm.py:7-29) on a batched graph: graph b owns node rows [off[b], off[b+1])

@@ -345,7 +345,7 @@ static int check_mlp(const char* fn, const int32_t* rowptr, const int32_t* items
     if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
     if (act2 != SIR_ACT_IDENTITY && act2 != SIR_ACT_RELU) return fail(SIR_EUNSUPPORTED, fn, "act2 must be IDENTITY or RELU");
     if (H <= 0 || H % 4 != 0 || H > (bwd ? 256 : 512)) return fail(SIR_EUNSUPPORTED, fn, bwd ? "H % 4 == 0 and H <= 256" : "H % 4 == 0 and H <= 512");
-    if (F <= 0 || F > 256) return fail(SIR_EUNSUPPORTED, fn, "F <= 256");
+    if (F <= 0 || F > (bwd ? 256 : 512)) return fail(SIR_EUNSUPPORTED, fn, bwd ? "F <= 256" : "F <= 512");
     if (n_items < 0 || n_splits < 0 || n_items > INT32_MAX) return fail(SIR_EINVAL, fn, "bad item count");
     if (n_items > 0 && (rowptr == nullptr || items == nullptr || packed == nullptr || Q == nullptr || K == nullptr))
         return fail(SIR_EINVAL, fn, "NULL buffer");
@@ -358,13 +358,13 @@ static int check_mlp(const char* fn, const int32_t* rowptr, const int32_t* items
 }
 
 int64_t sir_edge_mlp_pack_bytes(int64_t H, int64_t F) {
-    if (H <= 0 || F <= 0 || H > 512 || F > 256) return 0;
+    if (H <= 0 || F <= 0 || H > 512 || F > 512) return 0;
     return sir::mlp_pack_floats((int)H, (int)F) * 4;
 }
 
 int sir_edge_mlp_pack(const float* W, int64_t H, int64_t F, void* packed, void* stream) {
     const char* fn = "sir_edge_mlp_pack";
-    if (H <= 0 || F <= 0 || H > 512 || F > 256) return fail(SIR_EINVAL, fn, "H <= 512, F <= 256");
+    if (H <= 0 || F <= 0 || H > 512 || F > 512) return fail(SIR_EINVAL, fn, "H <= 512, F <= 512");
     if (W == nullptr || packed == nullptr || !al16(packed)) return fail(SIR_EINVAL, fn, "NULL / unaligned buffer");
     return finish(fn, sir::run_mlp_pack(W, (int)H, (int)F, packed, static_cast<hipStream_t>(stream)), nullptr);
 }
@@ -436,6 +436,57 @@ int sir_edge_mlp_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
     a.slope = slope; a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.W = W; a.bias = bias;
     a.out = dK; a.ldo = lddk; a.pval = partial; a.wpart = nullptr;
     return finish(fn, sir::run_mlp_bwd(a, false, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_edge_max_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                         const int32_t* splits, int64_t n_splits, int64_t H, int64_t O,
+                         const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* dY, int64_t ldy,
+                         const int32_t* arg, int64_t lda, int act1, float slope, const float* W,
+                         float* dQ, int64_t lddq, float* partial, float* wpart, void* stream) {
+    const char* fn = "sir_edge_max_bwd_dst";
+    if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
+    if (H <= 0 || H % 4 != 0 || H > 256 || O <= 0 || O > 256) return fail(SIR_EUNSUPPORTED, fn, "H % 4 == 0, H <= 256, O <= 256");
+    if (n_items < 0 || n_splits < 0 || n_items > INT32_MAX) return fail(SIR_EINVAL, fn, "bad item count");
+    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || !al16(Q) || !al16(K))
+        return fail(SIR_EUNSUPPORTED, fn, "Q/K rows must be 16-B aligned (ld % 4 == 0, ld >= H)");
+    if (n_items > 0 && (rowptr == nullptr || items == nullptr || Q == nullptr || K == nullptr || dY == nullptr ||
+                        ldy < O || arg == nullptr || lda < O || W == nullptr || dQ == nullptr || lddq < H ||
+                        wpart == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer / leading dimension");
+    if (n_splits > 0 && (splits == nullptr || partial == nullptr)) return fail(SIR_EINVAL, fn, "split rows need partial");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.splits = splits; a.n_splits = n_splits;
+    a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.G = dY; a.ldg = ldy; a.slope = slope;
+    a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)O; a.W = W;
+    a.out = dQ; a.ldo = lddq; a.pval = partial; a.wpart = wpart; a.arg = const_cast<int*>(arg); a.lda = lda;
+    return finish(fn, sir::run_mlp_bwd(a, true, SIR_AGG_MAX, act1, SIR_ACT_IDENTITY, static_cast<hipStream_t>(stream)),
+                  nullptr);
+}
+
+int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
+                         const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
+                         int64_t H, int64_t O, const float* K, int64_t ldk, const float* Q, int64_t ldq,
+                         const float* dY, int64_t ldy, const int32_t* arg, int64_t lda, int act1, float slope,
+                         const float* W, float* dK, int64_t lddk, float* partial, void* stream) {
+    const char* fn = "sir_edge_max_bwd_src";
+    if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
+    if (H <= 0 || H % 4 != 0 || H > 256 || O <= 0 || O > 256) return fail(SIR_EUNSUPPORTED, fn, "H % 4 == 0, H <= 256, O <= 256");
+    if (n_items < 0 || n_splits < 0 || n_items > INT32_MAX) return fail(SIR_EINVAL, fn, "bad item count");
+    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || !al16(Q) || !al16(K))
+        return fail(SIR_EUNSUPPORTED, fn, "Q/K rows must be 16-B aligned (ld % 4 == 0, ld >= H)");
+    if (n_items > 0 && (rowptr_s == nullptr || items == nullptr || Q == nullptr || K == nullptr || dY == nullptr ||
+                        ldy < O || arg == nullptr || lda < O || W == nullptr || dK == nullptr || lddk < H))
+        return fail(SIR_EINVAL, fn, "NULL buffer / leading dimension");
+    if (n_items > 0 && col_s != nullptr && perm_s == nullptr) return fail(SIR_EINVAL, fn, "NULL perm");
+    if (n_splits > 0 && (splits == nullptr || partial == nullptr)) return fail(SIR_EINVAL, fn, "split rows need partial");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr_s; a.col = col_s; a.items = items; a.n_items = n_items; a.splits = splits; a.n_splits = n_splits;
+    a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.G = dY; a.ldg = ldy; a.slope = slope;
+    a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)O; a.W = W;
+    a.out = dK; a.ldo = lddk; a.pval = partial; a.wpart = nullptr; a.arg = const_cast<int*>(arg); a.lda = lda;
+    a.perm = perm_s;
+    return finish(fn, sir::run_mlp_bwd(a, false, SIR_AGG_MAX, act1, SIR_ACT_IDENTITY, static_cast<hipStream_t>(stream)),
+                  nullptr);
 }
 
 // ------------------------------------------------------------------------------ GraphNorm

@@ -19,6 +19,10 @@
 // the layer) and a source pass (dK), each recomputing z, a, h for its edges:
 //   dm_e = g[v] * c_e,  dh_e = act2'(h_e) dm_e,  da_e = dh_e W,  dz_e = act1'(z_e) da_e,
 //   dQ[v] = sum dz_e,  dK[u] = sum dz_e,  dW = sum dh_e (x) a_e,  db = sum dh_e.
+// MAX (agg_type='max', act2 = identity, W = W_R): no h is needed — dm_e[n] = dY[v][n] when e is the
+// first arg-max edge of (v, n) (the forward's arg), else 0 — and the same passes give dQ, dK and the
+// per-block partial dW_R / db_R without any [E, *] tensor (the source pass finds its edges' arg
+// status through the source CSR's perm = dst-CSR position).
 // Accumulation orders are fixed (no atomics): run-to-run deterministic.
 #include "sirconv_edge_impl.h"
 
@@ -242,10 +246,12 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
           const float* __restrict__ norm_col, float slope, int H, int HP, int F,
           const float4* __restrict__ Wp, const float* __restrict__ W, const float* __restrict__ bias,
           float* __restrict__ out, int64_t ldo, float* __restrict__ partial, float* __restrict__ Gm,
-          float* __restrict__ wpart) {
+          float* __restrict__ wpart, const int* __restrict__ argm, int64_t lda, const int* __restrict__ perm) {
     constexpr int P = 32 * NW + 1;               // row pitch of every LDS tile (odd: conflict-free columns)
     constexpr int DWW = NW;                      // dW tiles per wave: (NW x NW tiles) / NW waves
+    constexpr bool MAXR = RED == 3;              // agg max: dh = dY routed to the first arg-max edge
     __shared__ float sZ[32 * P], sA[32 * P], sDH[32 * P], sG[DST ? P : 32 * P], sC[32];
+    __shared__ int sArg[(MAXR && DST) ? P : 1];
     const int l = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nt = (F + 31) / 32, nh = (HP + 31) / 32;
@@ -288,6 +294,7 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
                     }
                 }
                 sG[n] = g;
+                if constexpr (MAXR && DST) sArg[n] = (n < F) ? argm[(int64_t)row * lda + n] : -2;
             }
         }
         float dacc = 0.f;                        // dQ / dK of column kk (this lane's rows)
@@ -316,8 +323,15 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
             if (!DST) {                          // the gathered g rows of the tile's destinations
                 for (int i = w; i < 32; i += NW) {
                     const int o = (i < nv) ? col[t0 + i] : 0;
-                    for (int n = l; n < 32 * nt; n += 64)
-                        sG[i * P + n] = (i < nv && n < F) ? G[(int64_t)o * ldg + n] : 0.f;
+                    if constexpr (MAXR) {        // dY[v] where this edge (dst-CSR position pos) is the arg-max
+                        const int pos = (i < nv) ? perm[t0 + i] : -3;
+                        for (int n = l; n < 32 * nt; n += 64)
+                            sG[i * P + n] = (i < nv && n < F && argm[(int64_t)o * lda + n] == pos)
+                                                ? G[(int64_t)o * ldg + n] : 0.f;
+                    } else {
+                        for (int n = l; n < 32 * nt; n += 64)
+                            sG[i * P + n] = (i < nv && n < F) ? G[(int64_t)o * ldg + n] : 0.f;
+                    }
                 }
             }
             if (threadIdx.x < 32) {
@@ -334,7 +348,19 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
             }
             __syncthreads();
             // ---- h = a W^T + b (MFMA, this wave's feature tile), dh = act2'(h) * (g * c) -> sDH[i][n]
-            if (tf_own < nt) {
+            if (MAXR && tf_own < nt) {           // max: dh = dm (act2 = identity, no h needed)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = drow(r, l);
+                    float dh = 0.f;
+                    if (i < nv && nown < F) {
+                        if constexpr (DST) dh = (sArg[nown] == t0 + i) ? sG[nown] : 0.f;
+                        else dh = sG[i * P + nown];
+                    }
+                    sDH[i * P + nown] = dh;
+                    if (DST) db += dh;
+                }
+            } else if (tf_own < nt) {
                 mf16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -432,7 +458,8 @@ hipError_t mlp_fwd_nt(int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeM
     if (nt <= 1) SIR_MLP_FWD(1, 1);
     else if (nt <= 2) SIR_MLP_FWD(2, 1);
     else if (nt <= 4) SIR_MLP_FWD(4, 1);
-    else SIR_MLP_FWD(4, 2);
+    else if (nt <= 8) SIR_MLP_FWD(4, 2);
+    else SIR_MLP_FWD(8, 2);                      // F <= 512 (roman-empire: H = O = 512)
 #undef SIR_MLP_FWD
     return hipGetLastError();
 }
@@ -460,7 +487,7 @@ hipError_t mlp_bwd_launch(dim3 grid, hipStream_t st, const EdgeMlpArgs& a) {
     hipLaunchKernelGGL((k_mlp_bwd<ACT1, ACT2, RED, DST, NWV>), grid, dim3(64 * NWV), 0, st, a.rowptr, a.col,           \
                        reinterpret_cast<const int4*>(a.items), a.n_items, a.Q, a.ldq, a.K, a.ldk, a.G, a.ldg,          \
                        a.norm_row, a.norm_col, a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.W,   \
-                       a.bias, a.out, a.ldo, a.pval, a.Gm, a.wpart)
+                       a.bias, a.out, a.ldo, a.pval, a.Gm, a.wpart, a.arg, a.lda, a.perm)
     const int nw = mlp_bwd_nw(a.H, a.F);
     if (nw == 2) SIR_MLP_BWD(2);
     else if (nw == 4) SIR_MLP_BWD(4);
@@ -474,7 +501,10 @@ hipError_t mlp_bwd_red(int red, dim3 grid, hipStream_t st, const EdgeMlpArgs& a)
     switch (red) {
         case AGG_SUM: return mlp_bwd_launch<ACT1, ACT2, AGG_SUM, DST>(grid, st, a);
         case AGG_MEAN: return mlp_bwd_launch<ACT1, ACT2, AGG_MEAN, DST>(grid, st, a);
-        default: return mlp_bwd_launch<ACT1, ACT2, AGG_SYM, DST>(grid, st, a);
+        case AGG_SYM: return mlp_bwd_launch<ACT1, ACT2, AGG_SYM, DST>(grid, st, a);
+        default:
+            if constexpr (ACT2 == ACT_IDENTITY) return mlp_bwd_launch<ACT1, ACT2, 3, DST>(grid, st, a);
+            else return hipErrorInvalidValue;
     }
 }
 

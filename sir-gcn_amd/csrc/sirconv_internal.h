@@ -128,7 +128,8 @@ struct EdgeMlpArgs {
     const float* W;                     // W [F, H] row-major (backward)
     const float* bias;                  // [F] or NULL
     float* out;  int64_t ldo;           // forward: [rows, F]; backward: dQ / dK [rows, H]
-    int* arg;  int64_t lda;             // forward MAX
+    int* arg;  int64_t lda;             // MAX: forward output / backward input (first arg-max edges)
+    const int* perm;                    // MAX backward, source pass: source-CSR position -> dst-CSR position
     float* pval;                        // split partials (values)
     int* parg;                          // split partials (MAX args)
     float* Gm;                          // backward destination pass, MEAN: g / deg rows [rows, F]

@@ -6,9 +6,10 @@ whose message runs a Linear on every edge, without any [E, *] tensor in the forw
   H, F <= 256 (the config-1 shape is H = F = 64; the DictionaryLookup sweep reaches H = F = 200,
   ``dictionary-lookup/README.md:8``).
 * ``agg_type='max'`` (``conv.py:46-47``: ``linear_relation`` per edge, DGL ``fn.max``):
-  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge); the backward
-  recomputes the edge activations once (the gradient needs the arg edges' activations, dW_R is an
-  edge-contracted GEMM) and runs them through the native gather / GEMM / segment kernels.
+  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge) and, for
+  H, O <= 256, fused backward (``sir_edge_max_bwd_*``: dY routed to the arg edges, z and a
+  recomputed per edge, dW_R / db_R per-block partials — no [E, *] tensor); wider layers recompute
+  the edge activations once into [E, H] buffers and run the native gather / GEMM / segment kernels.
 
 Everything is fp32; a CPU tensor or a shape outside the kernels' limits is never silently served
 by another path — :func:`seq_sigma` / :func:`max_supported` say up front which form applies.
@@ -53,7 +54,9 @@ def seq_sigma(act, H):
 
 
 def max_supported(H, O):
-    return H % 4 == 0 and H <= 512 and O <= 256
+    """The max form's fused forward: H, O <= 512 (roman-empire's H = O = 512,
+    heterophilous-datasets/README.md:8)."""
+    return H % 4 == 0 and H <= 512 and O <= 512
 
 
 def _pack(W):
@@ -167,8 +170,11 @@ class EdgeMaxLinear(torch.autograd.Function):
         QK, W, arg = ctx.saved_tensors
         plan, H, act1, slope = ctx.plan, ctx.H, ctx.act1, ctx.slope
         dY = dY.contiguous().float()
-        E = plan.dst.col.numel()
         O = W.shape[0]
+        if max_bwd_fused(H, O):
+            dQK, dW, db = _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope)
+            return dQK, dW, (db if ctx.has_b else None), None, None, None, None
+        E = plan.dst.col.numel()
         dev = dY.device
         # the arg edges' activations are needed for dW_R: recompute z_e once (no copy kept from the forward)
         Z = torch.empty((E, H), device=dev, dtype=torch.float32)
@@ -188,6 +194,44 @@ class EdgeMaxLinear(torch.autograd.Function):
         _native.segment_sum(plan.dst, dZ, dQK[:, :H], partial=part)                     # dQ
         _native.segment_sum(plan.src, dZ, dQK[:, H:], perm=plan.src.perm, partial=part)  # dK
         return dQK, dW, (db if ctx.has_b else None), None, None, None, None
+
+
+def max_bwd_fused(H, O):
+    """The max form's backward runs fused (no [E, *] tensor) for H, O <= 256."""
+    return H % 4 == 0 and H <= 256 and O <= 256
+
+
+def _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope):
+    """``sir_edge_max_bwd_dst`` (dQ, per-block dW_R / db_R partials) + ``sir_edge_max_bwd_src`` (dK):
+    dY reaches each (v, o)'s first arg-max edge only; z, a recomputed per edge."""
+    lib = _native.load()
+    P = _native._ptr
+    O = W.shape[0]
+    dev = dY.device
+    d, s = plan.dst, plan.src
+    dQK = torch.empty_like(QK)
+    Q, K = QK[:, :H], QK[:, H:]
+    parts = lib.sir_edge_mlp_bwd_parts(d.n_items, H, O)
+    OP, HP = (O + 31) // 32 * 32, (H + 7) // 8 * 8
+    wpart = torch.empty((parts, OP * HP + OP), device=dev, dtype=torch.float32)
+    part = torch.empty((max(d.n_slots, s.n_slots, 1) * H,), device=dev, dtype=torch.float32)
+    st = _native._stream(dev)
+    with _native._Timed("sir_edge_max_bwd_dst", dev):
+        rc = lib.sir_edge_max_bwd_dst(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, O,
+                                      P(Q), Q.stride(0), P(K), K.stride(0), P(dY), dY.stride(0), P(arg),
+                                      arg.stride(0), act1, float(slope), P(W), P(dQK), dQK.stride(0), P(part),
+                                      P(wpart), st)
+    _native._check(rc, lib)
+    with _native._Timed("sir_edge_max_bwd_src", dev):
+        rc = lib.sir_edge_max_bwd_src(P(s.rowptr), P(s.col), P(s.perm), P(s.items), s.n_items, P(s.splits),
+                                      s.n_splits, H, O, P(K), K.stride(0), P(Q), Q.stride(0), P(dY), dY.stride(0),
+                                      P(arg), arg.stride(0), act1, float(slope), P(W), P(dQK[:, H:]), dQK.stride(0),
+                                      P(part), st)
+    _native._check(rc, lib)
+    tot = _native.col_sum(wpart)                    # per-block partials summed in block order
+    dW = tot[:OP * HP].view(OP, HP)[:O, :H].contiguous()
+    db = tot[OP * HP:OP * HP + O].contiguous()
+    return dQK, dW, db
 
 
 def _act(z, code, slope):

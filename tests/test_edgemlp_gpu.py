@@ -101,8 +101,16 @@ def test_seq_sigma_fused_vs_oracle(agg, H, Fo, chunk, monkeypatch):
 
 @pytest.mark.parametrize("chunk", [256, 64, 4])
 @pytest.mark.parametrize("act", ["leaky", "relu", "gelu"])
-@pytest.mark.parametrize("H,O", [(256, 40), (64, 64), (300, 24)])
-def test_max_fused_vs_oracle_first_wins(act, H, O, chunk):
+@pytest.mark.parametrize("H,O", [(256, 40), (64, 64), (300, 24), (128, 256), (100, 200), (512, 512)])
+def test_max_fused_vs_oracle_first_wins(act, H, O, chunk, monkeypatch):
+    """Fused forward for H, O <= 512 (roman-empire: H = O = 512, heterophilous-datasets/README.md:8)
+    and, for H, O <= 256, the fused backward: no [E, H] gather of edge activations is allowed."""
+    from sirgcn.edgemlp import max_bwd_fused
+    _no_generic(monkeypatch)
+    if max_bwd_fused(H, O):
+        def boom(*a, **k):
+            raise AssertionError("edge-materialised max backward reached")
+        monkeypatch.setattr(_native, "edge_gather_add", boom)
     src, dst, V, gen = _graph(H + O + chunk)
     d = 32
     X, dY = torch.randn(V, d, generator=gen), torch.randn(V, O, generator=gen)

@@ -104,6 +104,10 @@ int main() {
                                                             nullptr, SIR_AGG_MAX, 1, 0.f, 1, v, f, nullptr, f, 64,
                                                             nullptr, nullptr), SIR_EINVAL, "agg");
     expect("mlp_pack_bytes: range", (int)sir_edge_mlp_pack_bytes(1024, 64), 0);
+    expect("max_bwd_dst: H > 256", sir_edge_max_bwd_dst(p, p, p, 1, nullptr, 0, 300, 64, f, 300, f, 300, f, 64, p, 64, 1,
+                                                        0.f, f, f, 300, nullptr, f, nullptr), SIR_EUNSUPPORTED, "H");
+    expect("max_bwd_src: NULL perm", sir_edge_max_bwd_src(p, p, nullptr, p, 1, nullptr, 0, 64, 64, f, 64, f, 64, f, 64,
+                                                          p, 64, 1, 0.f, f, f, 64, nullptr, nullptr), SIR_EINVAL, "perm");
     std::printf("%s: %d failure(s)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }
