@@ -299,8 +299,9 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rehearsal = not torch.cuda.is_available()
     if rehearsal:
-        if args.dist_backend != "gloo" or args.workload != "cfg4":
-            raise SystemExit("no GPU: only the cfg4 edge-cut plumbing can be rehearsed (--dist-backend gloo)")
+        if args.dist_backend != "gloo" or args.workload not in ("cfg4", "cfg5"):
+            raise SystemExit("no GPU: only the cfg4 edge-cut and cfg5 data-parallel plumbing can be rehearsed "
+                             "(--dist-backend gloo)")
         dev = torch.device("cpu")
         torch.set_num_threads(max(1, min(4, os.cpu_count() // max(world, 1))))
     else:
@@ -314,6 +315,8 @@ def main():
             dist.init_process_group("gloo")
     if args.workload == "cfg4":
         out = run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn)
+    elif rehearsal:
+        out = rehearse_stack(args, world, rank, dev, torch, dist)
     else:
         out = run_stack(args, world, rank, dev, torch, dist)
     if rank == 0:
@@ -523,6 +526,40 @@ def design_bytes(kernels, gemm, steps, ms):
     g = sum(k["hbm_bytes"] * k["launches"] for k in gemm.values()) / steps
     return {"edge_passes": e, "projections": g, "total": e + g,
             "GBps_over_step": round((e + g) / (ms * 1e-3) / 1e9, 1)}
+
+
+def rehearse_stack(args, world, rank, dev, torch, dist):
+    """cfg5 without a GPU: the same per-rank batches, DDP wrapper and gloo all-reduce as the RCCL run,
+    with the test-only CPU stand-ins of the conv / norm modules (tests/cpu_stack_modules.py): a
+    rehearsal of the launcher and the data-parallel plumbing, not a measurement."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import cpu_stack_modules as cpu
+    from sirgcn.workloads import CONFIGS, dp_replica
+    name = args.workload
+    c = CONFIGS[name]
+    p_drop = c["feat_dropout"] if args.dropout is None else args.dropout
+    model, stack, g, X, dY = dp_replica(name, rank, world, dev, cpu.SIRConv, cpu.GraphNorm, feat_dropout=p_drop)
+    X.requires_grad_(True)
+
+    def step():
+        model.zero_grad(set_to_none=True)
+        X.grad = None
+        model(g, X).backward(dY)
+
+    el, _ = rehearsal_loop(step, args.steps, args.warmup, world, dist)
+    tot = torch.tensor([g.num_edges(), g.num_nodes(), g.batch_size], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(tot)
+    E_all, V_all, B_all = (int(x) for x in tot.tolist())
+    return {"metric": "layer-edges/sec SIRConv stack fwd+bwd (E x layers / step time)",
+            "value": round(E_all * c["layers"] / (el / args.steps), 1), "unit": "edges/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{name}: {dict(c, feat_dropout=p_drop)} per rank, DDP over gloo",
+                       "V_total": V_all, "E_total": E_all, "graphs": B_all,
+                       "parallelism": f"data-parallel x{world}"},
+            "rehearsal": "CPU gloo rehearsal of the launcher / per-rank batches / DDP all-reduce plumbing with the "
+                         "test-only CPU stand-in modules (tests/cpu_stack_modules.py); measures nothing"}
 
 
 def run_stack(args, world, rank, dev, torch, dist):

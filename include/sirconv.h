@@ -48,6 +48,12 @@ enum { SIR_ACT_IDENTITY = 0, SIR_ACT_RELU = 1, SIR_ACT_LEAKY_RELU = 2, SIR_ACT_G
  * fp16 is autocast's CUDA default, bf16 is BASELINE config 2).  16-bit values are widened to fp32 on
  * load; sigma, sigma', the norm product and the accumulation run in fp32 (the reference promotes its
  * messages to fp32 before the reduction) and each output is rounded once (RNE).
+ * Deviation from the reference's AMP dataflow (stated, not hidden): autocast forms eq + ek as a 16-bit
+ * add and sigma's output in 16 bits before the norm multiply promotes it; here z = Q[v] + K[u] and
+ * sigma(z) stay fp32 (no intermediate 16-bit rounding), and the autocast layer keeps dX and the weight
+ * gradients in fp32 (the reference rounds them to the 16-bit type first).  The results are at least
+ * as accurate; parity under autocast is tolerance-level (tests/test_amp_gpu.py), never bit-level, and a
+ * GradScaler step that the reference would skip on a 16-bit overflow of dW is not skipped here.
  * 16-bit storage needs H % 4 == 0 and leading dimensions that are multiples of 4 (8-B aligned rows).
  * Norms and the `partial` workspace are fp32 in every mode. */
 enum { SIR_DTYPE_F32 = 0, SIR_DTYPE_BF16 = 1, SIR_DTYPE_F16 = 2 };

@@ -1175,6 +1175,8 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     if (gemm_nt_w_ok(N, K) && M >= SIR_NT_W_MINROWS)
         return run_gemm_nt_w(A, lda, M, K, static_cast<const char*>(packed) + gemm_pack_base_bytes(N, K), N, bias, C,
                              ldc, st, drop);
+    if (gemm_nt_g_ok(A, lda, K, N, C, ldc))
+        return run_gemm_nt_g(A, lda, M, K, packed, N, bias, C, ldc, st, drop);
     if (SIR_NT_PERSIST && N > 128 && np <= NT_P_NMAX && kfull && (kc == 4 || kc == 8 || kc == 16)) {
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;

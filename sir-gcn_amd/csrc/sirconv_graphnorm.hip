@@ -8,7 +8,8 @@
 //   backward: A = sum gy*d, G = sum gy;  gd = w*gy/std - w*d*A/(n*std^3);  Bs = sum gd;
 //             dx = gd - ms*Bs/n;  per-graph partials A/std, -mean*Bs, G for dw, dms, db
 //             (reduced over graphs by the host with the deterministic column sum).
-// The whole graph is re-read from L2 by each pass (molecule-sized graphs: a few KB).
+// The whole graph is re-read from L2 by each pass (molecule-sized graphs: a few KB), 8 rows' loads in
+// flight at a time (walk_rows).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -33,6 +34,62 @@ __device__ __forceinline__ void gst(float* __restrict__ p, const float (&s)[VW])
     else p[0] = s[0];
 }
 
+
+// Walk rows [r0, r1) in node order, RB rows' loads in flight at a time (a molecule has ~25 rows: a
+// one-load-per-iteration loop paid one memory latency per row and pass, ~40 us per launch on cfg5);
+// f(i, v) is applied in row order, so every per-graph sum keeps the reference's node order.
+constexpr int RB = 8;
+template <int VW, typename Fn>
+__device__ __forceinline__ void walk_rows(int64_t r0, int64_t r1, const float* __restrict__ base, int64_t ld, int c,
+                                          Fn f) {
+    int64_t i = r0;
+    for (; i + RB <= r1; i += RB) {
+        float v[RB][VW];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) gld<VW>(v[k], base + (i + k) * ld + c * VW);
+#pragma unroll
+        for (int k = 0; k < RB; ++k) f(i + k, v[k]);
+    }
+    if (i < r1) {
+        const int n = (int)(r1 - i);
+        float v[RB][VW];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) gld<VW>(v[k], base + (i + (k < n ? k : 0)) * ld + c * VW);
+#pragma unroll
+        for (int k = 0; k < RB; ++k)
+            if (k < n) f(i + k, v[k]);
+    }
+}
+// the same over two row-aligned arrays (X and dY)
+template <int VW, typename Fn>
+__device__ __forceinline__ void walk_rows2(int64_t r0, int64_t r1, const float* __restrict__ a, int64_t lda,
+                                           const float* __restrict__ b, int64_t ldb, int c, Fn f) {
+    int64_t i = r0;
+    for (; i + RB <= r1; i += RB) {
+        float u[RB][VW], v[RB][VW];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            gld<VW>(u[k], a + (i + k) * lda + c * VW);
+            gld<VW>(v[k], b + (i + k) * ldb + c * VW);
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k) f(i + k, u[k], v[k]);
+    }
+    if (i < r1) {
+        const int n = (int)(r1 - i);
+        float u[RB][VW], v[RB][VW];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+            const int64_t q = i + (k < n ? k : 0);
+            gld<VW>(u[k], a + q * lda + c * VW);
+            gld<VW>(v[k], b + q * ldb + c * VW);
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k)
+            if (k < n) f(i + k, u[k], v[k]);
+    }
+}
+
 template <int VW>
 __global__ void __launch_bounds__(256)
 k_gn_fwd(const int64_t* __restrict__ off, int64_t B, int F, int n_cc,
@@ -50,12 +107,10 @@ k_gn_fwd(const int64_t* __restrict__ off, int64_t B, int F, int n_cc,
     float s[VW], q[VW], t[VW], wv[VW], bv[VW], mv[VW];
 #pragma unroll
     for (int x = 0; x < VW; ++x) { s[x] = 0.f; q[x] = 0.f; }
-    for (int64_t i = r0; i < r1; ++i) {                   // norm.py:20 scatter_add_ (node order)
-        float v[VW];
-        gld<VW>(v, X + i * ldx + c * VW);
+    walk_rows<VW>(r0, r1, X, ldx, c, [&](int64_t, const float (&v)[VW]) {   // norm.py:20 scatter_add_ (node order)
 #pragma unroll
         for (int x = 0; x < VW; ++x) s[x] += v[x];
-    }
+    });
     gld<VW>(wv, w + c * VW);
     if (bias) gld<VW>(bv, bias + c * VW);
     if (ms) gld<VW>(mv, ms + c * VW);
@@ -64,30 +119,26 @@ k_gn_fwd(const int64_t* __restrict__ off, int64_t B, int F, int n_cc,
         s[x] = (r1 > r0) ? s[x] / nf : 0.f;               // norm.py:21 mean
         t[x] = ms ? s[x] * mv[x] : s[x];                  // norm.py:23 mean * mean_scale
     }
-    for (int64_t i = r0; i < r1; ++i) {                   // norm.py:26 scatter_add_(demean^2)
-        float v[VW];
-        gld<VW>(v, X + i * ldx + c * VW);
+    walk_rows<VW>(r0, r1, X, ldx, c, [&](int64_t, const float (&v)[VW]) {   // norm.py:26 scatter_add_(demean^2)
 #pragma unroll
         for (int x = 0; x < VW; ++x) {
             const float d = v[x] - t[x];
             q[x] += d * d;
         }
-    }
+    });
     float sd[VW];
 #pragma unroll
     for (int x = 0; x < VW; ++x) sd[x] = (r1 > r0) ? sqrtf(q[x] / nf + eps) : 0.f;   // norm.py:27
-    for (int64_t i = r0; i < r1; ++i) {                   // norm.py:29
-        float v[VW];
-        gld<VW>(v, X + i * ldx + c * VW);
+    walk_rows<VW>(r0, r1, X, ldx, c, [&](int64_t i, const float (&v)[VW]) {   // norm.py:29
+        float y[VW];
 #pragma unroll
         for (int x = 0; x < VW; ++x) {
             const float d = v[x] - t[x];
-            float y = wv[x] * d / sd[x];
-            if (bias) y = y + bv[x];
-            v[x] = y;
+            y[x] = wv[x] * d / sd[x];
+            if (bias) y[x] = y[x] + bv[x];
         }
-        gst<VW>(Y + i * ldy + c * VW, v);
-    }
+        gst<VW>(Y + i * ldy + c * VW, y);
+    });
     gst<VW>(mean_out + b * F + c * VW, s);
     gst<VW>(std_out + b * F + c * VW, sd);
 }
@@ -118,34 +169,26 @@ k_gn_bwd(const int64_t* __restrict__ off, int64_t B, int F, int n_cc,
     gld<VW>(sd, sdv + b * F + c * VW);
 #pragma unroll
     for (int x = 0; x < VW; ++x) { t[x] = ms ? mu[x] * mv[x] : mu[x]; A[x] = 0.f; G[x] = 0.f; Bs[x] = 0.f; }
-    for (int64_t i = r0; i < r1; ++i) {
-        float v[VW], g[VW];
-        gld<VW>(v, X + i * ldx + c * VW);
-        gld<VW>(g, dY + i * ldg + c * VW);
+    walk_rows2<VW>(r0, r1, X, ldx, dY, ldg, c, [&](int64_t, const float (&v)[VW], const float (&g)[VW]) {
 #pragma unroll
         for (int x = 0; x < VW; ++x) { A[x] += g[x] * (v[x] - t[x]); G[x] += g[x]; }
-    }
+    });
     float k1[VW], k2[VW];
 #pragma unroll
     for (int x = 0; x < VW; ++x) {
         k1[x] = wv[x] / sd[x];                                       // w / s
         k2[x] = wv[x] * A[x] / (nf * sd[x] * sd[x] * sd[x]);          // w A / (n s^3)
     }
-    for (int64_t i = r0; i < r1; ++i) {
-        float v[VW], g[VW];
-        gld<VW>(v, X + i * ldx + c * VW);
-        gld<VW>(g, dY + i * ldg + c * VW);
+    walk_rows2<VW>(r0, r1, X, ldx, dY, ldg, c, [&](int64_t, const float (&v)[VW], const float (&g)[VW]) {
 #pragma unroll
         for (int x = 0; x < VW; ++x) Bs[x] += k1[x] * g[x] - k2[x] * (v[x] - t[x]);
-    }
-    for (int64_t i = r0; i < r1; ++i) {
-        float v[VW], g[VW];
-        gld<VW>(v, X + i * ldx + c * VW);
-        gld<VW>(g, dY + i * ldg + c * VW);
+    });
+    walk_rows2<VW>(r0, r1, X, ldx, dY, ldg, c, [&](int64_t i, const float (&v)[VW], const float (&g)[VW]) {
+        float o[VW];
 #pragma unroll
-        for (int x = 0; x < VW; ++x) v[x] = (k1[x] * g[x] - k2[x] * (v[x] - t[x])) - mv[x] * Bs[x] / nf;
-        gst<VW>(dX + i * lddx + c * VW, v);
-    }
+        for (int x = 0; x < VW; ++x) o[x] = (k1[x] * g[x] - k2[x] * (v[x] - t[x])) - mv[x] * Bs[x] / nf;
+        gst<VW>(dX + i * lddx + c * VW, o);
+    });
     float pw[VW], pm[VW];
 #pragma unroll
     for (int x = 0; x < VW; ++x) {

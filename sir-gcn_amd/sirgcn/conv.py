@@ -131,11 +131,8 @@ def edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK, drop=None):
             # both passes of MEAN read g = G / deg(v) (the reference's DivBackward, rounded once to
             # the storage dtype): form it first, then the one-launch SUM backward on it is the MEAN
             # backward (bit-identical to the two-launch form, which divides inside the dQ pass)
-            deg = getattr(plan, "_deg_f", None)
-            if deg is None:
-                rp = plan.dst.rowptr
-                deg = plan._deg_f = (rp[1:] - rp[:-1]).clamp(min=1).to(torch.float32)[:, None]
-            G = (G.float() / deg).to(G.dtype) if G.dtype != torch.float32 else G / deg
+            deg = plan.in_degree_f()
+            G = torch.div(G, deg, out=torch.empty_like(G))  # fp32 math, one rounding to G's dtype, no fp32 temporary
             agg = "sum"
         _native.edge_agg_bwd(plan.dst, plan.src, G, mask, in_norm, out_norm, agg, act, slope, dQK[:, :H],
                              dQK[:, H:], _slots(plan.dst, H, G.device), _slots(plan.src, H, G.device), drop=drop)

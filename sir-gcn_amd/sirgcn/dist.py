@@ -235,7 +235,7 @@ def _edge_backward_exchange(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, 
             if dg._deg_f is None:
                 rp = dg.dst.rowptr
                 dg._deg_f = (rp[1:] - rp[:-1]).clamp(min=1).to(torch.float32)[:, None]
-            G = (G.float() / dg._deg_f).to(G.dtype) if G.dtype != torch.float32 else G / dg._deg_f
+            G = torch.div(G, dg._deg_f, out=torch.empty_like(G))   # fp32 math, one rounding to G's dtype
             agg = "sum"
         _native.edge_agg_bwd(dg.dst, dg.src, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK_ext,
                              _slots(dg.dst, H, G.device), _slots(dg.src, H, G.device))

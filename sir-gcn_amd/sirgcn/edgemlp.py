@@ -11,8 +11,12 @@ whose message runs a Linear on every edge, without any [E, *] tensor in the forw
   recomputed per edge, dW_R / db_R per-block partials — no [E, *] tensor); wider layers recompute
   the edge activations once into [E, H] buffers and run the native gather / GEMM / segment kernels.
 
-Everything is fp32; a CPU tensor or a shape outside the kernels' limits is never silently served
-by another path — :func:`seq_sigma` / :func:`max_supported` say up front which form applies.
+Everything is fp32, under autocast too: there the reference runs the per-edge Linear (and sigma)
+in 16 bits, these kernels take Q, K widened to fp32 and return the result cast back to QK's dtype —
+a stated deviation (more accurate, not bit-level AMP parity; ``tests/test_amp_gpu.py::
+test_fused_edge_mlp_forms_under_autocast``).  A CPU tensor or a shape outside the kernels' limits is
+never silently served by another path — :func:`seq_sigma` / :func:`max_supported` say up front which
+form applies.
 """
 import ctypes
 

@@ -262,6 +262,13 @@ class GraphPlan:
             self._norms["sym"] = (in_norm, out_norm)
         return self._norms["sym"]
 
+    def in_degree_f(self):
+        """fp32 [V, 1] in-degree clamped at 1 (the mean's divisor, ``fn.mean``), cached with the norms."""
+        if "deg" not in self._norms:
+            rp = self.dst.rowptr
+            self._norms["deg"] = (rp[1:] - rp[:-1]).clamp(min=1).to(torch.float32)[:, None]
+        return self._norms["deg"]
+
 
 _weak_plans = weakref.WeakKeyDictionary()
 

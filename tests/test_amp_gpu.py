@@ -224,3 +224,47 @@ def test_autocast_layer_native_nt16_large(dt, monkeypatch):
     for k, v in got.items():
         e, e_amp = rel_err(v, ref32[k]), rel_err(amp[k], ref32[k])
         assert e <= max(tol, AMP_SLACK * e_amp), f"{k}: relL2 {e:.3e} vs fp32 (reference AMP {e_amp:.3e})"
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("form", ["max", "seq"])
+def test_fused_edge_mlp_forms_under_autocast(form, dt):
+    """agg='max' (conv.py:46-47, roman-empire trains it under AMP) and the DictionaryLookup
+    Sequential sigma run their per-edge Linear inside the fused kernels in fp32 even under autocast
+    (sirgcn/edgemlp.py: stated deviation, more accurate than the reference's 16-bit per-edge Linear):
+    outputs and gradients within the AMP bar of the fp32 layer, or no worse than 1.25x the
+    reference's own AMP dataflow (oracle.SIRConvRef under the same autocast)."""
+    gen = torch.Generator().manual_seed(31 + len(dt))
+    V, E, d, H, O = 300, 2400, 32, 64, 48
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V - 10, (E,), generator=gen)
+    dst[:300] = 4                                            # a split row
+    X = torch.randn(V, d, generator=gen).to(DEV)
+    dY = torch.randn(V, O, generator=gen).to(DEV)
+    torch.manual_seed(5)
+    if form == "max":
+        act = nn.LeakyReLU(0.2)
+        m = SIRConv(d, H, O, act, 0, agg_type="max").to(DEV)
+    else:
+        act = nn.Sequential(nn.ReLU(), nn.Linear(H, H), nn.ReLU())
+        m = SIRConv(d, H, O, act, 0, agg_type="sum").to(DEV)
+    ref = oracle.SIRConvRef(d, H, O, act, 0, agg_type=m._agg_type).to(DEV)
+    ref.load_state_dict(m.state_dict())
+    g = Graph(src, dst, V)
+
+    def run(mod, amp):
+        for p in mod.parameters():
+            p.grad = None
+        x = X.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=DT[dt], enabled=amp):
+            y = mod(g, x)
+        y.float().backward(dY)
+        out = {"Y": y.detach().float(), "dX": x.grad}
+        out.update({n: p.grad for n, p in mod.named_parameters()})
+        return {k: v.detach().float().cpu() for k, v in out.items()}
+
+    got, truth, amp = run(m, True), run(ref, False), run(ref, True)
+    tol = 2e-2 if dt == "bf16" else 1e-2
+    for k in truth:
+        e, e_amp = rel_err(got[k], truth[k]), rel_err(amp[k], truth[k])
+        assert e <= max(tol, AMP_SLACK * e_amp), f"{form} {k}: relL2 {e:.3e} (reference AMP {e_amp:.3e})"

@@ -287,6 +287,7 @@ def test_gemm_nt_weight_resident_opt_in_bit_identical(M, K, N, monkeypatch):
     b = torch.randn(N, device=DEV, generator=g)
     pk = _native.gemm_pack(W)
     out = []
+    monkeypatch.setenv("SIR_NT_G", "0")        # the reference kernel of this test is k_gemm_nt_p
     for w in ("0", "1"):
         monkeypatch.setenv("SIR_NT_W", w)
         wide = torch.full((M, N + 12), 7.0, device=DEV)
@@ -294,3 +295,32 @@ def test_gemm_nt_weight_resident_opt_in_bit_identical(M, K, N, monkeypatch):
     assert torch.equal(out[0][0], out[1][0])
     _check(out[1][0], A.double(), W.double().t(), torch.addmm(b, A, W.t()), b, f"nt_w M={M} K={K} N={N}")
     assert torch.all(out[1][1][:, :4] == 7.0) and torch.all(out[1][1][:, 4 + N:] == 7.0)
+
+
+@pytest.mark.parametrize("M,K,N", [(70001, 256, 256), (4099, 256, 512), (3001, 128, 256), (66000, 512, 256),
+                                   (513, 256, 300), (1, 512, 256), (255, 128, 512)])
+def test_gemm_nt_dma_kernel_vs_persistent(M, K, N, monkeypatch):
+    """The LDS-DMA NT kernel (sirconv_gemm_g.hip, the default for K in {128, 256, 512}, N in (128,
+    512]) against k_gemm_nt_p (SIR_NT_G=0): both within the fp64 bound, on rows spanning 2^60 of
+    range, rows whose maximum grows by 2^40 along K (the rescale branch), a strided C (the columns
+    around it untouched) and a ragged last tile."""
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + K)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-30, 30, (M, 1), device=DEV, generator=g).float())
+    if M > 300:
+        A[100:300] *= torch.exp2(torch.linspace(-20, 20, K, device=DEV))
+    W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g)
+    pk = _native.gemm_pack(W)
+    outs = {}
+    for sw in ("1", "0"):
+        monkeypatch.setenv("SIR_NT_G", sw)
+        wide = torch.full((M, N + 12), 7.0, device=DEV)
+        outs[sw] = (_native.gemm_nt(A, pk, b, out=wide[:, 4:4 + N]), wide)
+        torch.cuda.synchronize()
+    ref32 = torch.addmm(b, A, W.t())
+    for sw, (C, wide) in outs.items():
+        _check(C, A.double(), W.double().t(), ref32, b, f"nt SIR_NT_G={sw} M={M} K={K} N={N}")
+        assert torch.all(wide[:, :4] == 7.0) and torch.all(wide[:, 4 + N:] == 7.0)
+    d = _rel(outs["1"][0].double(), outs["0"][0].double())
+    assert d < 1e-6, f"dma vs persistent relL2 {d:.2e}"
