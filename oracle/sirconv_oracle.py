@@ -147,17 +147,18 @@ def max_first_wins(dst, num_nodes, M):
     """DGL ``fn.max`` over in-edges (``conv.py:41,63`` with agg_type='max'): elementwise max, the
     arg is the FIRST maximal edge in CSC order (= smallest edge id; DGL SpMMCmpCsr updates on
     strict >), rows without in-edges give 0 / arg -1.  Returns (Y, arg) with arg = edge ids."""
-    dst = torch.as_tensor(dst, dtype=torch.int64)
+    dev = M.device                      # runs where M lives (CPU for the fixtures, GPU as a test checker)
+    dst = torch.as_tensor(dst, dtype=torch.int64).to(dev)
     E, F = M.shape
-    Y = torch.zeros((num_nodes, F), dtype=M.dtype)
-    arg = torch.full((num_nodes, F), -1, dtype=torch.int64)
+    Y = torch.zeros((num_nodes, F), dtype=M.dtype, device=dev)
+    arg = torch.full((num_nodes, F), -1, dtype=torch.int64, device=dev)
     if E == 0:
         return Y, arg
     idx = dst.unsqueeze(1).expand(E, F)
     Y = Y.scatter_reduce(0, idx, M, reduce="amax", include_self=False)
-    eid = torch.arange(E).unsqueeze(1).expand(E, F)
+    eid = torch.arange(E, device=dev).unsqueeze(1).expand(E, F)
     cand = torch.where(M == Y[dst], eid, torch.full_like(eid, E))
-    arg = torch.full((num_nodes, F), E, dtype=torch.int64).scatter_reduce(0, idx, cand, reduce="amin")
+    arg = torch.full((num_nodes, F), E, dtype=torch.int64, device=dev).scatter_reduce(0, idx, cand, reduce="amin")
     arg[arg == E] = -1
     return Y, arg
 
@@ -174,7 +175,7 @@ class _MaxFirstWins(torch.autograd.Function):
     def backward(ctx, dY):
         arg, dst = ctx.saved_tensors
         E, F = ctx.E, dY.shape[1]
-        dM = torch.zeros((E, F), dtype=dY.dtype)
+        dM = torch.zeros((E, F), dtype=dY.dtype, device=dY.device)
         hit = arg >= 0
         rows, cols = torch.nonzero(hit, as_tuple=True)
         dM[arg[rows, cols], cols] = dY[rows, cols]

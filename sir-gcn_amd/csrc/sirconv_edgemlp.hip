@@ -201,6 +201,218 @@ k_mlp_fwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
     }
 }
 
+// ------------------------------------------------------------------------------ forward, split-fp16 MFMA
+// The same dataflow as k_mlp_fwd with h = a W^T on v_mfma_f32_32x32x16_f16 and the two-term operand
+// split of the projection GEMMs (sirconv_gemm.hip): a = (a_hi + a_lo) / s_e with one power-of-two
+// scale per edge row (the whole row is staged before it is split), W = (w_hi + w_lo) / s_n per
+// feature (packed once, k_mlp_pack16), h = (a_hi w_hi + a_hi w_lo + a_lo w_hi) / (s_e s_n) with fp32
+// accumulation: per product <= 3 * 2^-22 relative (tests/test_gemm_gpu.py's bound), 3 MFMAs of 32
+// cycles per 16 k instead of 8 fp32 MFMAs of 64 cycles (5.3x fewer MFMA cycles).
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ int mlp_bexp(float m) { return (int)((__float_as_uint(m) >> 23) & 255u) - 126; }
+__device__ __forceinline__ float mlp_pow2(int e) {
+    e = e < -126 ? -126 : (e > 127 ? 127 : e);
+    return __uint_as_float((uint32_t)(e + 127) << 23);
+}
+// scale exponent with |x| * 2^se < 2^15 for the row maximum m (clamped to a normal float)
+__device__ __forceinline__ int mlp_scale_exp(float m) { const int s = 15 - mlp_bexp(m); return s > 126 ? 126 : s; }
+// fragment image of one 16-k step plane: piece (row, h) of 16 B at (row / 32) * 1024 + h * 512 + (row % 32) * 16
+__device__ __forceinline__ int mlp_fimg(int row, int h) { return ((row >> 5) << 10) + (h << 9) + ((row & 31) << 4); }
+
+// pack: out16[((t * NG + g) * 2 + p) * 64 + l] = 8 halves of part p (hi / lo) of W[32t + l%32][16g + 8(l/32) + j]
+// scaled by 2^se(n); inv[n] = 2^-se(n) (0 past F).  One 64-thread block per padded feature.
+__global__ void __launch_bounds__(64)
+k_mlp_pack16(const float* __restrict__ W, int H, int F, int NG, _Float16* __restrict__ out16, float* __restrict__ inv) {
+    const int n = blockIdx.x, l = threadIdx.x;
+    float m = 0.f;
+    if (n < F)
+        for (int k = l; k < H; k += 64) m = fmaxf(m, fabsf(W[(int64_t)n * H + k]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const int se = mlp_scale_exp(m);
+    const float s = mlp_pow2(se);
+    const int t = n >> 5, r = n & 31;
+    for (int k = l; k < NG * 16; k += 64) {
+        const float x = (n < F && k < H) ? W[(int64_t)n * H + k] : 0.f;
+        const float y = x * s;
+        const _Float16 hh = (_Float16)y;
+        const int g = k >> 4, h = (k >> 3) & 1, j = k & 7;
+        const int lane = h * 32 + r;
+        out16[(((int64_t)t * NG + g) * 2 + 0) * 512 + lane * 8 + j] = hh;
+        out16[(((int64_t)t * NG + g) * 2 + 1) * 512 + lane * 8 + j] = (_Float16)(y - (float)hh);
+    }
+    if (l == 0) inv[n] = (n < F) ? mlp_pow2(-se) : 0.f;
+}
+
+// RPW = rows of the 32-edge tile per wave (32 / NW), C4 = float4 chunks of 256 features per row (HP16 / 256)
+template <int ACT1, int ACT2, int RED, int NW, int TPW, int C4>
+__global__ void __launch_bounds__(64 * NW)
+k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
+            const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
+            const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope,
+            int H, int NG, int F, const h8v* __restrict__ Wp16, const float* __restrict__ winv,
+            const float* __restrict__ bias, float* __restrict__ out, int64_t ldo, int* __restrict__ arg, int64_t lda,
+            float* __restrict__ pval, int* __restrict__ parg) {
+    constexpr int RPW = 32 / NW;
+    extern __shared__ float smem[];
+    char* const img = reinterpret_cast<char*>(smem);                // [NG][2][32 rows fimg] halves
+    float* const sInv = reinterpret_cast<float*>(img + NG * 2048);  // [32] 2^-se of the edge rows
+    float* const sC = sInv + 32;                                    // [32] c_e (0 past the tile's last edge)
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int4 it = uniform_item(items, blockIdx.x);
+    const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
+    const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
+    const float* qp = Q + (int64_t)row * ldq;
+    const int ntile = (F + 31) / 32;
+
+    float racc[TPW], best[TPW], bb[TPW], iw[TPW];
+    int bidx[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        racc[j] = 0.f; best[j] = -INFINITY; bidx[j] = INT_MAX;
+        const int n = 32 * (w + NW * j) + (l & 31);
+        bb[j] = (bias != nullptr && n < F) ? bias[n] : 0.f;
+        iw[j] = (n < F) ? winv[n] : 0.f;
+    }
+    float4 q4[C4];
+#pragma unroll
+    for (int c = 0; c < C4; ++c) {
+        const int k = 256 * c + 4 * l;
+        q4[c] = (k < H) ? *reinterpret_cast<const float4*>(qp + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+
+    for (int t0 = e0; t0 < e1; t0 += 32) {
+        const int nv = (e1 - t0) < 32 ? (e1 - t0) : 32;
+        // ---- stage: this wave's rows i = w + NW * ii; every K row gathered before any is used
+        float4 kv[RPW][C4];
+#pragma unroll
+        for (int ii = 0; ii < RPW; ++ii) {
+            const int i = w + NW * ii;
+            const int u = col[t0 + (i < nv ? i : 0)];
+#pragma unroll
+            for (int c = 0; c < C4; ++c) {
+                const int k = 256 * c + 4 * l;
+                kv[ii][c] = (k < H) ? *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int ii = 0; ii < RPW; ++ii) {
+            const int i = w + NW * ii;
+            float4 a4[C4];
+            float m = 0.f;
+#pragma unroll
+            for (int c = 0; c < C4; ++c) {
+                const int k = 256 * c + 4 * l;
+                const bool ok = i < nv && k < H;
+                a4[c].x = ok ? act_f<ACT1>(q4[c].x + kv[ii][c].x, slope) : 0.f;
+                a4[c].y = ok ? act_f<ACT1>(q4[c].y + kv[ii][c].y, slope) : 0.f;
+                a4[c].z = ok ? act_f<ACT1>(q4[c].z + kv[ii][c].z, slope) : 0.f;
+                a4[c].w = ok ? act_f<ACT1>(q4[c].w + kv[ii][c].w, slope) : 0.f;
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(a4[c].x), fabsf(a4[c].y)), fmaxf(fabsf(a4[c].z), fabsf(a4[c].w))));
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+            const int se = mlp_scale_exp(m);
+            const float sc = mlp_pow2(se);
+#pragma unroll
+            for (int c = 0; c < C4; ++c) {
+                const int k = 256 * c + 4 * l;
+                if (k < NG * 16) {
+                    const float y[4] = {a4[c].x * sc, a4[c].y * sc, a4[c].z * sc, a4[c].w * sc};
+                    _Float16 hv[4], lv[4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
+                    const int g = k >> 4, h = (k >> 3) & 1, j8 = k & 7;
+                    char* d = img + g * 2048 + mlp_fimg(i, h) + j8 * 2;
+                    *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
+                    *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
+                }
+            }
+            if (l == 0) sInv[i] = mlp_pow2(-se);
+        }
+        if (w == 0 && l < 32) {
+            float c = 0.f;
+            if (l < nv) c = (RED == AGG_SYM) ? norm_col[col[t0 + l]] * nr : 1.f;   // conv.py:45 operand order
+            sC[l] = c;
+        }
+        __syncthreads();
+        // ---- h = a W^T on split-fp16 MFMA (this wave's output tiles)
+        mf16 acc[TPW];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        const int fo = mlp_fimg(l & 31, l >> 5);
+        for (int g = 0; g < NG; ++g) {
+            const h8v ahi = *reinterpret_cast<const h8v*>(img + g * 2048 + fo);
+            const h8v alo = *reinterpret_cast<const h8v*>(img + g * 2048 + 1024 + fo);
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) {
+                const int t = w + NW * j;
+                if (t >= ntile) continue;            // wave-uniform: tiles past F have no packed W
+                const h8v whi = Wp16[(((int64_t)t * NG + g) * 2 + 0) * 64 + l];
+                const h8v wlo = Wp16[(((int64_t)t * NG + g) * 2 + 1) * 64 + l];
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi, acc[j], 0, 0, 0);
+            }
+        }
+        // ---- m = act2(h + b), reduced in edge order within the lane
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = drow(r, l);
+                if (i < nv) {
+                    const float m = act_f<ACT2>(acc[j][r] * sInv[i] * iw[j] + bb[j], slope);
+                    if constexpr (RED == 3) {
+                        if (m > best[j]) { best[j] = m; bidx[j] = t0 + i; }    // strict >: first wins
+                    } else {
+                        racc[j] += sC[i] * m;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- the two half-waves hold interleaved edge groups of the same columns: combine, store
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        const int n = 32 * (w + NW * j) + (l & 31);
+        if constexpr (RED == 3) {
+            const float ob = __shfl_xor(best[j], 32);
+            const int oi = __shfl_xor(bidx[j], 32);
+            if (ob > best[j] || (ob == best[j] && oi < bidx[j])) { best[j] = ob; bidx[j] = oi; }
+            if (l < 32 && n < F) {
+                const bool any = bidx[j] != INT_MAX;
+                if (slot < 0) {
+                    out[(int64_t)row * ldo + n] = any ? best[j] : 0.f;
+                    arg[(int64_t)row * lda + n] = any ? bidx[j] : -1;
+                } else {
+                    pval[(int64_t)slot * F + n] = best[j];
+                    parg[(int64_t)slot * F + n] = bidx[j];
+                }
+            }
+        } else {
+            const float other = __shfl_xor(racc[j], 32);
+            float v = (l < 32) ? racc[j] + other : other + racc[j];
+            if (l < 32 && n < F) {
+                if (slot < 0) {
+                    if constexpr (RED == AGG_MEAN) {
+                        const int d = e1 - e0;
+                        v = v / (float)(d > 1 ? d : 1);
+                    }
+                    out[(int64_t)row * ldo + n] = v;
+                } else {
+                    pval[(int64_t)slot * F + n] = v;
+                }
+            }
+        }
+    }
+}
+
 // max: combine the chunk partials of split rows in chunk (= edge) order, strict > (first wins)
 __global__ void k_mlp_max_combine(const int4* __restrict__ splits, int F, const float* __restrict__ pval,
                                   const int* __restrict__ parg, float* __restrict__ Y, int64_t ldy,
@@ -447,6 +659,40 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
     }
 }
 
+#ifndef SIR_MLP_F16
+#define SIR_MLP_F16 1           // 1: the forward on split-fp16 MFMA (k_mlp_fwd16); 0: fp32 MFMA (k_mlp_fwd)
+#endif
+int mlp_ng(int H) { return (H + 15) / 16; }
+int64_t mlp_pack16_bytes(int H, int F) {
+    const int FP = (F + 31) / 32 * 32;
+    return (int64_t)FP * mlp_ng(H) * 16 * 2 * 2 + (int64_t)FP * 4;
+}
+
+template <int ACT1, int ACT2, int RED>
+hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
+    const int NG = mlp_ng(a.H), FP = (a.F + 31) / 32 * 32;
+    const h8v* w16 = static_cast<const h8v*>(p16);
+    const float* winv = reinterpret_cast<const float*>(static_cast<const char*>(p16) + (int64_t)FP * NG * 64);
+    const size_t lds = (size_t)NG * 2048 + 64 * sizeof(float);
+#define SIR_MLP_FWD16(NWV, TPWV, C4V)                                                                            \
+    hipLaunchKernelGGL((k_mlp_fwd16<ACT1, ACT2, RED, NWV, TPWV, C4V>), grid, dim3(64 * NWV), lds, st, a.rowptr,     \
+                       a.col, reinterpret_cast<const int4*>(a.items), a.Q, a.ldq, a.K, a.ldk, a.norm_row, a.norm_col, \
+                       a.slope, a.H, NG, a.F, w16, winv, a.bias, a.out, a.ldo, a.arg, a.lda, a.pval, a.parg)
+    if (NG * 16 <= 256) {
+        if (nt <= 1) SIR_MLP_FWD16(1, 1, 1);
+        else if (nt <= 2) SIR_MLP_FWD16(2, 1, 1);
+        else if (nt <= 4) SIR_MLP_FWD16(4, 1, 1);
+        else if (nt <= 8) SIR_MLP_FWD16(4, 2, 1);
+        else SIR_MLP_FWD16(8, 2, 1);
+    } else {
+        if (nt <= 4) SIR_MLP_FWD16(4, 1, 2);
+        else if (nt <= 8) SIR_MLP_FWD16(4, 2, 2);
+        else SIR_MLP_FWD16(8, 2, 2);
+    }
+#undef SIR_MLP_FWD16
+    return hipGetLastError();
+}
+
 template <int ACT1, int ACT2, int RED>
 hipError_t mlp_fwd_nt(int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeMlpArgs& a) {
 #define SIR_MLP_FWD(NWV, TPWV)                                                                                 \
@@ -462,6 +708,16 @@ hipError_t mlp_fwd_nt(int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeM
     else SIR_MLP_FWD(8, 2);                      // F <= 512 (roman-empire: H = O = 512)
 #undef SIR_MLP_FWD
     return hipGetLastError();
+}
+
+template <int ACT1, int ACT2>
+hipError_t mlp_fwd16_red(int red, int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
+    switch (red) {
+        case AGG_SUM: return mlp_fwd16_nt<ACT1, ACT2, AGG_SUM>(nt, grid, st, a, p16);
+        case AGG_MEAN: return mlp_fwd16_nt<ACT1, ACT2, AGG_MEAN>(nt, grid, st, a, p16);
+        case AGG_SYM: return mlp_fwd16_nt<ACT1, ACT2, AGG_SYM>(nt, grid, st, a, p16);
+        default: return mlp_fwd16_nt<ACT1, ACT2, 3>(nt, grid, st, a, p16);
+    }
 }
 
 template <int ACT1, int ACT2>
@@ -526,9 +782,15 @@ hipError_t by_acts(int act1, int act2, Fn&& fn) {
 
 }  // namespace
 
-int64_t mlp_pack_floats(int H, int F) {
+// the packed weight: the fp32 fragment image (k_mlp_pack: the backward and the fp32 forward), then,
+// 16-B aligned, the split-fp16 image + inverse scales of the forward (k_mlp_pack16)
+static int64_t mlp_pack32_floats(int H, int F) {
     const int HP = (H + 7) / 8 * 8, FP = (F + 31) / 32 * 32;
     return (int64_t)(FP / 32) * (HP / 8) * 64 * 4;
+}
+int64_t mlp_pack_floats(int H, int F) { return mlp_pack32_floats(H, F) + (mlp_pack16_bytes(H, F) + 3) / 4; }
+static const void* mlp_p16(const void* packed, int H, int F) {
+    return static_cast<const char*>(packed) + mlp_pack32_floats(H, F) * 4;
 }
 
 hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t st) {
@@ -536,6 +798,12 @@ hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t 
     const int64_t n = (int64_t)(FP / 32) * (HP / 8) * 64;
     hipLaunchKernelGGL(k_mlp_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, F, HP, FP,
                        static_cast<float4*>(packed));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    char* p16 = static_cast<char*>(packed) + mlp_pack32_floats(H, F) * 4;
+    const int NG = mlp_ng(H);
+    hipLaunchKernelGGL(k_mlp_pack16, dim3((unsigned)FP), dim3(64), 0, st, W, H, F, NG,
+                       reinterpret_cast<_Float16*>(p16), reinterpret_cast<float*>(p16 + (int64_t)FP * NG * 64));
     return hipGetLastError();
 }
 
@@ -544,8 +812,11 @@ hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStr
         const int nt = (a.F + 31) / 32;
         const size_t lds = (size_t)(32 * (a.HP + 1) + 32) * sizeof(float);
         const dim3 grid((unsigned)a.n_items);
+        const bool f16 = SIR_MLP_F16 && a.H <= 512;
         hipError_t err = by_acts(act1, act2, [&](auto A1, auto A2) {
-            return mlp_fwd_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, lds, st, a);
+            return f16 ? mlp_fwd16_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, st, a,
+                                                                               mlp_p16(a.Wp, a.H, a.F))
+                       : mlp_fwd_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, lds, st, a);
         });
         if (err != hipSuccess) return err;
     }

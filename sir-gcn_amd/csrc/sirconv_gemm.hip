@@ -95,7 +95,32 @@ __device__ inline void drop4(const Drop& d, int64_t row, int n, float4& o) {
     o.w = drop_keep(d, rh, c + 3) ? o.w * d.scale : 0.f;
 }
 
+#ifndef SIR_SPLIT_MIX
+#define SIR_SPLIT_MIX 1         // TN loaders: 1 = the split by v_fma_mix (2 VALU per element), 0 = plain C (~4.5)
+#endif                          // (the NT kernels keep the C form: the asm one costs them a spill in the loop)
 // hi/lo fp16 split of 8 floats scaled by s (exact power of two)
+// hi = fp16(x s), lo = fp16(x s - hi), one v_fma_mix each, written into the halves of the fragment
+// registers (x s is exact, and x s - hi is exact in the fused op: the same bits as rounding y = x s
+// and y - hi separately, sirconv_gemm_w.hip).  s_nop 1: the VALU-write -> MFMA-read wait states
+// (the hazard recognizer does not look inside inline asm).
+__device__ inline void split8_mix(float4 a, float4 b, float s, h8& hi, h8& lo) {
+    uint32_t h0, h1, h2, h3, l0, l1, l2, l3;
+    asm volatile(
+        "v_fma_mixlo_f16 %0, %8, %16, 0\n\tv_fma_mixhi_f16 %0, %9, %16, 0\n\t"
+        "v_fma_mixlo_f16 %1, %10, %16, 0\n\tv_fma_mixhi_f16 %1, %11, %16, 0\n\t"
+        "v_fma_mixlo_f16 %2, %12, %16, 0\n\tv_fma_mixhi_f16 %2, %13, %16, 0\n\t"
+        "v_fma_mixlo_f16 %3, %14, %16, 0\n\tv_fma_mixhi_f16 %3, %15, %16, 0\n\t"
+        "v_fma_mixlo_f16 %4, %8, %16, -%0 op_sel_hi:[0,0,1]\n\tv_fma_mixhi_f16 %4, %9, %16, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %5, %10, %16, -%1 op_sel_hi:[0,0,1]\n\tv_fma_mixhi_f16 %5, %11, %16, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %6, %12, %16, -%2 op_sel_hi:[0,0,1]\n\tv_fma_mixhi_f16 %6, %13, %16, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %7, %14, %16, -%3 op_sel_hi:[0,0,1]\n\tv_fma_mixhi_f16 %7, %15, %16, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "s_nop 1"
+        : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+        : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(s));
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    hi = __builtin_bit_cast(h8, u4{h0, h1, h2, h3});
+    lo = __builtin_bit_cast(h8, u4{l0, l1, l2, l3});
+}
 #define SIR_SPLIT1(x, i) { const float y_ = (x) * s; const _Float16 h_ = (_Float16)y_; hi[i] = h_; lo[i] = (_Float16)(y_ - (float)h_); }
 __device__ inline void split8(float4 a, float4 b, float s, h8& hi, h8& lo) {
     SIR_SPLIT1(a.x, 0) SIR_SPLIT1(a.y, 1) SIR_SPLIT1(a.z, 2) SIR_SPLIT1(a.w, 3)
@@ -103,6 +128,12 @@ __device__ inline void split8(float4 a, float4 b, float s, h8& hi, h8& lo) {
 }
 #undef SIR_SPLIT1
 
+// m = max(m, |v|) in two v_max3_f32 with |.| source modifiers (fmaxf makes hipcc canonicalise every
+// input first)
+__device__ inline float fmax4_mix(float m, float4 v) {
+    asm("v_max3_f32 %0, %0, |%1|, |%2|\n\tv_max3_f32 %0, %0, |%3|, |%4|" : "+v"(m) : "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    return m;
+}
 __device__ inline float fmax4(float m, float4 v) {
     return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
 }
@@ -970,7 +1001,7 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
-        for (int j = 0; j < XR / 4; ++j) m = fmax4(m, xv[j]);
+        for (int j = 0; j < XR / 4; ++j) m = SIR_SPLIT_MIX ? fmax4_mix(m, xv[j]) : fmax4(m, xv[j]);
         if (KSPT == 1) m = fmaxf(m, __shfl_xor(m, 1));
         const int se_old = se_run, se = next_se(se_old, bexp(m));
         se_run = se;
@@ -978,8 +1009,13 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
 #pragma unroll
         for (int q = 0; q < KSPT; ++q) {      // k-step kse + q: rows 16q .. 16q+15 of x
             h8 hv[2], lv[2];
-            split8(xv[4 * q + 0], xv[4 * q + 1], s, hv[0], lv[0]);
-            split8(xv[4 * q + 2], xv[4 * q + 3], s, hv[1], lv[1]);
+            if constexpr (SIR_SPLIT_MIX) {
+                split8_mix(xv[4 * q + 0], xv[4 * q + 1], s, hv[0], lv[0]);
+                split8_mix(xv[4 * q + 2], xv[4 * q + 3], s, hv[1], lv[1]);
+            } else {
+                split8(xv[4 * q + 0], xv[4 * q + 1], s, hv[0], lv[0]);
+                split8(xv[4 * q + 2], xv[4 * q + 3], s, hv[1], lv[1]);
+            }
             char* hd = st + hi_off + q * rows_img * 32;    // fimg(cl, 1) = fimg(cl, 0) + 512
             *reinterpret_cast<h8*>(hd) = hv[0];
             *reinterpret_cast<h8*>(hd + 512) = hv[1];

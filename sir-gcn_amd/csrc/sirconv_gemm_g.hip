@@ -32,7 +32,11 @@
 #include <cstdlib>
 
 #ifndef SIR_NT_G
-#define SIR_NT_G 1              // 0: the fp32 NT projections stay on k_gemm_nt_p (A/B builds)
+// OPT-IN (SIR_NT_G=1 in the environment, read per call; 0 here disables it entirely): measured slower than
+// k_gemm_nt_p on every S2 shape (profiles/r03_ab_gemm_dma.txt: QK 2.10 vs 1.96, Y 1.06 vs 0.99, dX 1.92
+// vs 1.74 ms) — each data row is split by the two waves that share it and the split runs between the
+// barrier and the MFMAs of every 16-k stage, so the DMA depth does not pay for it
+#define SIR_NT_G 1
 #endif
 
 namespace sir {
@@ -54,6 +58,10 @@ constexpr int GLDS = GEPI_OFF + 2 * 512 * 4;
 static_assert(GLDS <= 160 * 1024, "LDS budget");
 constexpr int GOPS = 4;                         // DMA instructions per wave per stage (2 A + 2 W)
 constexpr int GSTORES = 32;                     // epilogue stores per wave per tile
+#ifndef SIR_NTG_TB
+#define SIR_NTG_TB 1            // 32-row MFMA tiles per wave: 1 = 32 rows x 256 features (each row split once),
+#endif                          // 2 = 64 rows x 128 features (each row split by the two waves sharing it)
+constexpr int GTB = SIR_NTG_TB, GTA = 8 / GTB, GWF = 8 / GTA;   // row tiles, feature tiles, waves along features
 
 #ifndef SIR_HR
 #define SIR_HR 8
@@ -141,7 +149,7 @@ k_gemm_nt_g(const float* __restrict__ A, int64_t lda, int64_t M, const char* __r
 
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int l = t & 63, r = l & 31, h = l >> 5;
-    const int d_w = (w >> 1) * 64, f_w = (w & 1) * 128;
+    const int d_w = (w / GWF) * 32 * GTB, f_w = (w % GWF) * 32 * GTA;
     const uint32_t wbytes = (uint32_t)((int64_t)(NST / 2) * 4 * Npad * 32);
 
     // ---- DMA of stage s (block-local stage sequence: tile tb + s / NST, k16 step s % NST) ----
@@ -181,48 +189,58 @@ k_gemm_nt_g(const float* __restrict__ A, int64_t lda, int64_t M, const char* __r
         dma16(wrs, wo + lo_off, st + GW + GWLO + w * 1024);
     };
 
-    f16v acc[4][2];
-    int se[2] = {SE_INIT, SE_INIT};
+    f16v acc[GTA][GTB];
+    int se[GTB];
+#pragma unroll
+    for (int b = 0; b < GTB; ++b) se[b] = SE_INIT;
     const int sw = (r >> 2) & 3;                  // A piece swizzle of this lane's rows
 
-    // multiply the k16 step in stage slot `slot`; first: the tile's first step (zero accumulators)
+    // multiply the k16 step in stage slot `slot`; first: the tile's first step (zero accumulators).
+    // The (rare) rescale is one branch ahead of the splits and MFMAs, which then form one basic block
+    // the scheduler can interleave (fragment reads and splits under the MFMAs).
     auto compute = [&](int slot, bool first) {
         const char* st = lds + slot * GSTAGE;
-        float4 av[2][2];
+        float4 av[GTB][2];
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < GTB; ++b)
 #pragma unroll
             for (int u = 0; u < 2; ++u)
                 av[b][u] = *reinterpret_cast<const float4*>(st + GA + (d_w + 32 * b + r) * 64 + (((2 * h + u) ^ sw) << 4));
-        h8 wh[4], wl[4];
+        h8 wh[GTA], wl[GTA];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
+        for (int a = 0; a < GTA; ++a) {
             wh[a] = *reinterpret_cast<const h8*>(st + GW + fimg(f_w + 32 * a + r, h));
             wl[a] = *reinterpret_cast<const h8*>(st + GW + GWLO + fimg(f_w + 32 * a + r, h));
         }
-        h8 dh[2], dl[2];
+        int se_new[GTB];
+        bool ch = false;
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < GTB; ++b) {
             float m = fmax4(fmax4(0.f, av[b][0]), av[b][1]);
             const auto sx = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
             m = fmaxf(__uint_as_float(sx[0]), __uint_as_float(sx[1]));
-            const int se_new = next_se(first ? SE_INIT : se[b], bexp(m));
-            if (!first) {
-                const bool ch = se_new != se[b];
-                if (__builtin_amdgcn_ballot_w64(ch) != 0) {         // rare: a row's maximum rose past 2^SIR_HR
-                    const float fac = pow2(se_new - se[b]);
+            se_new[b] = next_se(first ? SE_INIT : se[b], bexp(m));
+            ch |= se_new[b] != se[b];
+        }
+        if (!first && __builtin_amdgcn_ballot_w64(ch) != 0) {     // rare: a row's maximum rose past 2^SIR_HR
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) acc[a][b] *= fac;
-                }
+            for (int b = 0; b < GTB; ++b) {
+                const float fac = pow2(se_new[b] - se[b]);
+#pragma unroll
+                for (int a = 0; a < GTA; ++a) acc[a][b] *= fac;
             }
-            se[b] = se_new;
-            split8(av[b][0], av[b][1], pow2(se_new), dh[b], dl[b]);
+        }
+        h8 dh[GTB], dl[GTB];
+#pragma unroll
+        for (int b = 0; b < GTB; ++b) {
+            se[b] = se_new[b];
+            split8(av[b][0], av[b][1], pow2(se_new[b]), dh[b], dl[b]);
         }
         const f16v zero = {};
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < GTA; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
+            for (int b = 0; b < GTB; ++b) {
                 acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[a], dh[b], first ? zero : acc[a][b], 0, 0, 0);
                 acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[a], dl[b], acc[a][b], 0, 0, 0);
                 acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[a], dh[b], acc[a][b], 0, 0, 0);
@@ -242,10 +260,10 @@ k_gemm_nt_g(const float* __restrict__ A, int64_t lda, int64_t M, const char* __r
         char* const slot = lds + GSLOT_OFF + w * GSLOT;
         const int rq = l >> 2, pq = l & 3;            // read-back role: row rq (+16), piece pq
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < GTB; ++b) {
             const float is = pow2(-se[b]);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            for (int q = 0; q < 2 * GTA; ++q) {
                 const int a = q >> 1;
 #pragma unroll
                 for (int gg = 0; gg < 2; ++gg) {
@@ -331,8 +349,8 @@ k_gemm_nt_g(const float* __restrict__ A, int64_t lda, int64_t M, const char* __r
 // the shapes k_gemm_nt_g takes: K = 128 / 256 / 512, 128 < N <= 512, 16-B aligned rows of A and C
 bool gemm_nt_g_ok(const float* A, int64_t lda, int K, int N, const float* C, int64_t ldc) {
     if (!SIR_NT_G) return false;
-    const char* e = getenv("SIR_NT_G");       // "0": k_gemm_nt_p instead (read per call, for A/B in one process)
-    if (e != nullptr && e[0] == '0') return false;
+    const char* e = getenv("SIR_NT_G");       // "1": this kernel (read per call, for A/B in one process)
+    if (e == nullptr || e[0] != '1') return false;
     return (K == 128 || K == 256 || K == 512) && N > 128 && gemm_pack_npad(N) <= 512 && lda % 4 == 0 &&
            ldc % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)C & 15) == 0 && (int64_t)256 * lda * 4 < ((int64_t)1 << 32);
 }

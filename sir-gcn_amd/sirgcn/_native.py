@@ -10,7 +10,9 @@ import threading
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libsirconv.so")
+# SIRGCN_LIB: an A/B build of the same sources (tools/build_variant.sh), for measurement runs only
+LIB_PATH = os.environ.get("SIRGCN_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                        "lib", "libsirconv.so")
 
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)

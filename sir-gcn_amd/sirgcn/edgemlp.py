@@ -6,10 +6,11 @@ whose message runs a Linear on every edge, without any [E, *] tensor in the forw
   H, F <= 256 (the config-1 shape is H = F = 64; the DictionaryLookup sweep reaches H = F = 200,
   ``dictionary-lookup/README.md:8``).
 * ``agg_type='max'`` (``conv.py:46-47``: ``linear_relation`` per edge, DGL ``fn.max``):
-  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge) and, for
-  H, O <= 256, fused backward (``sir_edge_max_bwd_*``: dY routed to the arg edges, z and a
-  recomputed per edge, dW_R / db_R per-block partials — no [E, *] tensor); wider layers recompute
-  the edge activations once into [E, H] buffers and run the native gather / GEMM / segment kernels.
+  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge) and two
+  backwards: fused for H, O <= 256 (``sir_edge_max_bwd_*``: dY routed to the arg edges, z and a
+  recomputed per edge, dW_R / db_R per-block partials — no [E, *] tensor), taken when the
+  edge-materialised one (edge activations recomputed once into [E, H] buffers, native gather /
+  split-fp16 GEMM / segment kernels — faster) would not fit its memory budget.
 
 Everything is fp32, under autocast too: there the reference runs the per-edge Linear (and sigma)
 in 16 bits, these kernels take Q, K widened to fp32 and return the result cast back to QK's dtype —
@@ -151,7 +152,16 @@ class EdgeMLPSum(torch.autograd.Function):
 
 
 class EdgeMaxLinear(torch.autograd.Function):
-    """Y[v] = max_e (W_R act1(Q[v] + K[u]) + b_R), first arg-max edge (DGL fn.max), empty rows 0."""
+    """Y[v] = max_e (W_R act1(Q[v] + K[u]) + b_R), first arg-max edge (DGL fn.max), empty rows 0.
+
+    Backward route (``fused_bwd``): ``None`` (default) picks by memory — the edge-materialised
+    backward (z recomputed once into [E, H], dM [E, O]; its GEMMs on the split-fp16 MFMA kernels) when
+    its buffers, E (2H + O) 4 bytes, stay within ``materialised_budget`` (48 GiB, and 40 % of the free
+    device memory), else the fused backward (no [E, *] buffer; its three edge-contracted products
+    run on fp32 MFMA, ~4x slower on MI355X at S1: the route of the S2 shape, whose buffers would take
+    123 GB); ``True`` / ``False`` force one (tests)."""
+    fused_bwd = None
+    materialised_budget = 48 << 30
 
     @staticmethod
     def forward(ctx, QK, W, b, plan, H, act1, slope):
@@ -175,11 +185,15 @@ class EdgeMaxLinear(torch.autograd.Function):
         plan, H, act1, slope = ctx.plan, ctx.H, ctx.act1, ctx.slope
         dY = dY.contiguous().float()
         O = W.shape[0]
-        if max_bwd_fused(H, O):
-            dQK, dW, db = _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope)
-            return dQK, dW, (db if ctx.has_b else None), None, None, None, None
         E = plan.dst.col.numel()
         dev = dY.device
+        fused = EdgeMaxLinear.fused_bwd
+        if fused is None:
+            need = E * (2 * H + O) * 4
+            fused = need > min(EdgeMaxLinear.materialised_budget, int(0.4 * torch.cuda.mem_get_info(dev)[0]))
+        if fused and max_bwd_fused(H, O):
+            dQK, dW, db = _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope)
+            return dQK, dW, (db if ctx.has_b else None), None, None, None, None
         # the arg edges' activations are needed for dW_R: recompute z_e once (no copy kept from the forward)
         Z = torch.empty((E, H), device=dev, dtype=torch.float32)
         _native.edge_gather_add(plan.dst, QK[:, :H], QK[:, H:], Z)
@@ -251,11 +265,12 @@ def _act(z, code, slope):
 
 
 def _act_bwd(z, g, code, slope):
-    """sigma'(z) * g as torch's backward computes it (in place into g where possible)."""
+    """sigma'(z) * g with torch's own backward kernels (the ops autograd runs: one fused pass over
+    the [E, H] tensors instead of compare + multiply + select, ~3x fewer bytes)."""
     if code == _native.ACT_RELU:
-        return g.masked_fill_(z <= 0, 0.0)
+        return torch.ops.aten.threshold_backward(g, z, 0.0)
     if code == _native.ACT_LEAKY:
-        return torch.where(z > 0, g, g * slope)
+        return torch.ops.aten.leaky_relu_backward(g, z, slope, False)
     if code in (_native.ACT_GELU, _native.ACT_GELU_TANH):
         zz = z.detach().requires_grad_(True)
         with torch.enable_grad():

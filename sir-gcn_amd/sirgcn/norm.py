@@ -15,12 +15,6 @@ from . import _native
 from .graph import node_offsets
 
 
-def _param_sum(part):
-    if part.shape[1] % 4 == 0:
-        return _native.col_sum(part)
-    return part.sum(0)
-
-
 class GraphNormFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, weight, bias, mean_scale, off, eps):
@@ -46,13 +40,15 @@ class GraphNormFunction(torch.autograd.Function):
         ms = ms if ctx.has_ms else None
         dY = dY.contiguous().float()
         dX = torch.empty_like(X)
-        dw_part = torch.empty_like(mean)
-        db_part = torch.empty_like(mean)
-        dms_part = torch.empty_like(mean) if ms is not None else None
-        _native.graph_norm_bwd(off, X, dY, w, ms, mean, std, dX, dw_part, dms_part, db_part)
-        dw = _param_sum(dw_part)
-        db = _param_sum(db_part) if ctx.has_b else None
-        dms = _param_sum(dms_part) if ms is not None else None
+        # the per-graph partials of dw, db (and dms) as slabs of one [n, B, F] buffer, reduced over
+        # the graphs by ONE launch (molecule batches are launch-bound: three column sums were six)
+        parts = torch.empty((3 if ms is not None else 2,) + tuple(mean.shape), device=X.device, dtype=torch.float32)
+        _native.graph_norm_bwd(off, X, dY, w, ms, mean, std, dX, parts[0], parts[2] if ms is not None else None,
+                               parts[1])
+        sums = parts.sum(1)
+        dw = sums[0]
+        db = sums[1] if ctx.has_b else None
+        dms = sums[2] if ms is not None else None
         return dX, dw, db, dms, None, None
 
 

@@ -104,10 +104,12 @@ def test_seq_sigma_fused_vs_oracle(agg, H, Fo, chunk, monkeypatch):
 @pytest.mark.parametrize("H,O", [(256, 40), (64, 64), (300, 24), (128, 256), (100, 200), (512, 512)])
 def test_max_fused_vs_oracle_first_wins(act, H, O, chunk, monkeypatch):
     """Fused forward for H, O <= 512 (roman-empire: H = O = 512, heterophilous-datasets/README.md:8)
-    and, for H, O <= 256, the fused backward: no [E, H] gather of edge activations is allowed."""
-    from sirgcn.edgemlp import max_bwd_fused
+    and, for H, O <= 256, the fused backward (forced: the memory budget picks the edge-materialised
+    one at these sizes): no [E, H] gather of edge activations is allowed."""
+    from sirgcn.edgemlp import EdgeMaxLinear, max_bwd_fused
     _no_generic(monkeypatch)
     if max_bwd_fused(H, O):
+        monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", True)   # the budget would pick the materialised one here
         def boom(*a, **k):
             raise AssertionError("edge-materialised max backward reached")
         monkeypatch.setattr(_native, "edge_gather_add", boom)
@@ -190,3 +192,22 @@ def test_dictionary_lookup_sweep_shapes_fused(n, monkeypatch):
                   ("linear_relation.weight", "dW_R"), ("activation.1.weight", "act.1.weight"),
                   ("activation.1.bias", "act.1.bias")):
         assert_parity(got[k], r32[kr], r64[kr], 1e-5, f"dictionary n={n} {k}", strict=(k == "Y"))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_max_backward_routes_agree(fused, monkeypatch):
+    """The two max backwards (fused, no [E, *] buffer / edge-materialised on the split-fp16 GEMMs)
+    route dY to the same first arg-max edges: gradients agree to fp32 rounding."""
+    from sirgcn.edgemlp import EdgeMaxLinear
+    src, dst, V, gen = _graph(91)
+    X, dY = torch.randn(V, 32, generator=gen), torch.randn(V, 96, generator=gen)
+    torch.manual_seed(9)
+    m = SIRConv(32, 128, 96, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
+    g = Graph(src, dst, V)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", fused)
+    a = _run(m, g, X, dY)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", not fused)
+    b = _run(m, g, X, dY)
+    for k in a:
+        e = (a[k] - b[k]).norm() / b[k].norm().clamp_min(1e-30)
+        assert e < 1e-5, (k, float(e))

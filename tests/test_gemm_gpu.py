@@ -300,8 +300,8 @@ def test_gemm_nt_weight_resident_opt_in_bit_identical(M, K, N, monkeypatch):
 @pytest.mark.parametrize("M,K,N", [(70001, 256, 256), (4099, 256, 512), (3001, 128, 256), (66000, 512, 256),
                                    (513, 256, 300), (1, 512, 256), (255, 128, 512)])
 def test_gemm_nt_dma_kernel_vs_persistent(M, K, N, monkeypatch):
-    """The LDS-DMA NT kernel (sirconv_gemm_g.hip, the default for K in {128, 256, 512}, N in (128,
-    512]) against k_gemm_nt_p (SIR_NT_G=0): both within the fp64 bound, on rows spanning 2^60 of
+    """The LDS-DMA NT kernel (sirconv_gemm_g.hip, opt-in SIR_NT_G=1, K in {128, 256, 512}, N in (128,
+    512]) against k_gemm_nt_p (the default): both within the fp64 bound, on rows spanning 2^60 of
     range, rows whose maximum grows by 2^40 along K (the rescale branch), a strided C (the columns
     around it untouched) and a ragged last tile."""
     g = torch.Generator(device=DEV).manual_seed(M * 7 + K)

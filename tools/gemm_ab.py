@@ -45,7 +45,14 @@ def main():
     W2 = torch.randn(2 * H, H, device=dev, generator=g) / H ** 0.5
     WR = torch.randn(H, H, device=dev, generator=g) / H ** 0.5
     b2 = torch.randn(2 * H, device=dev, generator=g)
-    libs = [(kv.split("=", 1)[0], open_lib(kv.split("=", 1)[1])) for kv in a.libs]
+    # name=path[@VAR=value]: the variable is set in the environment around every call of that library
+    # (kernel routes the library reads per call, e.g. SIR_NT_G=1)
+    libs, envs = [], {}
+    for kv in a.libs:
+        name, rest = kv.split("=", 1)
+        path, _, env = rest.partition("@")
+        libs.append((name, open_lib(path)))
+        envs[name] = tuple(env.split("=", 1)) if env else None
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def pack(lib, W, trans):
@@ -70,6 +77,11 @@ def main():
     ws = torch.empty(max(lib.sir_gemm_tn_workspace(V, 2 * H, H) for _, lib in libs), dtype=torch.uint8, device=dev)
 
     def run(n, lib, s):
+        if envs[n]:
+            os.environ[envs[n][0]] = envs[n][1]
+        else:
+            for e in {x[0] for x in envs.values() if x}:
+                os.environ.pop(e, None)
         v = shapes[s]
         if len(v) == 4:
             A, _, _, bias = v
