@@ -479,7 +479,9 @@ def roofline_fwd(args, kernels, V, E, V_src, H, s, world):
     uniq = fwd_unique_bytes(V_src, V, E, H, s)
     ach = alg / t / 1e9
     traffic = None
-    pmc_file = args.pmc_file or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.graph}.json")
+    dts = args.dtype or "f32"
+    pmc_file = args.pmc_file or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.graph}"
+                                             f"{'' if dts == 'f32' else '_' + dts}.json")
     try:
         with open(pmc_file) as f:
             pmc = json.load(f)

@@ -413,6 +413,154 @@ k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     }
 }
 
+// Persistent form for H <= 128, F <= 256 (the DictionaryLookup sigma of config 1):
+// 8 waves, wave w owns feature tile w and keeps its whole weight slice (hi and lo, NGT k16 steps:
+// 8 NGT VGPRs) in registers for the life of the block, which walks work items b, b + grid, ...  The
+// weight is read once per block instead of once per 32-edge tile (k_mlp_fwd16 streamed the packed W
+// from L2 for every tile: ~128 GB of L2 reads per S1 forward).  Everything else is k_mlp_fwd16.
+template <int ACT1, int ACT2, int RED, int NGT>
+__global__ void __launch_bounds__(512)
+k_mlp_fwd16p(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
+             int64_t n_items, const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
+             const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope,
+             int H, int F, const h8v* __restrict__ Wp16, const float* __restrict__ winv,
+             const float* __restrict__ bias, float* __restrict__ out, int64_t ldo, int* __restrict__ arg, int64_t lda,
+             float* __restrict__ pval, int* __restrict__ parg) {
+    constexpr int NW = 8, RPW = 4;
+    constexpr int NG = NGT;
+    __shared__ __attribute__((aligned(16))) char img[NG * 2048];
+    __shared__ float sInv[32], sC[32];
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ntile = (F + 31) / 32;
+    const bool has_t = w < ntile;                 // wave-uniform: waves past F only stage
+    const int n = 32 * w + (l & 31);
+    const float bbv = (bias != nullptr && n < F) ? bias[n] : 0.f;
+    const float iwv = (n < F) ? winv[n] : 0.f;
+    h8v whi[NG], wlo[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (has_t) {
+            whi[g] = Wp16[(((int64_t)w * NG + g) * 2 + 0) * 64 + l];
+            wlo[g] = Wp16[(((int64_t)w * NG + g) * 2 + 1) * 64 + l];
+        } else {
+            whi[g] = h8v{};
+            wlo[g] = h8v{};
+        }
+    }
+    const int fo = mlp_fimg(l & 31, l >> 5);
+    for (int64_t itx = blockIdx.x; itx < n_items; itx += gridDim.x) {
+        const int4 it = uniform_item(items, itx);
+        const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
+        const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
+        const float* qp = Q + (int64_t)row * ldq;
+        const int k4 = 4 * l;
+        const float4 q4 = (k4 < H) ? *reinterpret_cast<const float4*>(qp + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float racc = 0.f, best = -INFINITY;
+        int bidx = INT_MAX;
+        for (int t0 = e0; t0 < e1; t0 += 32) {
+            const int nv = (e1 - t0) < 32 ? (e1 - t0) : 32;
+            float4 kv[RPW];
+#pragma unroll
+            for (int ii = 0; ii < RPW; ++ii) {
+                const int i = w + NW * ii;
+                const int u = col[t0 + (i < nv ? i : 0)];
+                kv[ii] = (k4 < H) ? *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k4)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int ii = 0; ii < RPW; ++ii) {
+                const int i = w + NW * ii;
+                const bool ok = i < nv && k4 < H;
+                float4 a4;
+                a4.x = ok ? act_f<ACT1>(q4.x + kv[ii].x, slope) : 0.f;
+                a4.y = ok ? act_f<ACT1>(q4.y + kv[ii].y, slope) : 0.f;
+                a4.z = ok ? act_f<ACT1>(q4.z + kv[ii].z, slope) : 0.f;
+                a4.w = ok ? act_f<ACT1>(q4.w + kv[ii].w, slope) : 0.f;
+                float m = fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w)));
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+                const int se = mlp_scale_exp(m);
+                const float sc = mlp_pow2(se);
+                if (k4 < NG * 16) {
+                    const float y[4] = {a4.x * sc, a4.y * sc, a4.z * sc, a4.w * sc};
+                    _Float16 hv[4], lv[4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
+                    const int g = k4 >> 4, h = (k4 >> 3) & 1, j8 = k4 & 7;
+                    char* d = img + g * 2048 + mlp_fimg(i, h) + j8 * 2;
+                    *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
+                    *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
+                }
+                if (l == 0) sInv[i] = mlp_pow2(-se);
+            }
+            if (w == 0 && l < 32) {
+                float c = 0.f;
+                if (l < nv) c = (RED == AGG_SYM) ? norm_col[col[t0 + l]] * nr : 1.f;   // conv.py:45 operand order
+                sC[l] = c;
+            }
+            __syncthreads();
+            if (has_t) {
+                mf16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    const h8v ahi = *reinterpret_cast<const h8v*>(img + g * 2048 + fo);
+                    const h8v alo = *reinterpret_cast<const h8v*>(img + g * 2048 + 1024 + fo);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = drow(r, l);
+                    if (i < nv) {
+                        const float m = act_f<ACT2>(acc[r] * sInv[i] * iwv + bbv, slope);
+                        if constexpr (RED == 3) {
+                            if (m > best) { best = m; bidx = t0 + i; }    // strict >: first wins
+                        } else {
+                            racc += sC[i] * m;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (has_t) {
+            if constexpr (RED == 3) {
+                const float ob = __shfl_xor(best, 32);
+                const int oi = __shfl_xor(bidx, 32);
+                if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+                if (l < 32 && n < F) {
+                    const bool any = bidx != INT_MAX;
+                    if (slot < 0) {
+                        out[(int64_t)row * ldo + n] = any ? best : 0.f;
+                        arg[(int64_t)row * lda + n] = any ? bidx : -1;
+                    } else {
+                        pval[(int64_t)slot * F + n] = best;
+                        parg[(int64_t)slot * F + n] = bidx;
+                    }
+                }
+            } else {
+                const float other = __shfl_xor(racc, 32);
+                float v = (l < 32) ? racc + other : other + racc;
+                if (l < 32 && n < F) {
+                    if (slot < 0) {
+                        if constexpr (RED == AGG_MEAN) {
+                            const int d = e1 - e0;
+                            v = v / (float)(d > 1 ? d : 1);
+                        }
+                        out[(int64_t)row * ldo + n] = v;
+                    } else {
+                        pval[(int64_t)slot * F + n] = v;
+                    }
+                }
+            }
+        }
+    }
+}
+
 // max: combine the chunk partials of split rows in chunk (= edge) order, strict > (first wins)
 __global__ void k_mlp_max_combine(const int4* __restrict__ splits, int F, const float* __restrict__ pval,
                                   const int* __restrict__ parg, float* __restrict__ Y, int64_t ldy,
@@ -668,11 +816,36 @@ int64_t mlp_pack16_bytes(int H, int F) {
     return (int64_t)FP * mlp_ng(H) * 16 * 2 * 2 + (int64_t)FP * 4;
 }
 
+#ifndef SIR_MLP_RESIDENT
+// 1: H <= 128, F <= 256 on k_mlp_fwd16p (weights resident in registers, persistent blocks): cfg1 0.302 ->
+// 0.294 ms; at H = 256 it was slower than the per-item kernel (S1 max forward 15.5 vs 14.4 ms,
+// profiles/r03_ab_mlp_resident.txt: the W stream from L2 was not the bound), so NG = 16 stays per-item
+#define SIR_MLP_RESIDENT 1
+#endif
 template <int ACT1, int ACT2, int RED>
 hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
     const int NG = mlp_ng(a.H), FP = (a.F + 31) / 32 * 32;
     const h8v* w16 = static_cast<const h8v*>(p16);
     const float* winv = reinterpret_cast<const float*>(static_cast<const char*>(p16) + (int64_t)FP * NG * 64);
+    if (SIR_MLP_RESIDENT && a.F <= 256 && (NG == 4 || NG == 8)) {
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        // resident blocks only (a persistent block never yields its CU): NG = 16 takes ~208 VGPRs (one
+        // 512-thread block per CU), NG <= 8 fits two
+        const int64_t cap = (int64_t)ncu * (NG == 16 ? 1 : 2);
+        const int64_t nb = a.n_items < cap ? a.n_items : cap;
+        const dim3 g((unsigned)nb);
+#define SIR_MLP_FWD16P(NGV)                                                                                         \
+        hipLaunchKernelGGL((k_mlp_fwd16p<ACT1, ACT2, RED, NGV>), g, dim3(512), 0, st, a.rowptr, a.col,                 \
+                           reinterpret_cast<const int4*>(a.items), a.n_items, a.Q, a.ldq, a.K, a.ldk, a.norm_row,      \
+                           a.norm_col, a.slope, a.H, a.F, w16, winv, a.bias, a.out, a.ldo, a.arg, a.lda, a.pval, a.parg)
+        if (NG == 4) SIR_MLP_FWD16P(4);
+        else SIR_MLP_FWD16P(8);
+#undef SIR_MLP_FWD16P
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)NG * 2048 + 64 * sizeof(float);
 #define SIR_MLP_FWD16(NWV, TPWV, C4V)                                                                            \
     hipLaunchKernelGGL((k_mlp_fwd16<ACT1, ACT2, RED, NWV, TPWV, C4V>), grid, dim3(64 * NWV), lds, st, a.rowptr,     \

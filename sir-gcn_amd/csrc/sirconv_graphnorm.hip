@@ -8,8 +8,8 @@
 //   backward: A = sum gy*d, G = sum gy;  gd = w*gy/std - w*d*A/(n*std^3);  Bs = sum gd;
 //             dx = gd - ms*Bs/n;  per-graph partials A/std, -mean*Bs, G for dw, dms, db
 //             (reduced over graphs by the host with the deterministic column sum).
-// The whole graph is re-read from L2 by each pass (molecule-sized graphs: a few KB), 8 rows' loads in
-// flight at a time (walk_rows).
+// The whole graph is re-read from L2 by each pass (molecule-sized graphs: a few KB), 32 (forward) / 16
+// (backward, two arrays) rows' loads in flight at a time (walk_rows).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,11 +35,11 @@ __device__ __forceinline__ void gst(float* __restrict__ p, const float (&s)[VW])
 }
 
 
-// Walk rows [r0, r1) in node order, RB rows' loads in flight at a time (a molecule has ~25 rows: a
-// one-load-per-iteration loop paid one memory latency per row and pass, ~40 us per launch on cfg5);
+// Walk rows [r0, r1) in node order, RB rows' loads in flight at a time (a molecule has ~25 rows: the
+// forward's passes take one memory latency each, the backward's two; a one-load-per-iteration loop
+// paid one latency per row and pass, ~40 us per launch on cfg5);
 // f(i, v) is applied in row order, so every per-graph sum keeps the reference's node order.
-constexpr int RB = 8;
-template <int VW, typename Fn>
+template <int VW, int RB = 32, typename Fn>
 __device__ __forceinline__ void walk_rows(int64_t r0, int64_t r1, const float* __restrict__ base, int64_t ld, int c,
                                           Fn f) {
     int64_t i = r0;
@@ -61,7 +61,7 @@ __device__ __forceinline__ void walk_rows(int64_t r0, int64_t r1, const float* _
     }
 }
 // the same over two row-aligned arrays (X and dY)
-template <int VW, typename Fn>
+template <int VW, int RB = 16, typename Fn>
 __device__ __forceinline__ void walk_rows2(int64_t r0, int64_t r1, const float* __restrict__ a, int64_t lda,
                                            const float* __restrict__ b, int64_t ldb, int c, Fn f) {
     int64_t i = r0;

@@ -76,21 +76,25 @@ def main():
     ap.add_argument("--graph", default="S2")
     ap.add_argument("--agg", default="sum")
     ap.add_argument("--H", type=int, default=256)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16", "f16"])
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
     fetch = by_pass(load(a.fetch_dir, "FETCH_SIZE"))
     write = by_pass(load(a.write_dir, "WRITE_SIZE"))
-    res = {"graph": a.graph, "agg": a.agg, "H": a.H,
+    res = {"graph": a.graph, "agg": a.agg, "H": a.H, "dtype": a.dtype,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes = "
                      "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per launch (gfx950 FETCH_SIZE half-count "
-                     "correction for 16 B/lane reads); median over launches",
+                     "correction for 16 B/lane reads); median over launches"
+                     + ("" if a.dtype == "f32" else "; 16-bit storage gathers 8 B per lane, a width the x2 "
+                        "correction is not calibrated for (MI355X_MICROARCH.md): fetch bytes are an upper "
+                        "bound, fetch_kib_raw the lower one"),
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = sorted(fetch.get(k, [0.0]))
         w = sorted(write.get(k, [0.0]))
         fm, wm = f[len(f) // 2], w[len(w) // 2]
-        res["kernels"][k] = {"fetch_kib": fm, "write_kib": wm, "launches": len(f),
+        res["kernels"][k] = {"fetch_kib": fm, "fetch_kib_raw": fm, "write_kib": wm, "launches": len(f),
                              "hbm_bytes_per_launch": int(2 * fm * 1024 + wm * 1024)}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as fh:

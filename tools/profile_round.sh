@@ -12,4 +12,6 @@ timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --outp
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/pmc_write.log" 2>&1
 GRAPH=$(echo "$ARGS" | sed -n 's/.*--graph \([A-Za-z0-9]*\).*/\1/p'); GRAPH=${GRAPH:-S2}
 AGG=$(echo "$ARGS" | sed -n 's/.*--agg \([a-z]*\).*/\1/p'); AGG=${AGG:-sum}
-python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --graph "$GRAPH" --agg "$AGG" --out "$OUT/pmc_traffic_$GRAPH.json" > /dev/null
+DT=$(echo "$ARGS" | sed -n 's/.*--dtype \([a-z0-9]*\).*/\1/p'); DT=${DT:-f32}
+SUF=$([ "$DT" = f32 ] && echo "" || echo "_$DT")
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --graph "$GRAPH" --agg "$AGG" --dtype "$DT" --out "$OUT/pmc_traffic_$GRAPH$SUF.json" > /dev/null
