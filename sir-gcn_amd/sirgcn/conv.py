@@ -190,7 +190,8 @@ class SIRConvFunction(torch.autograd.Function):
         H = W_Q.shape[0]
         X = X.contiguous()
         W_cat = torch.cat([W_Q, W_K], 0)
-        QK = linalg.mm_wt(X, W_cat, torch.cat([b_Q, b_Q.new_zeros(H)]) if b_Q is not None else None, drop=drop)
+        # [b_Q; 0] by one pad kernel (a zeros fill + a cat were two launches: small batches are launch-bound)
+        QK = linalg.mm_wt(X, W_cat, F.pad(b_Q, (0, H)) if b_Q is not None else None, drop=drop)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=torch.float32)
@@ -255,7 +256,7 @@ class SIRConvFunction16(torch.autograd.Function):
     def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on, dt, drop=None):
         H = W_Q.shape[0]
         W_cat = torch.cat([W_Q, W_K], 0)
-        b_cat = torch.cat([b_Q, b_Q.new_zeros(H)]) if b_Q is not None else None
+        b_cat = F.pad(b_Q, (0, H)) if b_Q is not None else None
         X = X.contiguous()
         if X.dtype == dt:
             Xh = X
