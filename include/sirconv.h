@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 9
+#define SIR_ABI_VERSION 10
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -61,8 +61,8 @@ enum { SIR_DTYPE_F32 = 0, SIR_DTYPE_BF16 = 1, SIR_DTYPE_F16 = 2 };
 enum { SIR_OK = 0, SIR_EINVAL = 1, SIR_EUNSUPPORTED = 2, SIR_ELAUNCH = 3 };
 
 int sir_abi_version(void);
-/* First 16 hex digits of sha256 over the library's kernel and ABI sources (csrc/*.hip, *.h, *.cpp and
- * include/*.h, concatenated in path order) at build time: lets a host detect a stale prebuilt library. */
+/* First 16 hex digits of sha256 over the library's kernel and ABI sources (the .hip, .h and .cpp files
+ * of csrc/ and the .h files of include/, concatenated in path order) at build time: lets a host detect a stale prebuilt library. */
 const char* sir_source_hash(void);
 const char* sir_last_error(void);
 
@@ -367,6 +367,15 @@ int sir_gemm_pack(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, 
  * 4; A, C, bias 16-B aligned.  Replaces addmm(b, X, W^T) / mm(X, W). */
 int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
                 const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream);
+
+/* Small batches (config 5's 1.6k-node molecule batches): C[M, N] = A[M, K] B^T + bias with the
+ * weight read as fp32 straight from W (B[n][k] = W[n*ldw + k], trans = 0, or W[k*ldw + n], trans =
+ * 1) — no packing pass per weight update; both operands split in the kernel, each with running
+ * scales.  Same accuracy bar as sir_gemm_nt (fp32-equivalent); any M, but the 32 x 32 tiles and the
+ * in-kernel weight split make it the route for M below ~16k rows only.  K, N, lda, ldc multiples of
+ * 4; A, C, bias 16-B aligned; ldw <= SIR_GEMM_MAX_LD.  Replaces addmm(b, X, W^T) / mm(X, W). */
+int sir_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int64_t K, const float* W, int64_t ldw, int trans,
+                       int64_t N, const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream);
 
 /* C[M, N] = A^T B with A [R, M] (lda), B [R, N] (ldb): the weight gradients (contraction over the
  * R node rows, split over row ranges; the partial products are added in a fixed order, so the

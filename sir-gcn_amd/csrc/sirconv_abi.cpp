@@ -585,6 +585,25 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
     return finish(fn, err, nullptr);
 }
 
+int sir_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int64_t K, const float* W, int64_t ldw, int trans,
+                       int64_t N, const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream) {
+    const char* fn = "sir_gemm_nt_direct";
+    if (M < 0 || N <= 0 || K <= 0 || N > 65536 || K > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if ((M + 31) / 32 * ((N + 31) / 32) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
+    if (K % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldc % 4 != 0 || lda < K || ldc < N)
+        return fail(SIR_EINVAL, fn, "K, N, lda, ldc must be multiples of 4 (lda >= K, ldc >= N)");
+    if (trans != 0 && trans != 1) return fail(SIR_EINVAL, fn, "trans must be 0 or 1");
+    if (ldw < (trans ? N : K)) return fail(SIR_EINVAL, fn, "ldw too small");
+    if (lda > SIR_GEMM_MAX_LD || ldw > SIR_GEMM_MAX_LD) return fail(SIR_EINVAL, fn, "lda/ldw too large");
+    if (M > 0 && (A == nullptr || C == nullptr || W == nullptr)) return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(bias)) & 15u) != 0)
+        return fail(SIR_EINVAL, fn, "A, C and bias must be 16-B aligned");
+    if ((reinterpret_cast<uintptr_t>(W) & 3u) != 0) return fail(SIR_EINVAL, fn, "W must be 4-B aligned");
+    hipError_t err = sir::run_gemm_nt_direct(A, lda, M, (int)K, W, ldw, trans, (int)N, bias, C, ldc,
+                                             static_cast<hipStream_t>(stream), to_drop(drop, 0));
+    return finish(fn, err, nullptr);
+}
+
 int64_t sir_gemm_tn_workspace(int64_t R, int64_t M, int64_t N) {
     if (R < 0 || M <= 0 || N <= 0 || M > 65536 || N > 65536) return 0;
     return sir::gemm_tn_workspace(R, M, N);

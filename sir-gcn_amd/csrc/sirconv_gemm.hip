@@ -1175,7 +1175,408 @@ k_gemm_reduce(const float* __restrict__ part, int P, int64_t count, int Nc, floa
     C[(i / Nc) * ldc + i % Nc] = s;
 }
 
+// ------------------------------------------------------------------------------------------
+// Small-batch GEMMs (fewer than gemm_small_rows() node rows: config-5 / config-1 / ZINC batches of
+// a few thousand nodes).  The block-tiled kernels above have 256-row tiles: a 1.6k-row batch is 7
+// tiles on a 256-CU chip.  Here ONE WAVE owns one small output tile and runs alone — no LDS stage,
+// no barrier: its operand fragments come straight from global memory into registers (the data
+// rows' fp32 values, split in registers; the packed weight's fragments, in lane order, from L2),
+// the next 32-k chunk in flight while the current one is multiplied.  Same split, running-scale
+// rule and MFMA order per accumulator as k_gemm_nt_p / k_gemm_tn, so the NT result is
+// bit-identical to k_gemm_nt_p's (tests/test_gemm_gpu.py).
+//
+// k_gemm_nt_s: wave = 32 data rows x 32*S_FT features.  Lane l = 32h + r holds row r's k-range
+// 8h .. 8h+7 of each k16 step (the MFMA B-operand fragment), i.e. two 32-B pieces per 32-k chunk.
+constexpr int S_FT = 2;
+
+template <bool KFULL>
+__global__ void __launch_bounds__(256)
+k_gemm_nt_s(const float* __restrict__ A, int64_t lda, int64_t M, int K, const u4v* __restrict__ Wp, int Npad, int Kc,
+            const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C, int64_t ldc,
+            int nfg, int64_t n_waves, Drop drop) {
+    const int l = threadIdx.x & 63, r = l & 31, h = l >> 5;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= n_waves) return;                       // whole waves (4 per block)
+    const int64_t d0 = (w / nfg) * 32;
+    const int f0 = (int)(w % nfg) * S_FT;           // first 32-feature tile
+    const int rows = (M - d0 < 32) ? (int)(M - d0) : 32;
+    const rsrc_t ars = mk_rsrc(A + d0 * lda, (uint32_t)(rows * lda * 4));
+    const rsrc_t wrs = mk_rsrc(Wp, (uint32_t)((int64_t)Kc * 4 * Npad * 32));
+    const int aoff = (r * (int)lda + 8 * h) * 4;
+    const int woff = 16 * l;
+    float4 av[2][4];                                // [set][ks * 2 + q]: k = 32c + 16ks + 8h + 4q + (0..3)
+    u4v wv[2][S_FT][2][2];                          // [set][tile][part][ks]
+    auto load = [&](int set, int c) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u4v u = __builtin_amdgcn_raw_buffer_load_b128(ars, aoff + ((i >> 1) * 16 + (i & 1) * 4) * 4, c * KC * 4, 0);
+            av[set][i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+        }
+#pragma unroll
+        for (int a = 0; a < S_FT; ++a)
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    wv[set][a][pt][ks] = __builtin_amdgcn_raw_buffer_load_b128(
+                        wrs, woff, ((c * 2 + pt) * 2 + ks) * Npad * 32 + (f0 + a) * 1024, 0);
+    };
+    f16v acc[S_FT];
+#pragma unroll
+    for (int a = 0; a < S_FT; ++a)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[a][i] = 0.f;
+    int se_run = SE_INIT;
+    auto chunk = [&](int set, int c, bool first) {
+        float4 x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = av[set][i];
+        if (!KFULL && c == Kc - 1) {                 // columns past K (the next row's values) read as 0
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = c * KC + (i >> 1) * 16 + 8 * h + (i & 1) * 4;
+                x[i].x = k + 0 < K ? x[i].x : 0.f;
+                x[i].y = k + 1 < K ? x[i].y : 0.f;
+                x[i].z = k + 2 < K ? x[i].z : 0.f;
+                x[i].w = k + 3 < K ? x[i].w : 0.f;
+            }
+        }
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m = fmax4(m, x[i]);
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const int se_old = first ? SE_INIT : se_run, se = next_se(se_old, bexp(m));
+        se_run = se;
+        if (!first) {
+            const float f = pow2(se - se_old);
+            if (__builtin_amdgcn_ballot_w64(f != 1.f) != 0) {
+#pragma unroll
+                for (int a = 0; a < S_FT; ++a) acc[a] *= f;
+            }
+        }
+        const float s = pow2(se);
+        h8 dh[2], dl[2];
+        split8(x[0], x[1], s, dh[0], dl[0]);
+        split8(x[2], x[3], s, dh[1], dl[1]);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int a = 0; a < S_FT; ++a)
+                acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, wv[set][a][0][ks]), dh[ks], acc[a], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < S_FT; ++a)
+                acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, wv[set][a][0][ks]), dl[ks], acc[a], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < S_FT; ++a)
+                acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8, wv[set][a][1][ks]), dh[ks], acc[a], 0, 0, 0);
+        }
+    };
+    // chunk pairs with static register sets; every pair issues its loads (the last chunk's are
+    // re-issued past the end: same addresses, unused), so the wait counts stay exact
+    load(0, 0);
+    int c = 0;
+    for (; c + 2 <= Kc; c += 2) {
+        load(1, c + 1);
+        chunk(0, c, c == 0);
+        load(0, (c + 2 < Kc) ? c + 2 : Kc - 1);
+        chunk(1, c + 1, false);
+    }
+    if (c < Kc) chunk(0, c, c == 0);
+
+    // C[m][n] = acc * 2^-se(m) * inv_t[n] + bias[n] (k_gemm_nt_p's epilogue arithmetic)
+    const float is = pow2(-se_run);
+    const int64_t row = d0 + r;
+    if (row < M) {
+#pragma unroll
+        for (int a = 0; a < S_FT; ++a) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = (f0 + a) * 32 + 8 * g + 4 * h;
+                if (n < N) {
+                    const float4 it = *reinterpret_cast<const float4*>(inv_t + n);
+                    const float4 bb = bias != nullptr ? *reinterpret_cast<const float4*>(bias + n)
+                                                      : make_float4(-0.f, -0.f, -0.f, -0.f);
+                    float4 o;
+                    o.x = acc[a][4 * g + 0] * is * it.x + bb.x;
+                    o.y = acc[a][4 * g + 1] * is * it.y + bb.y;
+                    o.z = acc[a][4 * g + 2] * is * it.z + bb.z;
+                    o.w = acc[a][4 * g + 3] * is * it.w + bb.w;
+                    if (drop.on()) drop4(drop, row, n, o);
+                    *reinterpret_cast<float4*>(C + row * ldc + n) = o;
+                }
+            }
+        }
+    }
+}
+
+// Small contractions with both operands split in the kernel (no packed weight): a block of 4 waves
+// owns one 32 x 32 output tile, the waves take the 32-k chunks c = q, q + 4, ... of the contraction
+// (up to 4 chunks' operands loaded at once: one memory latency per 4 chunks, not one per chunk), each
+// with running scales on both operands (k_gemm_tn's rule), and the 4 partial tiles are added in wave
+// order through LDS.  Operand line j (an MFMA row of src0 / column of src1) of lane l = 32h + j holds
+// k = 32c + 16ks + 8h + (0..7): CONTIG lines run along k in memory (x[j * ld + k]: A rows, an
+// nn.Linear weight's rows), strided ones across it (x[k * ld + j]: the node-row contraction of the
+// weight gradients, a transposed weight).
+//   k_gemm_nt_sw : C = A W^T + bias (or A W), W read as fp32 (sir_gemm_nt_direct)
+//   k_gemm_tn_s  : part[p] = A[rows_p]^T B[rows_p] (+ column sums of A)
+template <bool CONTIG>
+struct SOp {
+    const float* x;      // element (line 0, k 0) of the tile
+    int64_t ld;          // elements between lines (CONTIG) / between k (strided)
+    int lines, klen;     // valid lines, contraction length
+    int j;               // this lane's line, clamped to a valid one
+    // the lane's 16 values of chunk c (zeros past klen; lines past `lines` re-read line 0's values:
+    // they feed only their own outputs, which are never stored)
+    __device__ __forceinline__ void load(float (&v)[16], int c, bool live, int h) const {
+        if constexpr (CONTIG) {
+            const rsrc_t rs = mk_rsrc(x, live ? (uint32_t)((int64_t)lines * ld * 4) : 0u);
+            const int voff = (int)((j * ld + 8 * h) * 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const u4v u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, (c * KC + (i >> 1) * 16 + (i & 1) * 4) * 4, 0);
+                v[4 * i + 0] = __uint_as_float(u.x); v[4 * i + 1] = __uint_as_float(u.y);
+                v[4 * i + 2] = __uint_as_float(u.z); v[4 * i + 3] = __uint_as_float(u.w);
+            }
+        } else {
+            const int64_t k0 = (int64_t)c * KC;
+            const int64_t left = klen - k0;
+            const uint32_t kr = (!live || left <= 0) ? 0u : (uint32_t)(left < KC ? left : KC);
+            const rsrc_t rs = mk_rsrc(x + (kr ? k0 : 0) * ld, kr * (uint32_t)ld * 4u);
+            const int voff = (int)((8 * h * ld + j) * 4);
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, ((i >> 3) * 16 + (i & 7)) * (int)ld * 4, 0));
+        }
+    }
+    // CONTIG: k past klen inside the last chunk reads the next line's values -> zero them
+    __device__ __forceinline__ void mask_tail(float (&v)[16], int c, int h) const {
+        if constexpr (CONTIG) {
+            if ((c + 1) * KC > klen) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int k = c * KC + (i >> 3) * 16 + 8 * h + (i & 7);
+                    v[i] = k < klen ? v[i] : 0.f;
+                }
+            }
+        }
+    }
+};
+
+// The contraction of one wave: chunks q, q + 4, ... < nc; returns the partial tile in true scale
+// (acc * 2^-se0(row i) * 2^-se1(lane column)) in p, and (if CS) the sums of the lane's src0 values.
+template <bool C0, bool C1, bool CS>
+__device__ __forceinline__ void small_contract(const SOp<C0>& o0, const SOp<C1>& o1, int nc, int q, int h,
+                                               float (&p)[16], float& cs) {
+    f16v acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    int se0 = SE_INIT, se1 = SE_INIT;
+    bool first = true;
+    auto colmax = [&](const float (&x)[16]) {
+        float mm = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) mm = fmax4(mm, make_float4(x[i], x[i + 1], x[i + 2], x[i + 3]));
+        return fmaxf(mm, __shfl_xor(mm, 32));
+    };
+    for (int cb = q; cb < nc; cb += 16) {
+        float x0[4][16], x1[4][16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int c = cb + 4 * g;
+            o0.load(x0[g], c, c < nc, h);
+            o1.load(x1[g], c, c < nc, h);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int c = cb + 4 * g;
+            if (c >= nc) break;
+            o0.mask_tail(x0[g], c, h);
+            o1.mask_tail(x1[g], c, h);
+            const int s0 = first ? SE_INIT : se0, s1 = first ? SE_INIT : se1;
+            se0 = next_se(s0, bexp(colmax(x0[g])));
+            se1 = next_se(s1, bexp(colmax(x1[g])));
+            if (!first) {
+                const float f0 = pow2(se0 - s0), f1 = pow2(se1 - s1);
+                if (__builtin_amdgcn_ballot_w64(f0 != 1.f || f1 != 1.f) != 0) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) acc[i] *= __shfl(f0, (i & 3) + 8 * (i >> 2) + 4 * h) * f1;
+                }
+            }
+            first = false;
+            if constexpr (CS) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) cs += x0[g][i];
+            }
+            h8 ah[2], al[2], bh[2], bl[2];
+            const float sa = pow2(se0), sb = pow2(se1);
+            split8(make_float4(x0[g][0], x0[g][1], x0[g][2], x0[g][3]), make_float4(x0[g][4], x0[g][5], x0[g][6], x0[g][7]), sa, ah[0], al[0]);
+            split8(make_float4(x0[g][8], x0[g][9], x0[g][10], x0[g][11]), make_float4(x0[g][12], x0[g][13], x0[g][14], x0[g][15]), sa, ah[1], al[1]);
+            split8(make_float4(x1[g][0], x1[g][1], x1[g][2], x1[g][3]), make_float4(x1[g][4], x1[g][5], x1[g][6], x1[g][7]), sb, bh[0], bl[0]);
+            split8(make_float4(x1[g][8], x1[g][9], x1[g][10], x1[g][11]), make_float4(x1[g][12], x1[g][13], x1[g][14], x1[g][15]), sb, bh[1], bl[1]);
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh[ks], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl[ks], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh[ks], acc, 0, 0, 0);
+            }
+        }
+    }
+    const float i0 = pow2(-se0), i1 = pow2(-se1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = acc[i] * __shfl(i0, (i & 3) + 8 * (i >> 2) + 4 * h) * i1;
+}
+
+// C[d0 + r][n0 + n] = sum_k A[d0 + r][k] W(n0 + n, k) + bias: src0 = W lines (features), src1 = A rows
+template <bool TRANS>
+__global__ void __launch_bounds__(256)
+k_gemm_nt_sw(const float* __restrict__ A, int64_t lda, int64_t M, int K, const float* __restrict__ W, int64_t ldw,
+             int N, const float* __restrict__ bias, float* __restrict__ C, int64_t ldc, int nft, Drop drop) {
+    __shared__ float red[4][16][64];
+    const int l = threadIdx.x & 63, r = l & 31, h = l >> 5, q = threadIdx.x >> 6;
+    const int64_t d0 = (int64_t)(blockIdx.x / nft) * 32;
+    const int n0 = (int)(blockIdx.x % nft) * 32;
+    const int rows = (M - d0 < 32) ? (int)(M - d0) : 32, feats = (N - n0 < 32) ? N - n0 : 32;
+    SOp<true> oa{A + d0 * lda, lda, rows, K, r < rows ? r : 0};
+    SOp<!TRANS> ow{TRANS ? W + n0 : W + (int64_t)n0 * ldw, ldw, feats, K, r < feats ? r : 0};
+    float p[16], cs = 0.f;
+    small_contract<!TRANS, true, false>(ow, oa, (K + KC - 1) / KC, q, h, p, cs);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[q][i][l] = p[i];
+    __syncthreads();
+    // wave q: acc elements 4q .. 4q+3 = features n0 + 8q + 4h + (0..3) of data row d0 + r
+    const int64_t row = d0 + r;
+    const int n = n0 + 8 * q + 4 * h;
+    if (row < M && n < N) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int i = 4 * q + e;
+            v[e] = ((red[0][i][l] + red[1][i][l]) + red[2][i][l]) + red[3][i][l];
+        }
+        const float4 bb = bias != nullptr ? *reinterpret_cast<const float4*>(bias + n) : make_float4(-0.f, -0.f, -0.f, -0.f);
+        float4 o = make_float4(v[0] + bb.x, v[1] + bb.y, v[2] + bb.z, v[3] + bb.w);
+        if (drop.on()) drop4(drop, row, n, o);
+        *reinterpret_cast<float4*>(C + row * ldc + n) = o;
+    }
+}
+
+// part[p][m0 + m][n0 + n] = sum over the split's rows of A[v][m0 + m] B[v][n0 + n]: src0 = A columns,
+// src1 = B columns (both strided: the contraction runs over the node rows)
+__global__ void __launch_bounds__(256)
+k_gemm_tn_s(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb, int64_t R, int Mc,
+            int Nc, float* __restrict__ part, float* __restrict__ csum_part, int nmt, int nnt, int64_t rps) {
+    __shared__ float red[4][16][64];
+    __shared__ float cred[4][64];
+    const int l = threadIdx.x & 63, r = l & 31, h = l >> 5, q = threadIdx.x >> 6;
+    const int tiles = nmt * nnt;
+    const int64_t p = blockIdx.x / tiles;
+    const int mt = (int)(blockIdx.x % tiles) / nnt, nt = (int)(blockIdx.x % tiles) % nnt;
+    const int m0 = mt * 32, n0 = nt * 32;
+    const int64_t v0 = p * rps, v1 = (v0 + rps < R) ? v0 + rps : R;
+    const int klen = v1 > v0 ? (int)(v1 - v0) : 0;
+    const int mcols = (Mc - m0 < 32) ? Mc - m0 : 32, ncols = (Nc - n0 < 32) ? Nc - n0 : 32;
+    SOp<false> oa{A + (klen ? v0 : 0) * lda + m0, lda, mcols, klen, r < mcols ? r : 0};
+    SOp<false> ob{B + (klen ? v0 : 0) * ldb + n0, ldb, ncols, klen, r < ncols ? r : 0};
+    const bool do_cs = csum_part != nullptr && nt == 0;
+    float pv[16], cs = 0.f;
+    if (do_cs) small_contract<false, false, true>(oa, ob, (klen + KC - 1) / KC, q, h, pv, cs);
+    else small_contract<false, false, false>(oa, ob, (klen + KC - 1) / KC, q, h, pv, cs);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[q][i][l] = pv[i];
+    cred[q][l] = cs;
+    __syncthreads();
+    // wave q: acc elements 4q .. 4q+3 = A columns m0 + 8q + 4h + (0..3), B column n0 + r
+    float* out = part + p * (int64_t)Mc * Nc;
+    const int n = n0 + r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int i = 4 * q + e, m = m0 + 8 * q + 4 * h + e;
+        const float v = ((red[0][i][l] + red[1][i][l]) + red[2][i][l]) + red[3][i][l];
+        if (m < Mc && n < Nc) out[(int64_t)m * Nc + n] = v;
+    }
+    if (do_cs && q == 0 && h == 0 && r < mcols) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) t += cred[w][r] + cred[w][r + 32];
+        csum_part[p * Mc + m0 + r] = t;
+    }
+}
+
+// k_gemm_reduce over the product partials [P][count] and, in the same launch (blocks past the
+// product's), the column-sum partials [P][Mc]: one launch fewer per weight gradient
+__global__ void __launch_bounds__(256)
+k_gemm_reduce2(const float* __restrict__ part, int P, int64_t count, int Nc, float* __restrict__ C, int64_t ldc,
+               const float* __restrict__ cpart, int Mc, float* __restrict__ colsum, int64_t nb_main) {
+    const bool cs = blockIdx.x >= nb_main;
+    const int64_t i = (int64_t)(cs ? blockIdx.x - nb_main : blockIdx.x) * 256 + threadIdx.x;
+    const float* src = cs ? cpart : part;
+    const int64_t cnt = cs ? (int64_t)Mc : count;
+    if (i >= cnt) return;
+    float s = 0.f;
+    int q = 0;
+    for (; q + 16 <= P; q += 16) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = src[(int64_t)(q + j) * cnt + i];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    for (; q < P; ++q) s += src[(int64_t)q * cnt + i];
+    if (cs) colsum[i] = s;
+    else C[(i / Nc) * ldc + i % Nc] = s;
+}
+
 }  // namespace
+
+#ifndef SIR_SMALL_ROWS
+#define SIR_SMALL_ROWS 16384    // fewest node rows for the block-tiled GEMMs; below: k_gemm_nt_s / k_gemm_tn_s
+#endif
+// env SIR_GEMM_SMALL_ROWS overrides the threshold per call (A/B and the route tests)
+static int64_t gemm_small_rows() {
+    const char* e = getenv("SIR_GEMM_SMALL_ROWS");
+    return (e != nullptr && e[0] != 0) ? atoll(e) : (int64_t)SIR_SMALL_ROWS;
+}
+
+#ifndef SIR_TN_S_ROWS
+#define SIR_TN_S_ROWS 512       // k_gemm_tn_s: node rows per split (<= 16 splits)
+#endif
+static int gemm_tn_splits_s(int64_t R, int64_t, int64_t) {
+    int64_t P = (R + SIR_TN_S_ROWS - 1) / SIR_TN_S_ROWS;
+    if (P > 16) P = 16;
+    if (P < 1) P = 1;
+    return (int)P;
+}
+
+static hipError_t run_gemm_nt_s(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
+                                const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
+    const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
+    const u4v* wp = static_cast<const u4v*>(packed);
+    const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
+    const int nfg = (N + 32 * S_FT - 1) / (32 * S_FT);
+    const int64_t waves = (M + 31) / 32 * nfg;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    if (K % KC == 0)
+        hipLaunchKernelGGL(k_gemm_nt_s<true>, dim3(blocks), dim3(256), 0, st, A, lda, M, K, wp, np, kc, inv, bias, N, C,
+                           ldc, nfg, waves, drop);
+    else
+        hipLaunchKernelGGL(k_gemm_nt_s<false>, dim3(blocks), dim3(256), 0, st, A, lda, M, K, wp, np, kc, inv, bias, N, C,
+                           ldc, nfg, waves, drop);
+    return hipGetLastError();
+}
+
+hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int trans,
+                              int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
+    if (M == 0 || N == 0) return hipSuccess;
+    const int nft = (N + 31) / 32;
+    const int64_t blocks = (M + 31) / 32 * nft;
+    if (trans)
+        hipLaunchKernelGGL(k_gemm_nt_sw<true>, dim3((unsigned)blocks), dim3(256), 0, st, A, lda, M, K, W, ldw, N, bias, C,
+                           ldc, nft, drop);
+    else
+        hipLaunchKernelGGL(k_gemm_nt_sw<false>, dim3((unsigned)blocks), dim3(256), 0, st, A, lda, M, K, W, ldw, N, bias,
+                           C, ldc, nft, drop);
+    return hipGetLastError();
+}
 
 int64_t gemm_pack_npad(int64_t N) { return (N + 255) / 256 * 256; }
 // the packed weight holds the k_gemm_nt / k_gemm_nt_p image and, for the shapes the
@@ -1208,6 +1609,7 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     const u4v* wp = static_cast<const u4v*>(packed);
     const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
     const bool kfull = K % KC == 0;
+    if (M < gemm_small_rows()) return run_gemm_nt_s(A, lda, M, K, packed, N, bias, C, ldc, st, drop);
     if (gemm_nt_w_ok(N, K) && M >= SIR_NT_W_MINROWS)
         return run_gemm_nt_w(A, lda, M, K, static_cast<const char*>(packed) + gemm_pack_base_bytes(N, K), N, bias, C,
                              ldc, st, drop);
@@ -1274,17 +1676,28 @@ int gemm_tn_splits(int64_t R, int64_t Mc, int64_t Nc) {
 }
 
 int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc) {
-    return (int64_t)gemm_tn_splits(R, Mc, Nc) * (Mc * Nc + Mc) * 4;    // partial products + column sums
+    int64_t P = gemm_tn_splits(R, Mc, Nc);                 // the block-tiled kernels (fp32 and 16-bit)
+    if (R < gemm_small_rows()) {
+        const int64_t ps = gemm_tn_splits_s(R, Mc, Nc);    // k_gemm_tn_s
+        if (ps > P) P = ps;
+    }
+    return P * (Mc * Nc + Mc) * 4;                         // partial products + column sums
 }
 
 hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
                        float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st) {
     if (Mc == 0 || Nc == 0) return hipSuccess;
-    const int P = gemm_tn_splits(R, Mc, Nc);
+    const bool small = R < gemm_small_rows();
+    const int P = small ? gemm_tn_splits_s(R, Mc, Nc) : gemm_tn_splits(R, Mc, Nc);
     const int64_t rps = (R + P - 1) / P;
     const int nmt = (Mc + 255) / 256, nnt = (Nc + 255) / 256;
     float* part = static_cast<float*>(workspace);
     float* cpart = colsum != nullptr ? part + (int64_t)P * Mc * Nc : nullptr;
+    if (small) {
+        const int smt = (Mc + 31) / 32, snt = (Nc + 31) / 32;
+        hipLaunchKernelGGL(k_gemm_tn_s, dim3((unsigned)((int64_t)P * smt * snt)), dim3(256), 0, st, A, lda, B, ldb, R,
+                           Mc, Nc, part, cpart, smt, snt, rps);
+    } else
 #if SIR_TN_CFG == 2
     // 8 waves (2 per SIMD, 256 registers), 128x64 per wave, a thread loads a whole column chunk
     hipLaunchKernelGGL((k_gemm_tn<2, 4, 4, 2>), dim3((unsigned)(P * nmt * nnt)), dim3(512), 0, st,
@@ -1293,12 +1706,11 @@ hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb,
     hipLaunchKernelGGL((k_gemm_tn<4, 4, 2, 2>), dim3((unsigned)(P * nmt * nnt)), dim3(1024), 0, st,
                        A, lda, B, ldb, R, Mc, Nc, part, cpart, nmt, nnt, rps);
 #endif
+    // C = sum_p part[p] and colsum = sum_p cpart[p], in split order, one launch
     const int64_t count = (int64_t)Mc * Nc;
-    hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
-                       part, P, count, Nc, C, ldc);
-    if (colsum != nullptr)      // colsum = sum_p cpart[p] in split order
-        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)((Mc + 255) / 256)), dim3(256), 0, st,
-                           cpart, P, (int64_t)Mc, Mc, colsum, (int64_t)0);
+    const int64_t nbm = (count + 255) / 256, nbc = colsum != nullptr ? (Mc + 255) / 256 : 0;
+    hipLaunchKernelGGL(k_gemm_reduce2, dim3((unsigned)(nbm + nbc)), dim3(256), 0, st, part, P, count, Nc, C, ldc, cpart,
+                       Mc, colsum, nbm);
     return hipGetLastError();
 }
 

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("SIRGCN_LIB") or os.path.join(os.path.dirname(os.path.
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 9
+ABI_VERSION = 10
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -44,6 +44,7 @@ SIGNATURES = {
     "sir_gemm_pack_bytes": (ctypes.c_int64, [_I64, _I64]),
     "sir_gemm_pack": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _P, _P]),
     "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P, _P]),
+    "sir_gemm_nt_direct": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, ctypes.c_int, _I64, _P, _P, _I64, _P, _P]),
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
     "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
     "sir_gemm_tn16": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _I, _P, _I64, _P, _P, _I64, _P]),
@@ -414,6 +415,22 @@ def gemm_nt(A, packed, bias=None, out=None, drop=None):
     with _Timed(f"sir_gemm_nt K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + N))):
         rc = lib.sir_gemm_nt(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(bias), _ptr(out), out.stride(0),
                              _drop(drop), _stream(A.device))
+    _check(rc, lib)
+    return out
+
+
+def gemm_nt_direct(A, W, trans=False, bias=None, out=None, drop=None):
+    """C = A W^T (+ bias) (trans=False, W [N, K]) or A W (trans=True, W [K, N]) with the fp32 weight
+    read directly — no packing pass (``sir_gemm_nt_direct``: the small-batch route)."""
+    lib = load()
+    M, K = A.shape
+    N = W.shape[1] if trans else W.shape[0]
+    assert A.stride(1) == 1 and W.stride(1) == 1 and W.shape[0 if trans else 1] == K
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    with _Timed(f"sir_gemm_nt_direct K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + N))):
+        rc = lib.sir_gemm_nt_direct(_ptr(A), A.stride(0), M, K, _ptr(W), W.stride(0), int(trans), N, _ptr(bias),
+                                    _ptr(out), out.stride(0), _drop(drop), _stream(A.device))
     _check(rc, lib)
     return out
 

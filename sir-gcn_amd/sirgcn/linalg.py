@@ -9,6 +9,8 @@ fp32 in / fp32 out at fp32 accuracy (tests/test_gemm_gpu.py).  Operands the kern
 views, fewer than ``MIN_ROWS`` node rows) go to torch's own GEMM; ``USE_NATIVE = False`` forces that
 for A/B runs.
 """
+import os
+
 import torch
 
 from . import _native
@@ -16,11 +18,13 @@ from . import _native
 USE_NATIVE = True
 MAX_DIM = 65536          # N, K (and M, N of the TN GEMM) limit of the native kernels
 MAX_LD = 1 << 20         # SIR_GEMM_MAX_LD (include/sirconv.h)
-# Below this many node rows the native kernels (256-row tiles, split-K over rows) cannot fill the
-# 256 CUs and the call is launch-bound: small batches (config 5: ~1.6k nodes) use torch's fp32 GEMM
-# (hipBLASLt), which is also IEEE fp32.
-DEFAULT_MIN_ROWS = 32768
-MIN_ROWS = DEFAULT_MIN_ROWS
+# Fewest node rows for the native route.  0: every batch size runs native — below 16,384 rows the
+# library itself switches to its one-wave-per-tile kernels (k_gemm_nt_s / k_gemm_tn_s, bit-identical
+# to the block-tiled NT kernels) that fill the chip at config 5's 1.6k-node and config 1's 5k-node
+# batches (profiles/r03_ab_gemm_small.txt).  A positive value sends smaller batches to torch's fp32
+# GEMM (hipBLASLt) instead.
+DEFAULT_MIN_ROWS = 0
+MIN_ROWS = int(os.environ.get("SIRGCN_GEMM_MIN_ROWS", DEFAULT_MIN_ROWS))
 
 
 def _ok(t):
@@ -33,6 +37,16 @@ def _w_ok(W, n_out):
     return W.is_cuda and W.dtype == torch.float32 and n_out % 4 == 0 and n_out <= MAX_DIM
 
 
+# Below this many rows the weight is read as fp32 by the GEMM itself (sir_gemm_nt_direct, 4-wave
+# split-k tiles of 32 x 32) instead of being packed first: at config 5's 1.6k rows the packing pass
+# cost as much as the product (profiles/r03_ab_gemm_small.txt).
+DIRECT_ROWS = int(os.environ.get("SIRGCN_GEMM_DIRECT_ROWS", 8192))
+
+
+def _direct_ok(A, W):
+    return (A.shape[0] < DIRECT_ROWS and W.stride(1) == 1 and W.stride(0) <= MAX_LD and W.data_ptr() % 4 == 0)
+
+
 def mm_wt(A, W, bias=None, out=None, drop=None):
     """A W^T + bias (nn.Linear); W [N, K].  ``drop``: (seed, p) feature dropout of the result
     (the QK projection, conv.py:60-61), applied in the native GEMM's epilogue — or, on the torch
@@ -40,6 +54,8 @@ def mm_wt(A, W, bias=None, out=None, drop=None):
     if (USE_NATIVE and _ok(A) and _w_ok(W, W.shape[0])
             and (bias is None or (bias.is_contiguous() and bias.data_ptr() % 16 == 0))
             and (out is None or _ok(out))):
+        if _direct_ok(A, W):
+            return _native.gemm_nt_direct(A, W, False, bias, out, drop=drop)
         return _native.gemm_nt(A, _native.gemm_pack(W.contiguous()), bias, out, drop=drop)
     if out is None:
         out = torch.addmm(bias, A, W.t()) if bias is not None else torch.mm(A, W.t())
@@ -55,6 +71,8 @@ def mm_wt(A, W, bias=None, out=None, drop=None):
 def mm_w(A, W):
     """A W; W [K, N]."""
     if USE_NATIVE and _ok(A) and _w_ok(W, W.shape[1]):
+        if _direct_ok(A, W):
+            return _native.gemm_nt_direct(A, W, True)
         return _native.gemm_nt(A, _native.gemm_pack(W.contiguous(), trans=True))
     return torch.mm(A, W)
 

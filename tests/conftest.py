@@ -34,9 +34,9 @@ def load_case(name):
 
 @pytest.fixture(autouse=True)
 def _native_gemm_at_every_size():
-    """The product routes GEMMs with fewer than linalg.MIN_ROWS node rows to torch (launch-bound
-    sizes); the tests' small graphs would then never reach the native split-fp16 MFMA kernels, so
-    the suite lowers the threshold to 0 (every fp32 GEMM the kernels accept runs natively)."""
+    """Every fp32 GEMM the native kernels accept runs natively in the tests, as in the product
+    (linalg.DEFAULT_MIN_ROWS = 0: small batches take the library's one-wave-per-tile kernels); the
+    fixture pins that in case a caller raised the threshold."""
     from sirgcn import linalg
     old = linalg.MIN_ROWS
     linalg.MIN_ROWS = 0

@@ -288,6 +288,7 @@ def test_gemm_nt_weight_resident_opt_in_bit_identical(M, K, N, monkeypatch):
     pk = _native.gemm_pack(W)
     out = []
     monkeypatch.setenv("SIR_NT_G", "0")        # the reference kernel of this test is k_gemm_nt_p
+    monkeypatch.setenv("SIR_GEMM_SMALL_ROWS", "0")   # block-tiled routes at every M (not k_gemm_nt_s)
     for w in ("0", "1"):
         monkeypatch.setenv("SIR_NT_W", w)
         wide = torch.full((M, N + 12), 7.0, device=DEV)
@@ -313,6 +314,7 @@ def test_gemm_nt_dma_kernel_vs_persistent(M, K, N, monkeypatch):
     b = torch.randn(N, device=DEV, generator=g)
     pk = _native.gemm_pack(W)
     outs = {}
+    monkeypatch.setenv("SIR_GEMM_SMALL_ROWS", "0")   # block-tiled routes at every M (not k_gemm_nt_s)
     for sw in ("1", "0"):
         monkeypatch.setenv("SIR_NT_G", sw)
         wide = torch.full((M, N + 12), 7.0, device=DEV)
@@ -324,3 +326,129 @@ def test_gemm_nt_dma_kernel_vs_persistent(M, K, N, monkeypatch):
         assert torch.all(wide[:, :4] == 7.0) and torch.all(wide[:, 4 + N:] == 7.0)
     d = _rel(outs["1"][0].double(), outs["0"][0].double())
     assert d < 1e-6, f"dma vs persistent relL2 {d:.2e}"
+
+
+# ---------------------------------------------------------------------------- small-batch route
+# Below SIR_SMALL_ROWS (16384) node rows the NT / TN GEMMs run one wave per output tile
+# (k_gemm_nt_s / k_gemm_tn_s: config 5's 1.6k-node molecule batches, config 1's 5k-node batches).
+# SIR_GEMM_SMALL_ROWS in the environment moves the threshold per call: "0" forces the block-tiled
+# kernels, a huge value the one-wave ones.
+ROUTES = {"small": "1000000000", "block": "0"}
+
+
+@pytest.mark.parametrize("M,K,N", [(1582, 256, 512), (1582, 512, 256), (5120, 128, 256), (1, 256, 300),
+                                   (33, 128, 64), (70001, 256, 256), (4099, 64, 128), (3000, 1024, 96)])
+@pytest.mark.parametrize("trans,with_bias,drop", [(False, True, False), (True, False, False), (False, True, True)])
+def test_gemm_nt_small_route_bit_identical_to_block_route(M, K, N, trans, with_bias, drop, monkeypatch):
+    """k_gemm_nt_s splits, scales and multiplies each row exactly as the block-tiled kernels do (same
+    32-k chunks, same running scale, the three MFMAs in the same order per accumulator, the same
+    epilogue arithmetic incl. the dropout mask): the two routes agree bit for bit, on rows spanning
+    2^60 and rows whose maximum grows along K; both within the fp64 bound."""
+    g = torch.Generator(device=DEV).manual_seed(M + 5 * K + N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-30, 30, (M, 1), device=DEV, generator=g).float())
+    if M > 300:
+        A[100:300] *= torch.exp2(torch.linspace(-20, 20, K, device=DEV))
+        A[17] = 0
+    W = (torch.randn(K, N, device=DEV, generator=g) if trans else torch.randn(N, K, device=DEV, generator=g)) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g) if with_bias else None
+    pk = _native.gemm_pack(W, trans=trans)
+    dr = (1234, 0.25) if drop else None
+    outs = {}
+    for name, v in ROUTES.items():
+        monkeypatch.setenv("SIR_GEMM_SMALL_ROWS", v)
+        outs[name] = _native.gemm_nt(A, pk, b, drop=dr)
+    assert torch.equal(outs["small"], outs["block"]), \
+        f"small vs block route differ: relL2 {_rel(outs['small'].double(), outs['block'].double()):.2e}"
+    if not drop:
+        Wt = W if trans else W.t()
+        ref = torch.addmm(b, A, Wt) if with_bias else A @ Wt
+        _check(outs["small"], A.double(), Wt.double(), ref, b, f"nt small M={M} K={K} N={N}")
+
+
+@pytest.mark.parametrize("M,K,N", [(1582, 300, 600), (1582, 600, 300), (777, 36, 132), (5, 300, 300),
+                                   (2000, 100, 12)])
+def test_gemm_nt_small_route_ragged_k(M, K, N, monkeypatch):
+    """K not a multiple of 32 (config 5: H = 300): the last chunk's columns past K (the next row's
+    values, or past the buffer) must not enter the row scale or the products; vs fp64, and an
+    A slice of a wider tensor (lda > K) whose neighbouring columns hold huge values."""
+    monkeypatch.setenv("SIR_GEMM_SMALL_ROWS", ROUTES["small"])
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    A0 = torch.full((M, K + 8), 3e37, device=DEV)
+    A = A0[:, 4:4 + K]
+    A.copy_(torch.randn(M, K, device=DEV, generator=g))
+    W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g)
+    C = _native.gemm_nt(A, _native.gemm_pack(W), b)
+    _check(C, A.double(), W.double().t(), torch.addmm(b, A, W.t()), b, f"nt small ragged M={M} K={K} N={N}")
+
+
+@pytest.mark.parametrize("R,M,N", [(0, 8, 4), (1, 300, 300), (37, 64, 128), (1582, 600, 300), (1582, 300, 300),
+                                   (5120, 128, 64), (16000, 256, 256), (70, 36, 100)])
+@pytest.mark.parametrize("route", ["small", "block"])
+def test_gemm_tn_small_and_block_routes_vs_fp64(R, M, N, route, monkeypatch):
+    """k_gemm_tn_s (one wave per 32 x 64 tile, >= 1024 waves over row splits) and the block-tiled
+    k_gemm_tn on the same small-batch shapes: vs fp64 on columns spanning 2^60, a late row block that
+    raises the B scales, leading zero rows; column sums (the bias gradient) vs fp64; run-to-run
+    deterministic, and the product unchanged by asking for the column sums."""
+    monkeypatch.setenv("SIR_GEMM_SMALL_ROWS", ROUTES[route])
+    g = torch.Generator(device=DEV).manual_seed(R + 3 * M + N)
+    A = torch.randn(R, M, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-30, 30, (1, M), device=DEV, generator=g).float())
+    B = torch.randn(R, N, device=DEV, generator=g)
+    if R > 100:
+        B[R // 2:R // 2 + 40] *= 2.0 ** 30
+        B[:50, :7] = 0
+    C, cs = _native.gemm_tn(A, B, colsum=True)
+    if R == 0:
+        assert torch.all(C == 0) and torch.all(cs == 0)
+        return
+    assert torch.equal(C, _native.gemm_tn(A, B)), "deterministic / independent of colsum"
+    _check(C, A.double().t(), B.double(), A.t() @ B, None, f"tn {route} R={R} M={M} N={N}")
+    ref64 = A.double().sum(0)
+    e_ours, e_torch = _rel(cs.double(), ref64), _rel(A.sum(0).double(), ref64)
+    assert e_ours <= max(2 * e_torch, 1e-6), (e_ours, e_torch)
+
+
+@pytest.mark.parametrize("M,K,N", [(1582, 300, 600), (1582, 300, 300), (1582, 600, 300), (5120, 64, 128),
+                                   (1, 256, 256), (33, 36, 12), (8191, 512, 256), (2000, 1024, 96)])
+@pytest.mark.parametrize("trans,with_bias", [(False, True), (True, False), (False, False)])
+def test_gemm_nt_direct_vs_fp64(M, K, N, trans, with_bias):
+    """sir_gemm_nt_direct (the small-batch route of nn.Linear: the fp32 weight split in the kernel,
+    running scales on both operands, 4 waves splitting K per 32 x 32 tile) vs fp64, on rows and
+    weight rows spanning 2^60, rows whose maximum grows along K, a zero row; strided A (lda > K)."""
+    g = torch.Generator(device=DEV).manual_seed(M + 7 * K + N)
+    A0 = torch.randn(M, K + 8, device=DEV, generator=g)
+    A = A0[:, 4:4 + K]
+    A *= torch.exp2(torch.randint(-30, 30, (M, 1), device=DEV, generator=g).float())
+    if M > 300:
+        A[100:300] *= torch.exp2(torch.linspace(-20, 20, K, device=DEV))
+        A[17] = 0
+    W = (torch.randn(K, N, device=DEV, generator=g) if trans else torch.randn(N, K, device=DEV, generator=g)) / K ** 0.5
+    W *= torch.exp2(torch.randint(-15, 15, (1, N) if trans else (N, 1), device=DEV, generator=g).float())
+    b = torch.randn(N, device=DEV, generator=g) if with_bias else None
+    C = _native.gemm_nt_direct(A, W, trans, b)
+    Wt = W if trans else W.t()
+    ref = torch.addmm(b, A, Wt) if with_bias else A @ Wt
+    _check(C, A.double(), Wt.double(), ref, b, f"nt direct M={M} K={K} N={N} trans={trans}")
+    assert torch.equal(C, _native.gemm_nt_direct(A, W, trans, b)), "deterministic"
+
+
+def test_gemm_nt_direct_dropout_epilogue_and_errors():
+    """The QK dropout in the direct kernel's epilogue: the kept entries are exactly the undropped
+    result times 1/(1-p), the same hashed mask as the packed-weight kernels, ~p dropped."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    A = torch.randn(1582, 300, device=DEV, generator=g)
+    W = torch.randn(600, 300, device=DEV, generator=g) / 17.0
+    b = torch.randn(600, device=DEV, generator=g)
+    p = 0.2
+    C0 = _native.gemm_nt_direct(A, W, False, b)
+    Cd = _native.gemm_nt_direct(A, W, False, b, drop=(77, p))
+    Cp = _native.gemm_nt(A, _native.gemm_pack(W), b, drop=(77, p))
+    keep = Cd != 0
+    assert torch.equal(keep, Cp != 0), "same mask as the packed-weight kernel"
+    assert torch.equal(Cd[keep], C0[keep] * (1.0 / (1.0 - p)))
+    frac = 1.0 - keep.float().mean().item()
+    assert abs(frac - p) < 0.01, frac
+    with pytest.raises(RuntimeError, match="multiples of 4"):
+        _native.gemm_nt_direct(torch.zeros(10, 6, device=DEV), torch.zeros(8, 6, device=DEV))

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--libs", nargs="+", required=True)
     ap.add_argument("--only", default=None, help="run only the shapes whose name starts with this")
+    ap.add_argument("--reps", type=int, default=1, help="back-to-back calls per timed sample (small shapes)")
+    ap.add_argument("--torch", action="store_true", help="add torch's fp32 GEMM (hipBLASLt) as a column")
     a = ap.parse_args()
     V, H = a.V, a.H
     dev = "cuda"
@@ -54,6 +56,9 @@ def main():
         libs.append((name, open_lib(path)))
         envs[name] = tuple(env.split("=", 1)) if env else None
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if a.torch:
+        libs.append(("torch", None))
+        envs["torch"] = None
 
     def pack(lib, W, trans):
         N, K = (W.shape[1], W.shape[0]) if trans else W.shape
@@ -72,9 +77,11 @@ def main():
     if a.only:
         pre = a.only.split(",")
         shapes = {k: v for k, v in shapes.items() if any(k.startswith(x) for x in pre)}
-    packs = {(n, s): pack(lib, v[1], v[2]) for n, lib in libs for s, v in shapes.items() if len(v) == 4}
+    packs = {(n, s): pack(lib, v[1], v[2]) for n, lib in libs if lib is not None for s, v in shapes.items()
+             if len(v) == 4}
     outs = {}
-    ws = torch.empty(max(lib.sir_gemm_tn_workspace(V, 2 * H, H) for _, lib in libs), dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(lib.sir_gemm_tn_workspace(V, 2 * H, H) for _, lib in libs if lib is not None),
+                     dtype=torch.uint8, device=dev)
 
     def run(n, lib, s):
         if envs[n]:
@@ -83,6 +90,14 @@ def main():
             for e in {x[0] for x in envs.values() if x}:
                 os.environ.pop(e, None)
         v = shapes[s]
+        if lib is None:                      # torch (hipBLASLt)
+            if len(v) == 4:
+                A, W, trans, bias = v
+                Wt = W if trans else W.t()
+                outs[(n, s)] = torch.addmm(bias, A, Wt) if bias is not None else A @ Wt
+            else:
+                outs[(n, s)] = v[0].t() @ v[1]
+            return
         if len(v) == 4:
             A, _, _, bias = v
             pk, N, K = packs[(n, s)]
@@ -102,10 +117,11 @@ def main():
                 run(n, lib, s)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                run(n, lib, s)
+                for _ in range(a.reps):
+                    run(n, lib, s)
                 e1.record()
                 torch.cuda.synchronize()
-                times[(n, s)].append(e0.elapsed_time(e1))
+                times[(n, s)].append(e0.elapsed_time(e1) / a.reps)
     base = libs[0][0]
     for s in shapes:
         row = [f"{s:20s}"]
