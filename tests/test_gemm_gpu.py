@@ -452,3 +452,34 @@ def test_gemm_nt_direct_dropout_epilogue_and_errors():
     assert abs(frac - p) < 0.01, frac
     with pytest.raises(RuntimeError, match="multiples of 4"):
         _native.gemm_nt_direct(torch.zeros(10, 6, device=DEV), torch.zeros(8, 6, device=DEV))
+
+
+@pytest.mark.parametrize("M,K,N", [(70001, 256, 256), (66000, 256, 512), (40000, 512, 256), (33000, 128, 300),
+                                   (20000, 256, 132), (16385, 512, 512)])
+@pytest.mark.parametrize("drop", [False, True])
+def test_gemm_nt_pingpong_opt_in_bit_identical(M, K, N, drop, monkeypatch):
+    """The ping-pong persistent NT kernel (opt-in SIR_NT_PP=1: the tile's two 128-row halves as two
+    wave groups half a step apart) splits, scales and multiplies every row exactly as k_gemm_nt_p:
+    identical bits on rows spanning 2^60, rows whose maximum grows along K, ragged last tiles, a
+    strided C (its neighbours untouched) and the QK dropout epilogue."""
+    g = torch.Generator(device=DEV).manual_seed(M + K + N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-30, 30, (M, 1), device=DEV, generator=g).float())
+    A[100:300] *= torch.exp2(torch.linspace(-20, 20, K, device=DEV))
+    W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g)
+    pk = _native.gemm_pack(W)
+    dr = (99, 0.2) if drop else None
+    outs = {}
+    monkeypatch.setenv("SIR_NT_G", "0")
+    for sw in ("1", "0"):
+        monkeypatch.setenv("SIR_NT_PP", sw)
+        wide = torch.full((M, N + 12), 7.0, device=DEV)
+        outs[sw] = (_native.gemm_nt(A, pk, b, out=wide[:, 4:4 + N], drop=dr), wide)
+        torch.cuda.synchronize()
+    assert torch.equal(outs["1"][0], outs["0"][0]), \
+        f"ping-pong vs persistent: relL2 {_rel(outs['1'][0].double(), outs['0'][0].double()):.2e}"
+    wide = outs["1"][1]
+    assert torch.all(wide[:, :4] == 7.0) and torch.all(wide[:, 4 + N:] == 7.0)
+    if not drop:
+        _check(outs["1"][0], A.double(), W.double().t(), torch.addmm(b, A, W.t()), b, f"nt pp M={M} K={K} N={N}")
