@@ -105,9 +105,16 @@ CASES = [c for c in golden_manifest() if c["agg"] in ("sum", "mean", "sym") and 
          and c["act"] in ("relu", "leaky", "gelu") and c["H"] % 4 == 0 and c["E"] > 0]
 
 
+@pytest.mark.parametrize("native16", [False, True], ids=["route-default", "native16-every-size"])
 @pytest.mark.parametrize("dt,tol", [("bf16", 2e-2), ("f16", 1e-2)])
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
-def test_sirconv_autocast_vs_reference_fp32_golden(case, dt, tol):
+def test_sirconv_autocast_vs_reference_fp32_golden(case, dt, tol, native16, monkeypatch):
+    """native16: linalg.MIN_ROWS_16 = 0, so the golden cases' small graphs run the native 16-bit NT / TN
+    GEMMs (sir_gemm_nt16 for K in {128, 256, 512}, sir_gemm_tn16 for every shape) across aggs and
+    dtypes, not only the large dedicated test."""
+    if native16:
+        from sirgcn import linalg
+        monkeypatch.setattr(linalg, "MIN_ROWS_16", 0)
     z = load_case(case["name"])
     m = SIRConv(case["d"], case["H"], case["O"], ACTS[case["act"]], 0, agg_type=case["agg"]).to(DEV)
     t = lambda k: torch.from_numpy(np.ascontiguousarray(z[k])).to(DEV)
