@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 10
+#define SIR_ABI_VERSION 11
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
 enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
@@ -75,11 +75,16 @@ const char* sir_last_error(void);
  * column), the backward edge passes apply the same bits to dQ (columns 0..H-1) and dK (H..2H-1)
  * before storing them — the dropout's backward (grad * mask * scale).  16-bit outputs scale the value
  * rounded to the 16-bit type and round again (the reference's Dropout of a half-precision tensor).
- * A NULL pointer, or p <= 0, means no dropout; p >= 1 drops everything.
+ * A NULL pointer, or p <= 0, means no dropout; p >= 1 drops everything.  `seed_ptr` (may be NULL): a
+ * DEVICE pointer to the 64-bit seed, read by each kernel when it starts, overriding `seed` — the
+ * graph-safe form: a HIP graph that captured the launch together with the device op writing the
+ * seed (the host's RNG draw on the stream) replays with a fresh mask each time, and the backward
+ * passes given the same pointer read the same seed.
  */
 typedef struct {
     uint64_t seed;
     double p;
+    const uint64_t* seed_ptr;
 } sir_dropout_t;
 
 /* In place: X[m][n] = keep(m, col0 + n) ? X[m][n] * scale : 0 for an [M, N] block of QK (ldx

@@ -10,7 +10,9 @@ vectors in ``tests/golden/*.npz``, which were produced by executing the referenc
 """
 from .sirconv_oracle import (  # noqa: F401
     ACTS, AGGS, act_fwd, act_bwd, csr_by_dst, csr_by_src, degree_norms,
-    edge_agg_fwd, edge_agg_bwd, layer_fwd_bwd, max_first_wins, reference_cpu_step,
+    edge_agg_fwd, edge_agg_bwd, layer_fwd_bwd, max_first_wins, max_tie_flips, max_edge_values,
+    sigma_tie_flips,
+    reference_cpu_step,
 )
 from .graphnorm_oracle import graph_norm_fwd, graph_norm_bwd  # noqa: F401
 from .sireconv_oracle import sire_reference_step  # noqa: F401

@@ -30,6 +30,11 @@ class SIRConvRef(nn.Module):
         self.linear_key = nn.Linear(input_dim, hidden_dim, bias=False)
         self.linear_relation = nn.Linear(hidden_dim, output_dim, bias=outer_bias)
         self._agg_type = agg_type
+        # conditioning (tests): qk_inject — a list of [V, 2H] value tensors, one consumed per forward,
+        # whose VALUES replace Q, K while the gradients still flow through the projections
+        # (straight-through); qk_record — a list that receives this forward's [Q | K] values
+        self.qk_inject = None
+        self.qk_record = None
 
     def forward(self, graph, feat):
         src, dst = (torch.as_tensor(t, dtype=torch.int64).to(feat.device) for t in graph.edges())
@@ -45,6 +50,13 @@ class SIRConvRef(nn.Module):
             in_norm, out_norm = torch.ones_like(in_degs), torch.ones_like(out_degs)
         K = self.dropout(self.linear_key(feat))                       # conv.py:60
         Q = self.dropout(self.linear_query(feat))                     # conv.py:61
+        H = Q.shape[1]
+        if self.qk_inject:
+            v = self.qk_inject.pop(0).to(device=Q.device, dtype=Q.dtype)
+            Q = Q + (v[:, :H] - Q).detach()
+            K = K + (v[:, H:] - K).detach()
+        if self.qk_record is not None:
+            self.qk_record.append(torch.cat([Q, K], 1).detach())
         a = self.activation(Q.index_select(0, dst) + K.index_select(0, src))   # conv.py:45
         if self._agg_type == "max":                                   # conv.py:46-47, DGL fn.max
             return _MaxFirstWins.apply(self.linear_relation(a), dst, V)

@@ -182,14 +182,102 @@ class _MaxFirstWins(torch.autograd.Function):
         return dM, None, None
 
 
+class _MaxGivenArg(_MaxFirstWins):
+    """``fn.max`` evaluated on GIVEN arg edges (edge ids [V, F], -1 = empty row): Y[v, f] = M[arg, f],
+    the gradient routed to that edge.  Used to score a result whose arg edges differ from this
+    evaluation's own only on near-ties (the kernel's fp32 values rank two edges the other way):
+    the oracle then follows the kernel's routing and everything else is compared as usual."""
+
+    @staticmethod
+    def forward(ctx, M, dst, num_nodes, arg):
+        arg = torch.as_tensor(arg, dtype=torch.int64)
+        hit = arg >= 0
+        Y = torch.zeros((num_nodes, M.shape[1]), dtype=M.dtype)
+        rows, cols = torch.nonzero(hit, as_tuple=True)
+        Y[rows, cols] = M[arg[rows, cols], cols]
+        ctx.save_for_backward(arg, torch.as_tensor(dst, dtype=torch.int64))
+        ctx.E = M.shape[0]
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        dM, _, _ = _MaxFirstWins.backward(ctx, dY)
+        return dM, None, None, None
+
+
+def max_tie_flips(M64, mag, dst, num_nodes, arg, c=16.0):
+    """Check the arg edges ``arg`` ([V, F] edge ids) of an fp32 evaluation against the fp64 values
+    M64 [E, F]: wherever ``arg`` is not the fp64 first arg-max ``a*``, the two edges must be a near-tie,
+    |M64[a*] - M64[arg]| <= c * 2^-24 * max(mag[a*], mag[arg]) — within the fp32 rounding of values of
+    magnitude ``mag`` (the sum of absolute terms that fed each M element).  Returns (n_flips, worst
+    ratio gap / (2^-24 mag), n_violations)."""
+    _, a64 = max_first_wins(dst, num_nodes, M64)
+    arg = torch.as_tensor(arg, dtype=torch.int64)
+    flip = (arg != a64)
+    if not flip.any():
+        return 0, 0.0, 0
+    rows, cols = torch.nonzero(flip, as_tuple=True)
+    ea, eb = a64[rows, cols], arg[rows, cols]
+    assert bool((ea >= 0).all() and (eb >= 0).all()), "an empty row got an arg edge (or lost one)"
+    gap = (M64[ea, cols] - M64[eb, cols]).abs()
+    scale = torch.maximum(mag[ea, cols], mag[eb, cols]) * 2.0 ** -24
+    ratio = gap / scale.clamp_min(1e-300)
+    return int(flip.sum()), float(ratio.max()), int((ratio > c).sum())
+
+
+def max_edge_values(src, dst, X, W_Q, b_Q, W_K, W_R, b_R, act, slope=0.01):
+    """fp64 per-edge messages of the max form (conv.py:45-47: M = W_R sigma(Q[v] + K[u]) + b_R) and
+    their magnitudes (the same expression over absolute values: |W_R| (|Q| + |K|) + |b_R|, with
+    |Q| = |X| |W_Q|^T + |b_Q|), for :func:`max_tie_flips`."""
+    src = torch.as_tensor(src, dtype=torch.int64)
+    dst = torch.as_tensor(dst, dtype=torch.int64)
+    X, W_Q, b_Q, W_K, W_R, b_R = (t.double() for t in (X, W_Q, b_Q, W_K, W_R, b_R))
+    Q = X @ W_Q.t() + b_Q
+    K = X @ W_K.t()
+    fn = act if callable(act) else (lambda z: act_fwd(z, act, slope))
+    A = fn(Q[dst] + K[src])
+    M = A @ W_R.t() + b_R
+    Qm = X.abs() @ W_Q.abs().t() + b_Q.abs()
+    Km = X.abs() @ W_K.abs().t()
+    mag = (Qm[dst] + Km[src]) @ W_R.abs().t() + b_R.abs()
+    return M, mag
+
+
 # ----------------------------------------------------------------------------- layer
+def sigma_tie_flips(qk, src, dst, X, W_Q, b_Q, W_K, c=4.0):
+    """sigma' near-ties: the elements z = Q[v] + K[u] whose sign differs between the kernel's own
+    projection ``qk`` ([V, 2H] fp32, as the edge kernels saw it: fl(Q + K) has the sign of the exact
+    sum) and an fp64 projection.  sigma' of the ReLU family jumps at 0, so ONE such element moves a
+    gradient by a whole dA element (relL2 ~1e-3 at the test sizes): a result that flipped only where
+    |z64| <= c * 2^-24 * (|X| |W_Q|^T + |b_Q| + |X| |W_K|^T) — i.e. inside the fp32 rounding of the
+    projection — is scored against the fp64 oracle evaluated on ``qk`` (``reference_cpu_step(...,
+    qk=qk)``).  Returns (n_flips, worst |z64| / (2^-24 mag), n_violations)."""
+    src = torch.as_tensor(src, dtype=torch.int64)
+    dst = torch.as_tensor(dst, dtype=torch.int64)
+    X, W_Q, b_Q, W_K = (t.double() for t in (X, W_Q, b_Q, W_K))
+    H = W_Q.shape[0]
+    qk = torch.as_tensor(qk).double()
+    z32 = qk[dst, :H] + qk[src, H:]
+    z64 = (X @ W_Q.t() + b_Q)[dst] + (X @ W_K.t())[src]
+    flip = (z32 > 0) != (z64 > 0)
+    if not flip.any():
+        return 0, 0.0, 0
+    mag = (X.abs() @ W_Q.abs().t() + b_Q.abs())[dst] + (X.abs() @ W_K.abs().t())[src]
+    ratio = z64[flip].abs() / (mag[flip] * 2.0 ** -24).clamp_min(1e-300)
+    return int(flip.sum()), float(ratio.max()), int((ratio > c).sum())
+
+
 def reference_cpu_step(src, dst, num_nodes, X, W_Q, b_Q, W_K, W_R, b_R, dY, agg, act,
-                       slope=0.01, need_grads=True):
+                       slope=0.01, need_grads=True, max_arg=None, qk=None):
     """The reference's CPU dataflow for one SIRConv layer, fwd (+ autograd bwd).
 
     ``conv.py:49-67``: norms (51-57), K = X W_K^T, Q = X W_Q^T + b_Q (59-61),
     update_all(message_func, agg) (63) as DGL's edge-UDF path runs it (gathers, elementwise,
     index_add), Y = S W_R^T + b_R (65).  Returns Y and (if ``need_grads``) the gradients.
+    ``max_arg`` (agg 'max' only): evaluate fn.max on these arg edges ([V, O] edge ids) instead of
+    this evaluation's own first arg-max (:class:`_MaxGivenArg`).  ``qk`` ([V, 2H]): evaluate the
+    layer on these projection VALUES (the gradients still flow through X W_Q^T + b_Q, X W_K^T) —
+    the oracle conditioned on a kernel's own Q, K for :func:`sigma_tie_flips` near-ties.
     """
     src = torch.as_tensor(src, dtype=torch.int64)
     dst = torch.as_tensor(dst, dtype=torch.int64)
@@ -198,11 +286,18 @@ def reference_cpu_step(src, dst, num_nodes, X, W_Q, b_Q, W_K, W_R, b_R, dY, agg,
     with torch.set_grad_enabled(need_grads):
         K = torch.nn.functional.linear(X_, W_K_)
         Q = torch.nn.functional.linear(X_, W_Q_, b_Q_)
+        if qk is not None:                  # values of qk, gradients through the projections
+            qk = torch.as_tensor(qk).to(Q.dtype)
+            H = Q.shape[1]
+            Q = Q + (qk[:, :H] - Q).detach()
+            K = K + (qk[:, H:] - K).detach()
         if callable(act) or agg == "max":
             # the general UDF dataflow (conv.py:43-47): sigma is any callable, max -> per-edge W_R
             fn = act if callable(act) else (lambda z: act_fwd(z, act, slope))
             a = fn(Q.index_select(0, dst) + K.index_select(0, src))
-            if agg == "max":
+            if agg == "max" and max_arg is not None:
+                Y = _MaxGivenArg.apply(torch.nn.functional.linear(a, W_R_, b_R_), dst, num_nodes, max_arg)
+            elif agg == "max":
                 Y = _MaxFirstWins.apply(torch.nn.functional.linear(a, W_R_, b_R_), dst, num_nodes)
             else:
                 in_deg = torch.bincount(dst, minlength=num_nodes)

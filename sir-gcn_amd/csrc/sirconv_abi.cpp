@@ -50,7 +50,7 @@ int check_mask(const char* fn, int64_t H, int act) {
 // the kernels' Drop of an ABI dropout argument (NULL / p <= 0: none); col0 = first QK column written
 sir::Drop to_drop(const sir_dropout_t* d, int64_t col0) {
     if (d == nullptr || !(d->p > 0.0)) return sir::Drop();
-    return sir::make_drop(d->p, d->seed, (int)col0);
+    return sir::make_drop(d->p, d->seed, (int)col0, d->seed_ptr);
 }
 
 int finish(const char* fn, hipError_t err, const char* why) {

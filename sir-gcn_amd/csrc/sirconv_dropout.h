@@ -9,6 +9,11 @@
 // which is the backward of the dropout (grad * mask * scale).  Q and K draw independent bits, as
 // the reference's two Dropout calls do.  The hash is murmur3's 32-bit finaliser, once per row and
 // once per element.
+//
+// The seed is a kernel argument or, when `sptr` is set, a uint64 in device memory read when the
+// kernel starts (drop_resolve, first thing in every kernel that takes a Drop): a forward captured in
+// a HIP graph then draws a fresh mask on every replay, because the captured RNG op that writes the
+// seed (torch.randint on the device, graph-safe philox) runs again; the backward reads the same word.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,8 +26,20 @@ struct Drop {
     uint32_t thr_hi = 0;
     float scale = 1.f;
     int col0 = 0;              // column of the first output feature in QK (0: Q / whole QK, H: K)
+    const uint64_t* sptr = nullptr;   // device-resident seed (overrides s0 / s1 at kernel start)
     __host__ __device__ bool on() const { return (thr_lo | thr_hi) != 0; }
 };
+
+__host__ __device__ inline void drop_seed_words(Drop& d, uint64_t seed) {
+    d.s0 = (uint32_t)seed;
+    d.s1 = (uint32_t)(seed >> 32) ^ 0x6A09E667u;
+}
+
+// device: a Drop whose seed words come from `sptr` when set (one load per thread, at kernel start)
+__device__ __forceinline__ Drop drop_resolve(Drop d) {
+    if (d.on() && d.sptr != nullptr) drop_seed_words(d, *d.sptr);
+    return d;
+}
 
 __host__ __device__ inline uint32_t drop_fmix(uint32_t h) {
     h ^= h >> 16;
@@ -41,7 +58,7 @@ __host__ __device__ inline bool drop_keep(const Drop& d, uint32_t rh, int col) {
 }
 
 // host: the Drop of a probability p and a 64-bit seed (p <= 0: off)
-inline Drop make_drop(double p, uint64_t seed, int col0 = 0) {
+inline Drop make_drop(double p, uint64_t seed, int col0 = 0, const uint64_t* sptr = nullptr) {
     Drop d;
     if (!(p > 0.0)) return d;
     const double t = p >= 1.0 ? 4294967296.0 : p * 4294967296.0;
@@ -50,9 +67,9 @@ inline Drop make_drop(double p, uint64_t seed, int col0 = 0) {
     d.thr_lo = (uint32_t)thr;
     d.thr_hi = (uint32_t)(thr >> 32);
     d.scale = p >= 1.0 ? 0.f : (float)(1.0 / (1.0 - p));
-    d.s0 = (uint32_t)seed;
-    d.s1 = (uint32_t)(seed >> 32) ^ 0x6A09E667u;
+    drop_seed_words(d, seed);
     d.col0 = col0;
+    d.sptr = sptr;
     return d;
 }
 

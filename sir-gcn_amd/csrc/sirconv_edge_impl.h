@@ -394,6 +394,7 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
        float slope, int H,
        typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
        typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask, Drop drop) {
+    drop = drop_resolve(drop);
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LPR;
@@ -998,6 +999,7 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
             const float* __restrict__ norm_row, const float* __restrict__ norm_col,
             float slope, int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
             typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, Drop drop) {
+    drop = drop_resolve(drop);
     const int64_t wave = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     if (wave >= n_items) return;
     mask_pass_item<ST, MODE, ACT, AGG, NV, U>(wave, rowptr, col, perm, items, G, ldg, mask, norm_row, norm_col, slope, H,
@@ -1024,6 +1026,8 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
                  const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
                  const float* __restrict__ in_norm, const float* __restrict__ out_norm, float slope, int H,
                  Drop drop_q, Drop drop_k) {
+    drop_q = drop_resolve(drop_q);
+    drop_k = drop_resolve(drop_k);
     const int64_t w = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int64_t nmin = n_items < n_items_s ? n_items : n_items_s;
     bool dst;
@@ -1061,6 +1065,7 @@ template <int ST, bool MEAN_DIV, int VW>
 __global__ void __launch_bounds__(1024)
 k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
           int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, Drop drop) {
+    drop = drop_resolve(drop);
     __shared__ float red[1024 * VW];
     const int4 sp = splits[blockIdx.x];
     const int HC = H / VW;

@@ -84,6 +84,14 @@ __device__ inline int next_se(int se_old, int e_c) {
     const int s = 15 - SIR_HR - e_c;
     return s > 126 ? 126 : s;
 }
+// compensated (Kahan) accumulation: s += x with the rounding error carried in c (no fp contraction
+// in this file, so the compensation is not optimised away)
+__device__ inline void kahan_add(float& s, float& c, float x) {
+    const float y = x - c;
+    const float t = s + y;
+    c = (t - s) - y;
+    s = t;
+}
 __device__ inline float pow2(int e) { e = e < -126 ? -126 : (e > 127 ? 127 : e); return __uint_as_float((uint32_t)(e + 127) << 23); }
 // feature dropout of QK (sirconv_dropout.h) on 4 consecutive output columns n .. n+3 of one row
 __device__ inline void drop4(const Drop& d, int64_t row, int n, float4& o) {
@@ -175,6 +183,7 @@ __global__ void __launch_bounds__(64 * WD * WF)
 k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
           const u4v* __restrict__ Wp, int Npad, const float* __restrict__ inv_t,
           const float* __restrict__ bias, int N, float* __restrict__ C, int64_t ldc, int n_ftiles, Drop drop) {
+    drop = drop_resolve(drop);
     constexpr int NT = 64 * WD * WF;
     constexpr int BD = 32 * TDT * WD;        // data rows per block
     constexpr int BF = 32 * TFT * WF;        // features per block
@@ -531,15 +540,13 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #define SIR_NT_P_EPI 1          // persistent NT epilogue through LDS with whole-row stores (1) or fragment stores (0)
 #endif
 constexpr int NT_P_NMAX = 512;
-#ifndef SIR_NT_W_MINROWS
-#define SIR_NT_W_MINROWS 0      // fewest rows for the weight-resident kernel (sirconv_gemm_w.hip)
-#endif
 
 template <int NCT>
 __global__ void __launch_bounds__(512)
 k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
             int64_t ldc, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop) {
+    drop = drop_resolve(drop);
     constexpr int WF = 4, TDT = 4, TFT = 2;
     constexpr int NT = 512, BD = 256, BF = 256, TPR = NT / BD, FPT = KC / TPR, WPT = BF * 8 / NT;
     static_assert(TPR == 2 && WPT == 4 && NCT >= 4 && NCT % 2 == 0, "mapping");
@@ -907,288 +914,6 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
 }
 
 // ------------------------------------------------------------------------------------------
-// Ping-pong persistent NT GEMM (opt-in SIR_NT_PP=1; shapes of k_gemm_nt_p).  In k_gemm_nt_p all 8
-// waves run the same phase between two barriers, so a step's LDS traffic, split VALU, memory issue and
-// MFMAs serialise (its skeleton alone outlasts its MFMAs: profiles/r03_ab_gemm_nt_decomposition.txt).
-// Here the block's two row halves are two wave groups (waves 0-3: rows 0-127 of the 256-row tile,
-// waves 4-7: rows 128-255; wave w and w + 4 share a SIMD) running half a step apart: in every
-// barrier interval one group multiplies while the other splits / stages, so on each SIMD one wave's
-// MFMAs run beside its partner's VALU, LDS writes and memory instructions
-// (MI355X_MICROARCH.md "Two waves per SIMD").
-//   interval 2c  : group 0 multiplies chunk c;  group 1 splits A1[c], stages half 1 of W[c+1]
-//   interval 2c+1: group 1 multiplies chunk c;  group 0 splits A0[c+1], stages half 0 of W[c+1]
-// A images are single-buffered per group (written one interval before their only reader), W images
-// double-buffered by chunk parity.  Chunks run on across the block's tiles; a group's epilogue
-// (fragment stores from the accumulators) is the first thing of the memory phase after its last
-// multiply of a tile.  Per-row split, running scale, MFMA order and epilogue arithmetic are those of
-// k_gemm_nt_p: bit-identical results.
-#ifndef SIR_NT_PP_SETS
-#define SIR_NT_PP_SETS 1        // A chunks in flight in registers per group (1: loaded one chunk ahead)
-#endif
-template <int NCT>
-__global__ void __launch_bounds__(512)
-k_gemm_nt_pp(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
-             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
-             int64_t ldc, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop) {
-    constexpr int TDT = 4, TFT = 2, SETS = SIR_NT_PP_SETS;
-    static_assert(NCT % SETS == 0 && NCT >= 2 * SETS, "register sets cycle within a tile");
-    constexpr int BDG = 128, BF = 256;                 // rows per group, features per tile
-    constexpr int A_BYTES = BDG * 128;                 // 4 planes (hi/lo x ks) of 128 rows x 16 halves
-    constexpr int W_BYTES = BF * 128;                  // 4 planes of 256 features
-    constexpr int FAC_OFF = 2 * A_BYTES + 2 * W_BYTES; // fac[2 groups][128]
-    constexpr int FIN_OFF = FAC_OFF + 2 * BDG * 4;     // fin[2 groups][2 tile parity][128]
-    constexpr int EPI_OFF = FIN_OFF + 4 * BDG * 4;     // inv_t[NT_P_NMAX], bias[NT_P_NMAX]
-    __shared__ __attribute__((aligned(16))) char lds[EPI_OFF + 2 * NT_P_NMAX * 4];
-
-    const int t = threadIdx.x;
-    const int g = __builtin_amdgcn_readfirstlane(t >> 8);     // wave group
-    const int tg = t & 255;
-    const int tb = blockIdx.x * tiles_per_block;
-    const int te = (tb + tiles_per_block < n_tiles) ? tb + tiles_per_block : n_tiles;
-    if (tb >= te) return;
-    float* const inv_l = reinterpret_cast<float*>(lds + EPI_OFF);
-    float* const bias_l = inv_l + NT_P_NMAX;
-    for (int n = t; n < Npad; n += 512) {
-        inv_l[n] = inv_t[n];
-        bias_l[n] = (bias != nullptr && n < N) ? bias[n] : -0.f;
-    }
-    char* const abuf = lds + g * A_BYTES;
-    float* const fac = reinterpret_cast<float*>(lds + FAC_OFF) + g * BDG;
-    float* const fin = reinterpret_cast<float*>(lds + FIN_OFF) + g * 2 * BDG;
-
-    // splitter role: row rho (of the group's 128), k half kp (16 values)
-    const int rho = tg >> 1, kp = tg & 1;
-    const int aoff = (rho * (int)lda + kp * 16) * 4;
-    const rsrc_t wrsrc = mk_rsrc(Wp, (uint32_t)((int64_t)NCT * Npad * 128));
-    struct TileP { rsrc_t a; int64_t r0; int f0; int rows; };
-    // resources from wave-uniform values, said so explicitly (else hipcc builds some in VGPRs and
-    // wraps their loads in readfirstlane loops)
-    auto mk_rsrc_u = [](const void* ptr, uint32_t bytes) {
-        const uint64_t v = reinterpret_cast<uint64_t>(ptr);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-        return mk_rsrc(reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo), __builtin_amdgcn_readfirstlane(bytes));
-    };
-    // the group's part of tile tb + jj; past the block's range (or jj < 0): zero rows (loads read 0,
-    // stores are dropped), features of the block's first tile (valid weight addresses)
-    auto tile_p = [&](int jj) {
-        TileP p;
-        jj = __builtin_amdgcn_readfirstlane(jj);
-        const bool live = jj >= 0 && tb + jj < te;
-        const int tt = tb + (live ? jj : 0);
-        p.r0 = (int64_t)(tt / n_ftiles) * 256 + g * BDG;
-        p.f0 = (tt % n_ftiles) * BF;
-        const int64_t left = M - p.r0;
-        p.rows = !live ? 0 : (left < BDG ? (int)(left > 0 ? left : 0) : BDG);
-        p.a = mk_rsrc_u(A + (p.rows > 0 ? p.r0 : 0) * lda, (uint32_t)(p.rows * lda * 4));
-        return p;
-    };
-    float4 dv[SIR_NT_PP_SETS][4];
-    u4v wv[4];
-    auto load_a = [&](int set, const TileP& p, int kc) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u4v u = __builtin_amdgcn_raw_buffer_load_b128(p.a, aoff + 16 * i, kc * KC * 4, 0);
-            dv[set][i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
-        }
-    };
-    auto load_w = [&](const TileP& p, int kc) {    // planes (pt = g, ks = 0 / 1), pieces tg, tg + 256
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int plane = 2 * g + (i >> 1);
-            const int soff = __builtin_amdgcn_readfirstlane((kc * 4 + plane) * Npad * 32 + p.f0 * 32);
-            wv[i] = __builtin_amdgcn_raw_buffer_load_b128(wrsrc, (tg + 256 * (i & 1)) * 16, soff, 0);
-        }
-    };
-    auto put_w = [&](int buf) {
-        char* wb = lds + 2 * A_BYTES + buf * W_BYTES;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int plane = 2 * g + (i >> 1);
-            *reinterpret_cast<u4v*>(wb + plane * BF * 32 + (tg + 256 * (i & 1)) * 16) = wv[i];
-        }
-    };
-    int se_run = SE_INIT;
-    // split chunk kc of a tile (register set) into the group's A image (j1: tile parity, for fin)
-    auto split = [&](int set, int kc, int j1) {
-        const bool first = kc == 0, last = kc == NCT - 1;
-        float m = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) m = fmax4(m, dv[set][i]);
-        m = fmaxf(m, __shfl_xor(m, 1));
-        const int se_old = first ? SE_INIT : se_run, se = next_se(se_old, bexp(m));
-        se_run = se;
-        const float s = pow2(se);
-#pragma unroll
-        for (int j = 0; j < 16; j += 8) {
-            const int kl = kp * 16 + j, ks = kl >> 4, pos = kl & 15;
-            h8 hv, lv;
-            split8(dv[set][j / 4], dv[set][j / 4 + 1], s, hv, lv);
-            *reinterpret_cast<h8*>(abuf + (0 * 2 + ks) * BDG * 32 + fimg(rho, pos >> 3)) = hv;
-            *reinterpret_cast<h8*>(abuf + (1 * 2 + ks) * BDG * 32 + fimg(rho, pos >> 3)) = lv;
-        }
-        fac[rho] = first ? 1.f : pow2(se - se_old);             // the two k halves store the same value
-        if (last) fin[j1 * BDG + rho] = pow2(-se);
-    };
-
-    // compute role: wave wq of the group, 128 rows (TDT = 4 tiles) x 64 features (TFT = 2)
-    const int l = t & 63, r = l & 31, h = l >> 5, wq = (t >> 6) & 3;
-    const int f_w = wq * TFT * 32;
-    f16v acc[TFT][TDT];
-    auto math = [&](int kc) {
-        const bool zinit = kc == 0;
-        const char* wb = lds + 2 * A_BYTES + (kc & 1) * W_BYTES;
-        if (!zinit) {
-            float f[TDT];
-            bool ch = false;
-#pragma unroll
-            for (int b = 0; b < TDT; ++b) { f[b] = fac[32 * b + r]; ch |= f[b] != 1.f; }
-            if (__builtin_amdgcn_ballot_w64(ch) != 0) {
-#pragma unroll
-                for (int b = 0; b < TDT; ++b)
-#pragma unroll
-                    for (int a = 0; a < TFT; ++a) acc[a][b] *= f[b];
-            }
-        }
-        // per ks: the W fragments, then the data tiles one at a time with the next tile's fragments
-        // in flight (24 fragment VGPRs instead of 48); per accumulator the MFMA order of k_gemm_nt_p
-        const f16v zero = {};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            h8 wf[TFT][2], df[2][2];
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) {
-#pragma unroll
-                for (int a = 0; a < TFT; ++a)
-                    wf[a][pt] = *reinterpret_cast<const h8*>(wb + (pt * 2 + ks) * BF * 32 + fimg(f_w + 32 * a + r, h));
-                df[0][pt] = *reinterpret_cast<const h8*>(abuf + (pt * 2 + ks) * BDG * 32 + fimg(r, h));
-            }
-#pragma unroll
-            for (int b = 0; b < TDT; ++b) {
-                if (b + 1 < TDT) {
-#pragma unroll
-                    for (int pt = 0; pt < 2; ++pt)
-                        df[(b + 1) & 1][pt] = *reinterpret_cast<const h8*>(abuf + (pt * 2 + ks) * BDG * 32 + fimg(32 * (b + 1) + r, h));
-                }
-                const h8 d0 = df[b & 1][0], d1 = df[b & 1][1];
-#pragma unroll
-                for (int a = 0; a < TFT; ++a)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][0], d0, (zinit && ks == 0) ? zero : acc[a][b], 0, 0, 0);
-#pragma unroll
-                for (int a = 0; a < TFT; ++a)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][0], d1, acc[a][b], 0, 0, 0);
-#pragma unroll
-                for (int a = 0; a < TFT; ++a)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[a][1], d0, acc[a][b], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    };
-    // C = acc * 2^-se(row) * inv_t[n] + bias[n] for the group's rows of tile p (j1: its parity)
-    auto epilogue = [&](const TileP& p, int j1) {
-        int tq = threadIdx.x;
-        asm volatile("" : "+v"(tq));
-        const int lq = tq & 63, rq = lq & 31, hq = lq >> 5, fq = ((tq >> 6) & 3) * TFT * 32;
-        const uint32_t ldc4 = (uint32_t)ldc * 4u;
-        const uint32_t nrec = (uint32_t)p.rows * ldc4;
-        const rsrc_t crs = mk_rsrc_u(C + (p.rows > 0 ? p.r0 : 0) * ldc, nrec);
-        const float* sc = fin + j1 * BDG;
-        const uint32_t rv = (uint32_t)rq * ldc4 + (uint32_t)(fq + 4 * hq) * 4u;
-#pragma unroll
-        for (int b = 0; b < TDT; ++b) {
-            const float is = sc[32 * b + rq];
-            const uint32_t rb = rv + (uint32_t)(32 * b) * ldc4;
-#pragma unroll
-            for (int a = 0; a < TFT; ++a) {
-#pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    const int nc0 = p.f0 + 32 * a + 8 * gq;
-                    const int n = nc0 + fq + 4 * hq;
-                    const float4 it = *reinterpret_cast<const float4*>(inv_l + n);
-                    const float4 bb = *reinterpret_cast<const float4*>(bias_l + n);
-                    float4 o;
-                    o.x = acc[a][b][4 * gq + 0] * is * it.x + bb.x;
-                    o.y = acc[a][b][4 * gq + 1] * is * it.y + bb.y;
-                    o.z = acc[a][b][4 * gq + 2] * is * it.z + bb.z;
-                    o.w = acc[a][b][4 * gq + 3] * is * it.w + bb.w;
-                    if (drop.on()) drop4(drop, p.r0 + 32 * b + rq, n, o);
-                    u4v ov;
-                    ov.x = __float_as_uint(o.x); ov.y = __float_as_uint(o.y);
-                    ov.z = __float_as_uint(o.z); ov.w = __float_as_uint(o.w);
-                    __builtin_amdgcn_raw_buffer_store_b128(ov, crs, (n < N) ? rb : nrec,
-                                                           __builtin_amdgcn_readfirstlane(nc0 * 4), 0);
-                    __builtin_amdgcn_sched_barrier(0);          // see k_gemm_nt_p's fragment epilogue
-                    asm volatile("s_nop 1" ::: "memory");
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        }
-    };
-
-    // Prologue: both groups load their A(0), A(1) and stage their half of W[0]; group 0 splits A0[0].
-    TileP cur = tile_p(0), nxt = tile_p(1);
-#pragma unroll
-    for (int i = 0; i < SETS; ++i) load_a(i, cur, i);
-    load_w(cur, 0);
-    put_w(0);
-    load_w(cur, 1);
-    if (g == 0) {
-        split(0, 0, 0);
-        load_a(0, cur, SETS);
-    }
-    __syncthreads();
-    // Every tile runs the same fully unrolled interval sequence (NCT chunks, 2 intervals each), so
-    // register sets, W buffers and chunk positions are static and no load sits in a branch.
-    // Chunk kc's register set and W buffer are kc & 1 (NCT even: the parity runs on across tiles).
-    if (g == 0) {
-        for (int j = 0; tb + j < te; ++j) {
-#pragma unroll
-            for (int kc = 0; kc < NCT; ++kc) {
-                math(kc);                                             // interval 2kc
-                __syncthreads();
-                if (kc + 1 < NCT) {                                   // interval 2kc+1: chunk kc+1
-                    split((kc + 1) % SETS, kc + 1, j & 1);
-                    if (kc + 1 + SETS < NCT) load_a((kc + 1) % SETS, cur, kc + 1 + SETS);
-                    else load_a((kc + 1) % SETS, nxt, kc + 1 + SETS - NCT);
-                    put_w((kc + 1) & 1);
-                    if (kc + 2 < NCT) load_w(cur, kc + 2);
-                    else load_w(nxt, kc + 2 - NCT);
-                } else {                                              // the tile's last: next tile's chunk 0
-                    epilogue(cur, j & 1);
-                    split(0, 0, (j + 1) & 1);
-                    load_a(0, nxt, SETS);
-                    put_w(0);
-                    load_w(nxt, 1);
-                }
-                __syncthreads();
-            }
-            cur = nxt;
-            nxt = tile_p(j + 2);
-        }
-    } else {
-        TileP prv = tile_p(-1);
-        for (int j = 0; tb + j < te; ++j) {
-#pragma unroll
-            for (int kc = 0; kc < NCT; ++kc) {
-                if (kc == 0) epilogue(prv, (j + 1) & 1);              // the previous tile (none: dropped)
-                split(kc % SETS, kc, j & 1);                          // interval 2kc: chunk kc
-                if (kc + SETS < NCT) load_a(kc % SETS, cur, kc + SETS);
-                else load_a(kc % SETS, nxt, kc + SETS - NCT);
-                put_w((kc + 1) & 1);                                  // half 1 of W[kc+1]
-                if (kc + 2 < NCT) load_w(cur, kc + 2);
-                else load_w(nxt, kc + 2 - NCT);
-                __syncthreads();
-                math(kc);                                             // interval 2kc+1
-                __syncthreads();
-            }
-            prv = cur;
-            cur = nxt;
-            nxt = tile_p(j + 2);
-        }
-        epilogue(prv, ((te - tb) + 1) & 1);
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // TN GEMM (split over row ranges).  WM x WN waves, each TMT x TNT tiles of 32 x 32.
 // Loader: one slot per thread — threads [0, 2BM) own column t/2 of the A block, threads
 // [2BM, 2BM+2BN) column (t-2BM)/2 of the B block; t&1 selects the k-step (16 rows of the chunk).
@@ -1242,7 +967,7 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     // bias gradient of the same linear (column sums of A) rides on the A loads: one partial row
     // per split, written by the blocks of the first n-tile
     const bool do_cs = csum_part != nullptr && is_a;
-    float cs = 0.f;
+    float cs = 0.f, csc = 0.f;
     auto load = [&](int set, int c) {
         float4 (&xv)[XR / 4] = xv_[set];
         const int64_t vc = v_begin + (int64_t)c * KC;
@@ -1305,9 +1030,11 @@ k_gemm_tn(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
             *reinterpret_cast<h8*>(hd + lo_delta + 512) = lv[1];
         }
         if (kse == 0) *reinterpret_cast<float*>(st + fac_byte) = first ? 1.f : pow2(se - se_old);
-        if (do_cs) {           // column sums of A from the fp32 values, in row order
+        if (do_cs) {           // column sums of A from the fp32 values: per-chunk sum, Kahan-added to the total
+            float t = 0.f;
 #pragma unroll
-            for (int j = 0; j < XR / 4; ++j) { cs += xv[j].x; cs += xv[j].y; cs += xv[j].z; cs += xv[j].w; }
+            for (int j = 0; j < XR / 4; ++j) { t += xv[j].x; t += xv[j].y; t += xv[j].z; t += xv[j].w; }
+            kahan_add(cs, csc, t);
         }
         if (!first && se != se_old) rescaled[buf] = chunk;
     };
@@ -1476,6 +1203,7 @@ __global__ void __launch_bounds__(256)
 k_gemm_nt_s(const float* __restrict__ A, int64_t lda, int64_t M, int K, const u4v* __restrict__ Wp, int Npad, int Kc,
             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C, int64_t ldc,
             int nfg, int64_t n_waves, Drop drop) {
+    drop = drop_resolve(drop);
     const int l = threadIdx.x & 63, r = l & 31, h = l >> 5;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= n_waves) return;                       // whole waves (4 per block)
@@ -1649,6 +1377,7 @@ struct SOp {
 template <bool C0, bool C1, bool CS>
 __device__ __forceinline__ void small_contract(const SOp<C0>& o0, const SOp<C1>& o1, int nc, int q, int h,
                                                float (&p)[16], float& cs) {
+    float csc = 0.f;            // Kahan compensation of the column sum
     f16v acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
@@ -1686,8 +1415,10 @@ __device__ __forceinline__ void small_contract(const SOp<C0>& o0, const SOp<C1>&
             }
             first = false;
             if constexpr (CS) {
+                float t = 0.f;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) cs += x0[g][i];
+                for (int i = 0; i < 16; ++i) t += x0[g][i];
+                kahan_add(cs, csc, t);
             }
             h8 ah[2], al[2], bh[2], bl[2];
             const float sa = pow2(se0), sb = pow2(se1);
@@ -1713,6 +1444,7 @@ template <bool TRANS>
 __global__ void __launch_bounds__(256)
 k_gemm_nt_sw(const float* __restrict__ A, int64_t lda, int64_t M, int K, const float* __restrict__ W, int64_t ldw,
              int N, const float* __restrict__ bias, float* __restrict__ C, int64_t ldc, int nft, Drop drop) {
+    drop = drop_resolve(drop);
     __shared__ float red[4][16][64];
     const int l = threadIdx.x & 63, r = l & 31, h = l >> 5, q = threadIdx.x >> 6;
     const int64_t d0 = (int64_t)(blockIdx.x / nft) * 32;
@@ -1861,14 +1593,10 @@ hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, con
 }
 
 int64_t gemm_pack_npad(int64_t N) { return (N + 255) / 256 * 256; }
-// the packed weight holds the k_gemm_nt / k_gemm_nt_p image and, for the shapes the
-// weight-resident kernel takes (sirconv_gemm_w.hip), its slice images after it (16-B aligned)
-static int64_t gemm_pack_base_bytes(int64_t N, int64_t K) {
+// the packed weight: the k_gemm_nt / k_gemm_nt_p fragment image, then the per-feature inverse scales
+int64_t gemm_pack_bytes(int64_t N, int64_t K) {
     const int64_t np = gemm_pack_npad(N), kc = (K + KC - 1) / KC;
     return (kc * 4 * np * 32 + np * 4 + 15) / 16 * 16;
-}
-int64_t gemm_pack_bytes(int64_t N, int64_t K) {
-    return gemm_pack_base_bytes(N, K) + gemm_pack_w_bytes((int)N, (int)K);
 }
 
 hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st) {
@@ -1876,11 +1604,6 @@ hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, v
     _Float16* out = static_cast<_Float16*>(packed);
     float* inv = reinterpret_cast<float*>(static_cast<char*>(packed) + (int64_t)kc * 4 * np * 32);
     hipLaunchKernelGGL(k_pack_weight, dim3(np), dim3(64), 0, st, W, ldw, N, K, trans, np, kc, out, inv);
-    if (gemm_pack_w_bytes(N, K) > 0) {     // the W image whenever the shape has one (route chosen per launch)
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        return run_gemm_pack_w(W, ldw, N, K, trans, static_cast<char*>(packed) + gemm_pack_base_bytes(N, K), st);
-    }
     return hipGetLastError();
 }
 
@@ -1892,11 +1615,6 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
     const bool kfull = K % KC == 0;
     if (M < gemm_small_rows()) return run_gemm_nt_s(A, lda, M, K, packed, N, bias, C, ldc, st, drop);
-    if (gemm_nt_w_ok(N, K) && M >= SIR_NT_W_MINROWS)
-        return run_gemm_nt_w(A, lda, M, K, static_cast<const char*>(packed) + gemm_pack_base_bytes(N, K), N, bias, C,
-                             ldc, st, drop);
-    if (gemm_nt_g_ok(A, lda, K, N, C, ldc))
-        return run_gemm_nt_g(A, lda, M, K, packed, N, bias, C, ldc, st, drop);
     if (SIR_NT_PERSIST && N > 128 && np <= NT_P_NMAX && kfull && (kc == 4 || kc == 8 || kc == 16)) {
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;
@@ -1908,10 +1626,7 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
         if (ntiles < (int64_t)1 << 30) {
             const int tpb = (int)((ntiles + ncu - 1) / ncu);
             const int nblk = (int)((ntiles + tpb - 1) / tpb);
-            const char* pe = getenv("SIR_NT_PP");      // opt-in ping-pong schedule (read per call: A/B)
-            const bool pp = pe != nullptr && pe[0] == '1';
-            auto kern = pp ? (kc == 4 ? k_gemm_nt_pp<4> : (kc == 8 ? k_gemm_nt_pp<8> : k_gemm_nt_pp<16>))
-                           : (kc == 4 ? k_gemm_nt_p<4> : (kc == 8 ? k_gemm_nt_p<8> : k_gemm_nt_p<16>));
+            auto kern = kc == 4 ? k_gemm_nt_p<4> : (kc == 8 ? k_gemm_nt_p<8> : k_gemm_nt_p<16>);
             hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, ldc,
                                nft, (int)ntiles, tpb, drop);
             return hipGetLastError();

@@ -264,6 +264,7 @@ __global__ void __launch_bounds__(512)
 k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
             const float* __restrict__ bias, int N, void* __restrict__ C, int64_t ldc, unsigned short* __restrict__ Acopy,
             int64_t ldac, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop) {
+    drop = drop_resolve(drop);
     constexpr int BD = 256, BFT = 256, WF = 4, TDT = 4, TFT = 2;
     constexpr int KS = KC / 16;                       // k16 planes per chunk
     constexpr int PLANE = 256 * 32;                   // one k16 plane of 256 rows
@@ -573,6 +574,7 @@ namespace {
 template <int DT>
 __global__ void __launch_bounds__(256)
 k_dropout_apply(void* __restrict__ X, int64_t ldx, int64_t M, int N, Drop drop) {
+    drop = drop_resolve(drop);
     const int64_t m = blockIdx.y;
     const uint32_t rh = drop_row_hash(drop, m);
     for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {

@@ -152,16 +152,7 @@ int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc);
 hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
                        float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st);
 int gemm_tn_splits(int64_t R, int64_t Mc, int64_t Nc);
-// weight-resident NT GEMM (sirconv_gemm_w.hip); its slice images follow the base packed image
-bool gemm_nt_w_ok(int N, int K);
 int64_t gemm_pack_npad(int64_t N);
-bool gemm_nt_g_ok(const float* A, int64_t lda, int K, int N, const float* C, int64_t ldc);
-hipError_t run_gemm_nt_g(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
-                         const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop);
-int64_t gemm_pack_w_bytes(int N, int K);
-hipError_t run_gemm_pack_w(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st);
-hipError_t run_gemm_nt_w(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
-                         const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop = Drop());
 // C = sum_p part[p] (count elements of rows of Nc, C row stride ldc), p in order
 hipError_t run_gemm_reduce(const float* part, int P, int64_t count, int Nc, float* C, int64_t ldc, hipStream_t st);
 // 16-bit TN GEMM (sirconv_gemm16.hip): A, B bf16 (dtype SIR_DTYPE_BF16) or fp16, fp32 result

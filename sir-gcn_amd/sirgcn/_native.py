@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("SIRGCN_LIB") or os.path.join(os.path.dirname(os.path.
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 10
+ABI_VERSION = 11
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -76,16 +76,22 @@ SIGNATURES = {
 }
 
 class Dropout(ctypes.Structure):
-    """``sir_dropout_t`` (include/sirconv.h): the hashed feature-dropout mask of QK (seed, p)."""
-    _fields_ = [("seed", ctypes.c_uint64), ("p", ctypes.c_double)]
+    """``sir_dropout_t`` (include/sirconv.h): the hashed feature-dropout mask of QK (seed, p), the
+    seed given by value or as a device pointer (``seed_ptr``, read by the kernels)."""
+    _fields_ = [("seed", ctypes.c_uint64), ("p", ctypes.c_double), ("seed_ptr", ctypes.c_void_p)]
 
 
 def _drop(drop):
-    """ctypes pointer argument for an optional (seed, p) pair."""
+    """ctypes pointer argument for an optional (seed, p) pair; ``seed`` is an int or a one-element
+    int64 device tensor (the graph-safe form: its value is read on the device by every kernel)."""
     if drop is None:
         return None
     seed, p = drop
-    return ctypes.byref(Dropout(int(seed) & (2 ** 64 - 1), float(p)))
+    if isinstance(seed, torch.Tensor):
+        if not (seed.is_cuda and seed.dtype == torch.int64 and seed.numel() >= 1):
+            raise ValueError("dropout seed tensor must be a CUDA int64 tensor")
+        return ctypes.byref(Dropout(0, float(p), seed.data_ptr()))
+    return ctypes.byref(Dropout(int(seed) & (2 ** 64 - 1), float(p), None))
 
 
 _lib = None

@@ -26,6 +26,16 @@ from . import _native, linalg
 from .graph import DEFAULT_CHUNK, get_plan
 
 
+# Test instrumentation: when a list, every forward appends the [Q | K] the edge kernels read (detached
+# copies, in call order), so a parity check can tell sigma' near-ties from errors (tests/test_stacks_gpu.py).
+QK_TRACE = None
+
+
+def _trace_qk(QK):
+    if QK_TRACE is not None:
+        QK_TRACE.append(QK.detach().clone())
+
+
 def activation_code(act):
     """Map the reference's ``activation`` callable (``conv.py:32,45``) to a kernel code."""
     if isinstance(act, nn.LeakyReLU):
@@ -192,6 +202,7 @@ class SIRConvFunction(torch.autograd.Function):
         W_cat = torch.cat([W_Q, W_K], 0)
         # [b_Q; 0] by one pad kernel (a zeros fill + a cat were two launches: small batches are launch-bound)
         QK = linalg.mm_wt(X, W_cat, F.pad(b_Q, (0, H)) if b_Q is not None else None, drop=drop)
+        _trace_qk(QK)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=torch.float32)
@@ -264,6 +275,7 @@ class SIRConvFunction16(torch.autograd.Function):
         else:       # X.to(dt) fused into the GEMM's loads; the rounded X (for dW) written by it
             Xh = torch.empty(X.shape, dtype=dt, device=X.device)
             QK = linalg.mm16_wt(X, W_cat, b_cat, dt, acopy=Xh, drop=drop)
+        _trace_qk(QK)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
         S = torch.empty((V, H), device=X.device, dtype=dt)
@@ -324,6 +336,7 @@ class SIRConv(nn.Module):
 
     use_fused = True      # whole-layer Function when dropout is off and inputs are fp32
     fuse_edge_mlp = True  # Sequential sigma / max aggregation on the fused edge-MLP kernels (sirgcn.edgemlp)
+    native_linear = True  # projections of the non-fused routes on the native GEMMs (linalg.linear)
 
     def __init__(self, input_dim, hidden_dim, output_dim, activation, dropout=0, inner_bias=True,
                  outer_bias=True, agg_type='sum'):
@@ -338,13 +351,29 @@ class SIRConv(nn.Module):
         self._agg_type = agg_type
         self.chunk = DEFAULT_CHUNK
 
-    def _drop(self):
+    def _drop(self, device):
         """(seed, p) of this forward's fused feature dropout (conv.py:35,60-61), or None (eval / p = 0).
-        The seed comes from torch's default CPU generator (reproducible under torch.manual_seed); a
-        forward captured into a HIP graph replays the mask drawn at capture time."""
+        The seed is a one-element int64 tensor drawn ON THE DEVICE from torch's CUDA generator — where
+        the reference's nn.Dropout draws its bits — and read by the kernels from device memory: no
+        host sync, the CPU RNG stream is untouched, and a forward captured in a HIP graph draws a
+        fresh mask on every replay (the captured randint is graph-safe philox)."""
         if not (self.training and self.dropout.p > 0):
             return None
-        return int(torch.randint(0, 2 ** 62, (1,)).item()), float(self.dropout.p)
+        return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64), float(self.dropout.p)
+
+    def _linear(self, x, W, b):
+        """nn.Linear on the native GEMMs (``linalg.linear``; torch's F.linear when disabled or for
+        operands the kernels do not take)."""
+        if self.native_linear:
+            return linalg.linear(x, W, b)
+        return F.linear(x, W, b)
+
+    def _relation(self, S):
+        """``linear_relation`` (conv.py:65) — native when it is still the constructor's nn.Linear."""
+        lin = self.linear_relation
+        if type(lin) is nn.Linear:
+            return self._linear(S, lin.weight, lin.bias)
+        return lin(S)
 
     def _project(self, feat_key, feat_query):
         """K = drop(X W_K^T), Q = drop(X W_Q^T + b_Q) (``conv.py:60-61``) as ONE GEMM -> [V, 2H]."""
@@ -354,11 +383,13 @@ class SIRConv(nn.Module):
             b = None
             if self.linear_query.bias is not None:
                 b = torch.cat([self.linear_query.bias, self.linear_query.bias.new_zeros(H)])
-            QK = F.linear(feat_query, W, b)
+            QK = self._linear(feat_query, W, b)
         else:
-            QK = torch.cat([self.linear_query(feat_query), self.linear_key(feat_key)], 1)
+            QK = torch.cat([self._linear(feat_query, self.linear_query.weight, self.linear_query.bias),
+                            self._linear(feat_key, self.linear_key.weight, None)], 1)
         if self.training and self.dropout.p > 0:
             QK = self.dropout(QK)   # independent masks for Q and K, as two nn.Dropout calls
+        _trace_qk(QK)
         return QK
 
     def forward(self, graph, feat):
@@ -393,7 +424,7 @@ class SIRConv(nn.Module):
                 a1, sl, lin, a2 = sq
                 QK = self._project(feat_key, feat_query)
                 S = EdgeMLPSum.apply(QK, lin.weight, lin.bias, plan, H, self._agg_type, a1, sl, a2)
-                return self.linear_relation(S.to(QK.dtype))
+                return self._relation(S.to(QK.dtype))
         if act is None or self._agg_type == "max":
             from .generic import generic_forward       # edge-materialised native path
             return generic_forward(self, plan, feat_key, feat_query)
@@ -403,7 +434,7 @@ class SIRConv(nn.Module):
             return SIRConvFunction.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
                                          self.linear_key.weight, self.linear_relation.weight,
                                          self.linear_relation.bias, plan, self._agg_type, act, slope,
-                                         torch.is_grad_enabled(), self._drop())
+                                         torch.is_grad_enabled(), self._drop(feat_query.device))
         if (self.use_fused and feat_key is feat_query and torch.is_autocast_enabled() and H % 4 == 0
                 and feat_query.dtype in (torch.float32, torch.bfloat16, torch.float16)
                 and self.linear_query.weight.dtype == torch.float32):
@@ -413,10 +444,10 @@ class SIRConv(nn.Module):
                     return SIRConvFunction16.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
                                                    self.linear_key.weight, self.linear_relation.weight,
                                                    self.linear_relation.bias, plan, self._agg_type, act, slope,
-                                                   torch.is_grad_enabled(), dt, self._drop())
+                                                   torch.is_grad_enabled(), dt, self._drop(feat_query.device))
         QK = self._project(feat_key, feat_query)
         S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope, torch.is_grad_enabled())
-        return self.linear_relation(S)
+        return self._relation(S)
 
     def extra_repr(self):
         return f"agg_type={self._agg_type!r}"

@@ -105,7 +105,7 @@ def generic_forward(conv, plan, feat_key, feat_query):
     Z = EdgeGatherAdd.apply(QK, plan, H)
     A = conv.activation(Z)                                   # any callable, autograd through torch
     if conv._agg_type == "max":
-        M = conv.linear_relation(A)                          # conv.py:47 per-edge W_R
+        M = conv._relation(A)                                # conv.py:47 per-edge W_R
         return EdgeMax.apply(M, plan)                        # conv.py:65: no post-projection for max
     S = EdgeSum.apply(A, plan, conv._agg_type)
-    return conv.linear_relation(S)
+    return conv._relation(S)

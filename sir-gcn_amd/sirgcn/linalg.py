@@ -113,6 +113,46 @@ def mm_tn16(A, B, colsum=False):
     return mm_tn(A.float(), B.float(), colsum=colsum)
 
 
+class _Linear(torch.autograd.Function):
+    """nn.Linear (``y = x W^T + b``) with forward and backward on the native GEMMs: y = mm_wt,
+    dx = mm_w(dy, W), (dW, db) = mm_tn(dy, x, colsum) — the weight and bias gradients from one pass."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return mm_wt(x, W, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = mm_w(dy, W) if ctx.needs_input_grad[0] else None
+        dW = db = None
+        need_b = ctx.has_b and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1]:
+            if need_b:
+                dW, db = mm_tn(dy, x, colsum=True)
+            else:
+                dW = mm_tn(dy, x)
+        elif need_b:
+            db = dy.sum(0)
+        return dx, dW, db
+
+
+def linear(x, W, b=None):
+    """``F.linear(x, W, b)`` (the reference's ``nn.Linear`` calls, conv.py:60-61,65) on the native
+    split-fp16 GEMMs for fp32 GPU operands the kernels take; anything else (autocast, fp64, other
+    layouts, CPU tensors) is torch's own ``F.linear`` — the same dataflow autocast would run."""
+    if (USE_NATIVE and not torch.is_autocast_enabled() and x.dim() == 2 and W.dim() == 2
+            and x.dtype == torch.float32 and W.dtype == torch.float32 and (b is None or b.dtype == torch.float32)):
+        xc = x if x.stride(1) == 1 else x.contiguous()
+        if _ok(xc) and _w_ok(W, W.shape[0]) and W.shape[1] % 4 == 0 and W.is_contiguous() \
+                and (b is None or b.is_cuda):
+            return _Linear.apply(xc, W, b.contiguous() if b is not None else None)
+    return torch.nn.functional.linear(x, W, b)
+
+
 def _tn_torch(A, B):
     """torch A^T B; long-K shapes run as k row blocks of one batched GEMM (hipBLASLt is 2x faster
     that way than as one GEMM) summed in a fixed order."""

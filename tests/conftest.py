@@ -107,12 +107,32 @@ def assert_parity(actual, ref32, truth64, rel=1e-5, what="", strict=False, facto
     tmax = t.abs().max().item() if t.numel() else 0.0
     bound = rel * t.abs() + 1e-6 * tmax + 4 * ref_abs
     bad = ((a - t).abs() > bound)
-    assert not bad.any(), f"{what}: {int(bad.sum())} elements beyond the reference's own error envelope"
+    if bad.any():
+        i = int(((a - t).abs() - bound).argmax())
+        af, rf, tf, bf = a.reshape(-1), r.reshape(-1), t.reshape(-1), bound.reshape(-1)
+        raise AssertionError(f"{what}: {int(bad.sum())} elements beyond the reference's own error envelope "
+                             f"(worst #{i}: ours {af[i].item():.6e} ref32 {rf[i].item():.6e} fp64 {tf[i].item():.6e} "
+                             f"bound {bf[i].item():.2e}; max|ref32-fp64| {ref_abs:.2e})")
     PARITY_FALLBACKS.append((what + (" [strict: relL2 ok, elementwise via envelope]" if strict else ""),
                              e_r, e_act, e_ref))
 
 
+TIE_CONDITIONED = []       # (what, sigma' flips, worst |z64| / ulp-mag, arg flips, worst gap / ulp-mag)
+
+
+def tie_conditioned(what, n_sigma, w_sigma, n_arg=0, w_arg=0.0):
+    """Record a case scored against the oracle conditioned on the kernel's own Q, K (and arg edges)
+    because of near-ties (oracle.sigma_tie_flips / max_tie_flips)."""
+    TIE_CONDITIONED.append((what, n_sigma, w_sigma, n_arg, w_arg))
+
+
 def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    if TIE_CONDITIONED:
+        terminalreporter.write_line(f"near-ties: {len(TIE_CONDITIONED)} case(s) scored against the oracle conditioned "
+                                    "on the kernel's Q, K / arg edges (sigma' flips, worst |z|/(2^-24 mag), "
+                                    "arg flips, worst gap/(2^-24 mag)):")
+        for what, n_s, w_s, n_a, w_a in TIE_CONDITIONED:
+            terminalreporter.write_line(f"  {what}: {n_s}, {w_s:.2f}, {n_a}, {w_a:.2f}")
     if PARITY_FALLBACKS:
         terminalreporter.write_line(f"assert_parity: {len(PARITY_FALLBACKS)} tensor(s) passed through the fp64 "
                                     "envelope (relL2 vs ref32 / vs fp64 / ref32's own vs fp64):")

@@ -59,14 +59,11 @@ def test_mask_statistics(p):
     assert torch.all(_mask(64, 64, 1, 1.0) == 0) and torch.all(_mask(64, 64, 1, 0.0) == 1)
 
 
-@pytest.mark.parametrize("M,K,N,ntw", [(70001, 256, 512, "0"), (3001, 128, 256, "0"), (5000, 256, 256, "0"),
-                                       (2000, 300, 200, "0"), (4099, 512, 256, "0"), (300, 64, 96, "0"),
-                                       (3001, 128, 256, "1"), (5000, 256, 256, "1"), (70001, 256, 200, "1")])
-def test_gemm_epilogue_applies_the_mask(M, K, N, ntw, monkeypatch):
+@pytest.mark.parametrize("M,K,N", [(70001, 256, 512), (3001, 128, 256), (5000, 256, 256), (2000, 300, 200),
+                                   (4099, 512, 256), (300, 64, 96), (70001, 256, 200)])
+def test_gemm_epilogue_applies_the_mask(M, K, N):
     """C = drop(A W^T + b) in the GEMM epilogue == sir_dropout_apply on the plain GEMM, bit for bit
-    (the shapes route to the persistent, tiled and — opted in with SIR_NT_W=1 — weight-resident
-    split-fp16 kernels)."""
-    monkeypatch.setenv("SIR_NT_W", ntw)
+    (the shapes route to the persistent, tiled and small-batch split-fp16 kernels)."""
     g = torch.Generator(device=DEV).manual_seed(M + N)
     A = torch.randn(M, K, device=DEV, generator=g)
     W = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
@@ -129,7 +126,7 @@ def test_fused_layer_train_mode_vs_explicit_mask(agg, H):
     m = SIRConv(d, H, O, nn.LeakyReLU(0.2), p, agg_type=agg).to(DEV).train()
     seeds = []
     draw = m._drop
-    m._drop = lambda: seeds.append(draw()) or seeds[-1]
+    m._drop = lambda dev: seeds.append(draw(dev)) or seeds[-1]
     g = Graph(src, dst, V)
     Xd = X.to(DEV).requires_grad_(True)
     Y = m(g, Xd)
@@ -179,7 +176,7 @@ def test_fused_autocast_layer_train_mode_vs_explicit_mask(dt):
     m = SIRConv(d, H, O, nn.LeakyReLU(0.2), p, agg_type="sum").to(DEV).train()
     seeds = []
     draw = m._drop
-    m._drop = lambda: seeds.append(draw()) or seeds[-1]
+    m._drop = lambda dev: seeds.append(draw(dev)) or seeds[-1]
     g = Graph(src, dst, V)
     Xd = X.to(DEV).requires_grad_(True)
     with torch.autocast("cuda", dtype=dt):
@@ -264,3 +261,65 @@ def test_modular_path_keeps_nn_dropout():
     m.eval()
     with torch.no_grad():
         assert not torch.equal(m(g, (X, X)), Y.detach())
+
+
+def test_device_seed_equals_host_seed():
+    """A seed given as a device tensor (the graph-safe form, sir_dropout_t.seed_ptr) draws exactly the
+    mask of the same value given by value — in sir_dropout_apply, the GEMM epilogue and the edge passes."""
+    seed = 0x1234_5678_9ABC_DEF0
+    st = torch.tensor([seed], dtype=torch.int64, device=DEV)
+    V, H2 = 1000, 512
+    assert torch.equal(_mask(V, H2, st, 0.3), _mask(V, H2, seed, 0.3))
+    g = torch.Generator(device=DEV).manual_seed(3)
+    A = torch.randn(20000, 256, device=DEV, generator=g)
+    W = torch.randn(512, 256, device=DEV, generator=g) / 16
+    pk = _native.gemm_pack(W)
+    assert torch.equal(_native.gemm_nt(A, pk, drop=(st, 0.2)), _native.gemm_nt(A, pk, drop=(seed, 0.2)))
+    assert torch.equal(_native.gemm_nt_direct(A[:3000], W, False, drop=(st, 0.2)),
+                       _native.gemm_nt_direct(A[:3000], W, False, drop=(seed, 0.2)))
+
+
+def test_captured_training_step_draws_a_fresh_mask_per_replay():
+    """a training forward captured in a HIP graph must not replay the capture-time mask.
+    The seed is drawn on the device (torch.randint, graph-safe) and read by the kernels, so two replays
+    give two different masks — each one consistent between the forward and the backward (the
+    gradients equal an eager step run on the replay's own mask)."""
+    gen = torch.Generator().manual_seed(21)
+    V, E, d, H, O, p = 600, 9000, 32, 256, 16, 0.3
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V, (E,), generator=gen)
+    X, dY = torch.randn(V, d, generator=gen).to(DEV), torch.randn(V, O, generator=gen).to(DEV)
+    torch.manual_seed(4)
+    m = SIRConv(d, H, O, nn.LeakyReLU(0.2), p, agg_type="sum").to(DEV).train()
+    g = Graph(src, dst, V)
+    seeds = []
+    draw = m._drop
+    m._drop = lambda dev: seeds.append(draw(dev)) or seeds[-1]
+    x = X.clone().requires_grad_(True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):                       # warm-up (plans, packs) outside the capture
+        for _ in range(2):
+            m.zero_grad(set_to_none=False)
+            x.grad = None
+            m(g, x).backward(dY)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    x.grad = torch.zeros_like(x)
+    with torch.cuda.graph(graph):
+        Y = m(g, x)
+        Y.backward(dY)
+    seed_t = seeds[-1][0]
+    outs = []
+    for _ in range(2):
+        x.grad.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        outs.append((seed_t.clone(), Y.detach().clone(), x.grad.clone()))
+    assert not torch.equal(outs[0][0], outs[1][0]), "the captured seed draw must run again on replay"
+    assert not torch.equal(outs[0][1], outs[1][1]), "two replays must use two different masks"
+    m._drop = lambda dev: (outs[1][0].clone(), p)   # eager step on the second replay's mask
+    x2 = X.clone().requires_grad_(True)
+    Y2 = m(g, x2)
+    Y2.backward(dY)
+    assert torch.equal(Y2, outs[1][1]) and torch.equal(x2.grad, outs[1][2])

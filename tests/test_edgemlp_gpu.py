@@ -11,7 +11,7 @@ import torch
 from torch import nn
 
 import oracle
-from conftest import assert_parity
+from conftest import assert_parity, tie_conditioned
 
 from sirgcn import SIRConv, _native
 from sirgcn.graph import Graph
@@ -35,19 +35,71 @@ def _graph(seed, V=300, E=3000, dup=200):
     return torch.cat([src, src[idx]]), torch.cat([dst, dst[idx]]), V, gen
 
 
-def _run(m, g, X, dY):
+def _run(m, g, X, dY, capture=None):
+    """One fwd + bwd; ``capture`` (a dict) receives the layer's own QK (the projection the edge
+    kernels read) and, for max, its arg edges as edge ids."""
     x = X.to(DEV).requires_grad_(True)
     m.zero_grad(set_to_none=True)
-    Y = m(g, x)
-    Y.backward(dY.to(DEV))
+    restore = []
+    if capture is not None:
+        from sirgcn import edgemlp
+        from sirgcn.graph import get_plan
+        orig_proj, orig_fwd = m._project, edgemlp._fwd
+
+        def proj(fk, fq):
+            QK = orig_proj(fk, fq)
+            capture["qk"] = QK.detach().double().cpu()
+            return QK
+
+        def fwd(*a, **k):
+            out = orig_fwd(*a, **k)
+            if a[-1] is not None and a[-1].dtype == torch.int32:
+                pos = a[-1].long().cpu()
+                eid = get_plan(g, torch.device(DEV), m.chunk).dst.eid.cpu()
+                capture["arg"] = torch.where(pos >= 0, eid[pos.clamp_min(0)], torch.full_like(pos, -1))
+            return out
+        m._project = proj
+        edgemlp._fwd = fwd
+        restore = [lambda: delattr(m, "_project"), lambda: setattr(edgemlp, "_fwd", orig_fwd)]
+    try:
+        Y = m(g, x)
+        Y.backward(dY.to(DEV))
+    finally:
+        for r in restore:
+            r()
     torch.cuda.synchronize()
     out = {"Y": Y.detach().cpu(), "dX": x.grad.cpu()}
     out.update({n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.grad is not None})
     return out
 
 
-def _oracle(m, src, dst, V, X, dY, agg, act, dtype):
-    """reference_cpu_step with m's weights, in dtype; act: kernel-activation name or a module."""
+def _tie_condition(m, src, dst, V, X, act, cap, what):
+    """oracle kwargs for scoring a layer whose sigma' signs or max arg edges differ from the fp64
+    oracle's ONLY on near-ties (|z| or the gap within a few fp32 ulps of the values' magnitude;
+    the assertion fails otherwise): the oracle is then evaluated on the kernel's own Q, K and arg
+    edges (oracle.reference_cpu_step qk= / max_arg=).  {} when nothing flipped."""
+    Wq, bq, Wk, Wr, br = (t.detach().cpu() for t in (m.linear_query.weight, m.linear_query.bias,
+                                                     m.linear_key.weight, m.linear_relation.weight,
+                                                     m.linear_relation.bias))
+    n_s, w_s, bad_s = oracle.sigma_tie_flips(cap["qk"], src, dst, X, Wq, bq, Wk)
+    assert bad_s == 0, f"{what}: {bad_s} sigma' sign flips beyond the fp32 rounding of z (worst {w_s:.1f} ulp-mag)"
+    n_a = w_a = 0
+    if "arg" in cap:
+        M64, mag = oracle.max_edge_values(src, dst, X, Wq, bq, Wk, Wr, br, act, 0.2)
+        n_a, w_a, bad_a = oracle.max_tie_flips(M64, mag, dst, V, cap["arg"])
+        assert bad_a == 0, f"{what}: {bad_a} arg-max flips beyond fp32 rounding (worst {w_a:.1f} ulp-mag)"
+    if n_s == 0 and n_a == 0:
+        return {}
+    tie_conditioned(what, n_s, w_s, n_a, w_a)
+    kw = {"qk": cap["qk"]} if n_s else {}
+    if n_a:
+        kw["max_arg"] = cap["arg"]
+    return kw
+
+
+def _oracle(m, src, dst, V, X, dY, agg, act, dtype, **cond):
+    """reference_cpu_step with m's weights, in dtype; act: kernel-activation name or a module;
+    ``cond``: qk= / max_arg= (see :func:`_tie_condition`)."""
     w = [t.detach().cpu().to(dtype) for t in (m.linear_query.weight, m.linear_query.bias, m.linear_key.weight,
                                               m.linear_relation.weight, m.linear_relation.bias)]
     a = act
@@ -55,7 +107,7 @@ def _oracle(m, src, dst, V, X, dY, agg, act, dtype):
         a = copy.deepcopy(act).cpu().to(dtype)
         for p in a.parameters():
             p.requires_grad_(True)
-    r = oracle.reference_cpu_step(src, dst, V, X.to(dtype), *w, dY.to(dtype), agg, a, 0.2)
+    r = oracle.reference_cpu_step(src, dst, V, X.to(dtype), *w, dY.to(dtype), agg, a, 0.2, **cond)
     if isinstance(act, nn.Module):
         r["act.1.weight"] = a[1].weight.grad
         r["act.1.bias"] = a[1].bias.grad
@@ -88,10 +140,12 @@ def test_seq_sigma_fused_vs_oracle(agg, H, Fo, chunk, monkeypatch):
     m = m.to(DEV)
     m.chunk = chunk
     g = Graph(src, dst, V)
-    got = _run(m, g, X, dY)
+    cap = {}
+    got = _run(m, g, X, dY, capture=cap)
     assert "activation.1.weight" in got
-    r32 = _oracle(m, src, dst, V, X, dY, agg, m.activation, torch.float32)
-    r64 = _oracle(m, src, dst, V, X, dY, agg, m.activation, torch.float64)
+    cond = _tie_condition(m, src, dst, V, X, None, cap, f"seq {agg} H{H} F{Fo} c{chunk}")
+    r32 = _oracle(m, src, dst, V, X, dY, agg, m.activation, torch.float32, **cond)
+    r64 = _oracle(m, src, dst, V, X, dY, agg, m.activation, torch.float64, **cond)
     for k, kr in (("Y", "Y"), ("dX", "dX"), ("linear_query.weight", "dW_Q"), ("linear_query.bias", "db_Q"),
                   ("linear_key.weight", "dW_K"), ("linear_relation.weight", "dW_R"),
                   ("linear_relation.bias", "db_R"), ("activation.1.weight", "act.1.weight"),
@@ -121,10 +175,12 @@ def test_max_fused_vs_oracle_first_wins(act, H, O, chunk, monkeypatch):
     m = SIRConv(d, H, O, mod, 0, agg_type="max").to(DEV)
     m.chunk = chunk
     g = Graph(src, dst, V)
-    got = _run(m, g, X, dY)
+    cap = {}
+    got = _run(m, g, X, dY, capture=cap)
     assert torch.all(got["Y"][V - 25:] == 0)                   # isolated destinations: 0 (no bias)
-    r32 = _oracle(m, src, dst, V, X, dY, "max", act, torch.float32)
-    r64 = _oracle(m, src, dst, V, X, dY, "max", act, torch.float64)
+    cond = _tie_condition(m, src, dst, V, X, act, cap, f"max {act} H{H} O{O} c{chunk}")
+    r32 = _oracle(m, src, dst, V, X, dY, "max", act, torch.float32, **cond)
+    r64 = _oracle(m, src, dst, V, X, dY, "max", act, torch.float64, **cond)
     for k, kr in (("Y", "Y"), ("dX", "dX"), ("linear_query.weight", "dW_Q"), ("linear_query.bias", "db_Q"),
                   ("linear_key.weight", "dW_K"), ("linear_relation.weight", "dW_R"),
                   ("linear_relation.bias", "db_R")):
@@ -185,9 +241,11 @@ def test_dictionary_lookup_sweep_shapes_fused(n, monkeypatch):
     torch.manual_seed(n)
     sigma = nn.Sequential(nn.ReLU(inplace=True), nn.Linear(H, H), nn.ReLU(inplace=True))
     m = SIRConv(H, H, H, sigma, 0, agg_type="sum").to(DEV)
-    got = _run(m, g, X, dY)
-    r32 = _oracle(m, src, dst, V, X, dY, "sum", m.activation, torch.float32)
-    r64 = _oracle(m, src, dst, V, X, dY, "sum", m.activation, torch.float64)
+    cap = {}
+    got = _run(m, g, X, dY, capture=cap)
+    cond = _tie_condition(m, src, dst, V, X, None, cap, f"dictionary n={n}")
+    r32 = _oracle(m, src, dst, V, X, dY, "sum", m.activation, torch.float32, **cond)
+    r64 = _oracle(m, src, dst, V, X, dY, "sum", m.activation, torch.float64, **cond)
     for k, kr in (("Y", "Y"), ("dX", "dX"), ("linear_query.weight", "dW_Q"), ("linear_key.weight", "dW_K"),
                   ("linear_relation.weight", "dW_R"), ("activation.1.weight", "act.1.weight"),
                   ("activation.1.bias", "act.1.bias")):
