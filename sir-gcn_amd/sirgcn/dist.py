@@ -69,6 +69,7 @@ def all_reduce_sum(t, group=None):
 
 def partition_rows(in_deg, world):
     """Row boundaries [0, r_1, ..., V] with ≈E/world in-edges per range (edge-balanced)."""
+    in_deg = in_deg.cpu()                  # plan time: a few host syncs, any device
     V = in_deg.numel()
     E = int(in_deg.sum().item())
     cum = torch.cumsum(in_deg.to(torch.int64), 0)
