@@ -7,9 +7,17 @@
  * with the edge UDF  m = out_norm[u] * in_norm[v] * sigma(eq[v] + ek[u])   conv.py:43-45
  * which DGL 2.1.0 runs as index_select gathers + elementwise + GSpMM(copy_e, sum)
  * over the in-edge CSC (and, under autograd, gsddmm/index_add for the backward).
- * The three entry points below replace exactly that: the forward aggregation and the
- * two halves of its backward.  Everything around them (the nn.Linear projections
- * conv.py:60-61,65, degrees/norms conv.py:51-57) stays with the host (PyTorch on ROCm).
+ * Entry points, by the reference code they replace (INTEGRATION.md §2 has the table):
+ *  - the edge aggregation and its backward (conv.py:43-45,63): sir_edge_agg_fwd / _bwd_dst /
+ *    _bwd_src / _bwd (one launch), with the sign mask of the ReLU family (sir_mask_words);
+ *  - the degree norms (conv.py:51-57): sir_degree_norms;
+ *  - the projections and their gradients (nn.Linear, conv.py:60-61,65): the split-fp16 MFMA
+ *    GEMMs sir_gemm_nt / sir_gemm_nt_direct / sir_gemm_tn and the 16-bit (autocast) ones, the
+ *    bias gradients sir_col_sum, the Q/K feature dropout sir_dropout_t (conv.py:35,60-61);
+ *  - agg='max' and the per-edge Linear sigma (conv.py:46-47): sir_edge_mlp_* / sir_edge_max_*;
+ *    the edge-materialised helpers (sir_edge_gather_add, sir_segment_*);
+ *  - GraphNorm (models/norm.py:7-29): sir_graph_norm_fwd / _bwd;
+ *  - the graph input (DGL's CSC build for batched graphs): sir_csr_build / sir_csr_perm.
  *
  * Conventions
  *  - All pointers are DEVICE pointers; all work is enqueued on `stream` (a hipStream_t,
@@ -95,8 +103,11 @@ int sir_dropout_apply(void* X, int64_t ldx, int64_t M, int64_t N, int dtype, int
 /*
  * Per-edge sign-mask size (64-bit words) for hidden size H and activation `act`, or 0 when
  * the sign-mask backward is not available (needs act in {RELU, LEAKY_RELU}, H % 4 == 0,
- * 128 < H <= 1024, 16-B aligned rows).  Layout, edge e in destination-CSR order:
- *   word mask[e*NW + 4*j + w], bit l  =  (Q[v] + K[u])[4*(l + 64*j) + w] > 0.
+ * H <= 1024, 16-B aligned rows).  Layout, edge e in destination-CSR order:
+ *   128 < H (full-wave rows): word mask[e*NW + 4*j + w], bit l = (Q[v] + K[u])[4*(l + 64*j) + w] > 0;
+ *   H <= 128 (rows of L = 4, 8, 16 or 32 lanes, L = the smallest holding H/4): a record of
+ *   NW 64-bit words (NW = max(L/16, 1)) read as little-endian bits, bit (w*L + l) =
+ *   (Q[v] + K[u])[4*l + w] > 0 (bits past H zero).
  */
 int64_t sir_mask_words(int64_t H, int act);
 

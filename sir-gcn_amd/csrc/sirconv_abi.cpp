@@ -43,7 +43,7 @@ int check_common(const char* fn, const int32_t* rowptr, const int32_t* col, cons
 
 int check_mask(const char* fn, int64_t H, int act) {
     if (sir_mask_words(H, act) == 0)
-        return fail(SIR_EUNSUPPORTED, fn, "sign mask needs act RELU/LEAKY_RELU, H % 4 == 0 and 128 < H <= 1024");
+        return fail(SIR_EUNSUPPORTED, fn, "sign mask needs act RELU/LEAKY_RELU, H % 4 == 0 and H <= 1024");
     return SIR_OK;
 }
 
@@ -76,8 +76,12 @@ const char* sir_last_error(void) { return g_last_error.c_str(); }
 
 int64_t sir_mask_words(int64_t H, int act) {
     if (act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU) return 0;
-    if (H % 4 != 0 || H <= 128 || H > 1024) return 0;
-    return 4 * ((H + 255) / 256);
+    if (H % 4 != 0 || H <= 0 || H > 1024) return 0;
+    if (H > 128) return 4 * ((H + 255) / 256);       // full-wave rows: one 64-bit ballot per 256 features x 4 slots
+    // sub-wave rows (LPR = 4, 8, 16, 32 lanes of float4): an H-bit record, at least 8 bytes
+    const int64_t hc = H / 4;
+    const int64_t lpr = hc <= 4 ? 4 : (hc <= 8 ? 8 : (hc <= 16 ? 16 : 32));
+    return lpr >= 16 ? lpr / 16 : 1;
 }
 
 int sir_degree_norms(const int32_t* rowptr_dst, float* in_norm,
@@ -191,7 +195,7 @@ int sir_edge_agg_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
     if (n_items > 0 && Gd == nullptr) return fail(SIR_EINVAL, fn, "Gd must be non-NULL");
     if (mask != nullptr) {
         if ((rc = check_mask(fn, H, act))) return rc;
-        if (n_items > 0 && perm_s == nullptr) return fail(SIR_EINVAL, fn, "sign-mask mode needs perm_s");
+        if (n_items > 0 && col_s != nullptr && perm_s == nullptr) return fail(SIR_EINVAL, fn, "sign-mask mode needs perm_s");
     } else {
         if (ldq < H || ldk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
         if (n_items > 0 && (Q == nullptr || K == nullptr)) return fail(SIR_EINVAL, fn, "K/Q must be non-NULL");
@@ -232,7 +236,7 @@ int sir_edge_agg_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
     if ((rc = check_mask(fn, H, act))) return rc;
     if (ldg < H || lddq < H || lddk < H) return fail(SIR_EINVAL, fn, "leading dimensions must be >= H");
     if ((n_items > 0 || n_items_s > 0) && G == nullptr) return fail(SIR_EINVAL, fn, "G must be non-NULL");
-    if (n_items_s > 0 && perm_s == nullptr) return fail(SIR_EINVAL, fn, "sign-mask mode needs perm_s");
+    if (n_items_s > 0 && col_s != nullptr && perm_s == nullptr) return fail(SIR_EINVAL, fn, "sign-mask mode needs perm_s");
     if (n_items > INT32_MAX || n_items_s > INT32_MAX || n_items + n_items_s > (int64_t)INT32_MAX)
         return fail(SIR_EINVAL, fn, "too many work items for one launch");
     sir::EdgeArgs a{};

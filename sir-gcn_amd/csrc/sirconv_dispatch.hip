@@ -1,4 +1,6 @@
 // sirconv_dispatch.hip — shape selection, combine kernel launch, and the per-pass dispatch.
+#include <type_traits>
+
 #include "sirconv_edge_impl.h"
 
 namespace sir {
@@ -195,11 +197,30 @@ hipError_t run_edge_dual(int dtype, const EdgeArgs& a, const int32_t* splits, in
                     aligned_to(a.partial, 16) && aligned_to(b.partial, 16) &&
                     (a.ldg % 4 == 0) && (a.ldo % 4 == 0) && (b.ldo % 4 == 0);
     Shape s;
-    if (!pick_shape(a.H, v4, &s) || s.vw != 4 || s.lpr != 64) {
-        *why = "the one-launch backward needs the sign-mask layout (H % 4 == 0, 128 < H <= 1024, aligned rows)";
+    if (!pick_shape(a.H, v4, &s) || s.vw != 4) {
+        *why = "the sign-mask backward needs H % 4 == 0, H <= 1024 and aligned rows";
         return hipErrorInvalidValue;
     }
     hipError_t err;
+    if (s.lpr < 64) {
+        // sub-wave rows (H <= 128): the two mask-read passes one after the other (the dQ pass reads
+        // only the mask records, no VALU-heavy select chain to hide under the dK gathers)
+        if ((agg != AGG_SUM && agg != AGG_SYM) || (act != ACT_RELU && act != ACT_LEAKY)) {
+            *why = "the one-launch backward covers SUM/SYM with ReLU/LeakyReLU only";
+            return hipErrorInvalidValue;
+        }
+        auto two = [&](auto stt) -> hipError_t {
+            constexpr int STT = decltype(stt)::value;
+            hipError_t e2 = run_edge_t<STT>(MODE_BWD_DST, a, agg, act, s, splits, n_splits, a.out, a.ldo, false, st);
+            if (e2 != hipSuccess) return e2;
+            return run_edge_t<STT>(MODE_BWD_SRC, b, agg, act, s, splits_s, n_splits_s, b.out, b.ldo, false, st);
+        };
+        switch (dtype) {
+            case ST_BF16: return two(std::integral_constant<int, ST_BF16>());
+            case ST_F16: return two(std::integral_constant<int, ST_F16>());
+            default: return two(std::integral_constant<int, ST_F32>());
+        }
+    }
     switch (dtype) {
         case ST_BF16: err = launch_edge_dual<ST_BF16>(a, b, agg, act, s, st); break;
         case ST_F16: err = launch_edge_dual<ST_F16>(a, b, agg, act, s, st); break;

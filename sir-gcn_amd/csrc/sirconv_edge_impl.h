@@ -244,7 +244,15 @@ __device__ __forceinline__ void writelane(uint32_t& v, uint32_t x, int k) {
 
 // ------------------------------------------------------------------------------ edge batch
 // Processes UU consecutive edges [e, e+UU) of one row: all gathers issued before any use.
-template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int UU, bool MASKW>
+// Sub-wave rows (LPR < 64, H <= 128) in sign-mask mode: one record of MW uint32 per edge (>= 8 B),
+// bit (w * LPR + li) = (z of feature 4 li + w) > 0, i.e. per vector slot w an LPR-bit field of the
+// row's lanes.  The forward extracts each sub-row's field from the wave ballot (shift by the
+// sub-row's first lane), the backward passes read the record with one 8- or 16-B load per lane.
+template <int LPR> constexpr int sub_mask_words() { return LPR >= 16 ? LPR / 8 : 2; }
+
+// MK: 0 = no sign mask, 1 = write it (forward, ReLU family), 2 = read it (backward passes of sub-wave
+// rows: no Q / K gathered; the full-wave rows' mask backward is k_edge_mask below)
+template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int UU, int MK>
 __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                                            const typename Stor<ST>::T* __restrict__ C, int64_t ldc,
                                            const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
@@ -252,15 +260,36 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                                            int li, int HC,
                                            const float (&rv)[NV][VW], const float (&gv)[NV][VW],
                                            float (&acc)[NV][VW], uint64_t* __restrict__ mask, int lane,
-                                           const int* __restrict__ upre = nullptr) {
+                                           const int* __restrict__ upre = nullptr,
+                                           const int* __restrict__ perm = nullptr) {
+    constexpr bool MASKW = MK == 1, MASKR = MK == 2;
+    static_assert(!MASKR || (LPR < 64 && NV == 1 && VW == 4 && MODE != MODE_FWD), "mask-read rows are sub-wave float4 rows");
     int u[UU];
 #pragma unroll
     for (int i = 0; i < UU; ++i) u[i] = (upre != nullptr) ? upre[i] : col[e + i];
     constexpr bool kBufGather = SIR_FWD_BUFGATHER && MODE == MODE_FWD && ST == ST_F32 && VW == 4 && LPR == 64 && MASKW;
-    float cv[UU][NV][VW];
+    constexpr int MWS = sub_mask_words<LPR>();
+    uint32_t mr[MASKR ? UU : 1][MWS];
+    if constexpr (MASKR) {
+        // the batch's mask records (edge position: e + i in the dst CSR; perm[e + i] for the source pass)
+#pragma unroll
+        for (int i = 0; i < UU; ++i) {
+            const int p = (MODE == MODE_BWD_SRC) ? perm[e + i] : e + i;
+            const uint32_t* rp = reinterpret_cast<const uint32_t*>(mask) + (int64_t)p * MWS;
+            if constexpr (MWS == 4) {
+                const sir_u4 t = *reinterpret_cast<const sir_u4*>(rp);
+                mr[i][0] = t.x; mr[i][1] = t.y; mr[i][2] = t.z; mr[i][3] = t.w;
+            } else {
+                const sir_u2 t = *reinterpret_cast<const sir_u2*>(rp);
+                mr[i][0] = t.x; mr[i][1] = t.y;
+            }
+        }
+    }
+    float cv[MASKR ? 1 : UU][NV][VW];
     float gc[(MODE == MODE_BWD_SRC) ? UU : 1][NV][VW];
 #pragma unroll
     for (int i = 0; i < UU; ++i) {
+      if constexpr (!MASKR) {
         // gathers are unconditional: lanes past the row (c >= HC) re-read column 0 and their
         // values are never used.  A guarded load becomes an exec-masked branch whose result the
         // compiler may copy inside the branch, i.e. wait for right after issuing it — that
@@ -285,6 +314,7 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                 vload_gather<ST, VW>(cv[i][j], cp + (c < HC ? c : 0) * VW);
             }
         }
+      }
         if constexpr (MODE == MODE_BWD_SRC) {
             const auto* gp = G + (int64_t)u[i] * ldg;
 #pragma unroll
@@ -301,7 +331,44 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 #pragma unroll
         for (int i = 0; i < UU; ++i) cf[i] = norm_col[u[i]] * nr;  // out_norm[u] * in_norm[v]
     }
-    if constexpr (MASKW) {
+    if constexpr (MASKW && LPR < 64) {
+        // sub-wave rows: this sub-row's LPR-bit field of each slot's ballot (shifted down by its first
+        // lane), packed into the edge's record; lane li stores record word li (several rounds when the
+        // batch's words outnumber the sub-row's lanes)
+        static_assert(VW == 4 && NV == 1, "sub-wave mask rows are float4 rows");
+        constexpr uint32_t FM = (LPR == 32) ? 0xffffffffu : ((1u << LPR) - 1u);
+        const int sh = lane - li;
+        uint32_t wd[UU][MWS];
+#pragma unroll
+        for (int i = 0; i < UU; ++i) {
+            uint32_t x[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint64_t b = __builtin_amdgcn_ballot_w64(li < HC && (rv[0][w] + cv[i][0][w]) > 0.f);
+                x[w] = (uint32_t)(b >> sh) & FM;
+            }
+            if constexpr (LPR == 32) {
+                wd[i][0] = x[0]; wd[i][1] = x[1]; wd[i][2] = x[2]; wd[i][3] = x[3];
+            } else if constexpr (LPR == 16) {
+                wd[i][0] = x[0] | (x[1] << 16); wd[i][1] = x[2] | (x[3] << 16);
+            } else {
+                wd[i][0] = x[0] | (x[1] << LPR) | (x[2] << (2 * LPR)) | (x[3] << (3 * LPR)); wd[i][1] = 0u;
+            }
+        }
+        uint32_t* mrec = reinterpret_cast<uint32_t*>(mask) + (int64_t)e * MWS;
+        constexpr int NWB = UU * MWS;
+#pragma unroll
+        for (int r = 0; r < (NWB + LPR - 1) / LPR; ++r) {
+            uint32_t mine = 0u;
+#pragma unroll
+            for (int i = 0; i < UU; ++i)
+#pragma unroll
+                for (int k = 0; k < MWS; ++k)
+                    if ((i * MWS + k) / LPR == r) mine = (li == (i * MWS + k) % LPR) ? wd[i][k] : mine;
+            const int q = r * LPR + li;
+            if (q < NWB) mrec[q] = mine;
+        }
+    } else if constexpr (MASKW) {
         // sign mask of z for the sign-mask backward: word (j*4+w), bit lane = z[(lane+64j)*4+w] > 0.
         // The UU edges' words are contiguous; lane k takes word k (uniform -> per-lane select)
         // and ONE store writes the batch's UU*NW*8 bytes.
@@ -362,6 +429,13 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
                         float m = sig<ACT>(z, slope);
                         if constexpr (AGG == AGG_SYM) m = cf[i] * m;
                         acc[j][w] += m;
+                    } else if constexpr (MASKR) {
+                        // sigma'(z) from the stored sign: bit (w * LPR + li) of the record
+                        float t = (MODE == MODE_BWD_SRC) ? gc[i][j][w] : gv[j][w];
+                        if constexpr (AGG == AGG_SYM) t = t * cf[i];
+                        const int wi = (w * LPR) / 32;
+                        const bool pos = (mr[i][wi] >> (((w * LPR) % 32) + li)) & 1u;
+                        acc[j][w] += pos ? t : (ACT == ACT_RELU ? 0.f : t * slope);
                     } else if constexpr (MODE == MODE_BWD_DST) {
                         const float z = rv[j][w] + cv[i][j][w];
                         float t = gv[j][w];
@@ -383,9 +457,9 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 // MODE_FWD:     R = Q (rows = dst), C = K (gathered by src), out = S
 // MODE_BWD_DST: R = Q, C = K, G = dS rows (row-side), out = dQ, optional Gm = G/deg (MEAN)
 // MODE_BWD_SRC: R = K (rows = src), C = Q (gathered by dst), G = Gd (gathered), out = dK
-template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U, bool MASKW>
+template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U, int MK>
 __global__ void __launch_bounds__(256)
-k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
+k_edge(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
        const int4* __restrict__ items, int64_t n_items,
        const typename Stor<ST>::T* __restrict__ R, int64_t ldr,
        const typename Stor<ST>::T* __restrict__ C, int64_t ldc,
@@ -422,7 +496,7 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
         const int c = li + LPR * j;
 #pragma unroll
         for (int w = 0; w < VW; ++w) { acc[j][w] = 0.f; rv[j][w] = 0.f; gv[j][w] = 0.f; }
-        if (c < HC) vload_row<ST, VW>(rv[j], rp + c * VW);
+        if (MK != 2 && c < HC) vload_row<ST, VW>(rv[j], rp + c * VW);     // mask-read passes need no Q / K row
     }
     if constexpr (MODE == MODE_BWD_DST) {
         const auto* gp = G + (int64_t)row * ldg;
@@ -468,35 +542,35 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col,
 #pragma unroll
                 for (int i = 0; i < U; ++i) uc[i] = __builtin_amdgcn_readlane(vc, i);
                 vc = load_col(e + U);
-                edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC,
-                                                                     rv, gv, acc, mask, lane, uc);
+                edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC,
+                                                                  rv, gv, acc, mask, lane, uc, perm);
             }
         }
     } else {
         for (; e + U <= e1; e += U)
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv,
-                                                                 acc, mask, lane);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv,
+                                                              acc, mask, lane, nullptr, perm);
     }
     if constexpr (U > 8) {
         if (e + 8 <= e1) {
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 8, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 8, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
             e += 8;
         }
     }
     if constexpr (U > 4) {
         if (e + 4 <= e1) {
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 4, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 4, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
             e += 4;
         }
     }
     if constexpr (U > 2) {
         if (e + 2 <= e1) {
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 2, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 2, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
             e += 2;
         }
     }
     if (e < e1)
-        edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 1, MASKW>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane);
+        edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 1, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
 
     if (slot < 0) {
         if constexpr (MODE == MODE_FWD && AGG == AGG_MEAN) {
@@ -1165,12 +1239,12 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     const int64_t waves = (a.n_items + RPW - 1) / RPW;
     const int64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
-    constexpr bool kMaskable = (MODE == MODE_FWD) && (LPR == 64) && (VW == 4) &&
-                               (ACT == ACT_RELU || ACT == ACT_LEAKY);
+    constexpr bool kReluFamily = (ACT == ACT_RELU || ACT == ACT_LEAKY) && (VW == 4) && (LPR == 64 || NV == 1);
+    constexpr bool kMaskable = (MODE == MODE_FWD) && kReluFamily;
     if constexpr (kMaskable) {
         if (a.mask_out != nullptr) {
-            hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, true>), dim3((unsigned)blocks), dim3(256), 0, st,
-                               a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
+            hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, 1>), dim3((unsigned)blocks), dim3(256), 0, st,
+                               a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,
                                cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
                                a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out, a.drop);
             return hipGetLastError();
@@ -1178,8 +1252,19 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     } else {
         if (a.mask_out != nullptr) return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, false>), dim3((unsigned)blocks), dim3(256), 0, st,
-                       a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items,
+    if constexpr (MODE != MODE_FWD && kReluFamily && LPR < 64) {
+        if (a.mask_in != nullptr) {          // sub-wave rows, sign-mask backward
+            hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, 2>), dim3((unsigned)blocks), dim3(256), 0, st,
+                               a.rowptr, a.col, a.perm, reinterpret_cast<const int4*>(a.items), a.n_items,
+                               cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
+                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm,
+                               const_cast<uint64_t*>(a.mask_in), a.drop);
+            return hipGetLastError();
+        }
+    }
+    if (a.mask_in != nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, 0>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,
                        cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
                        a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr, a.drop);
     return hipGetLastError();
@@ -1248,8 +1333,9 @@ template <int ST, int MODE, int ACT, int AGG>
 static hipError_t launch_edge_shape(const EdgeArgs& a, Shape s, hipStream_t st) {
     if constexpr (MODE != MODE_FWD && (ACT == ACT_RELU || ACT == ACT_LEAKY)) {
         if (a.mask_in != nullptr) {
-            if (s.vw != 4 || s.lpr != 64) return hipErrorInvalidValue;
-            return launch_mask_shape<ST, MODE, ACT, AGG>(a, s, st);
+            if (s.vw != 4) return hipErrorInvalidValue;
+            if (s.lpr == 64) return launch_mask_shape<ST, MODE, ACT, AGG>(a, s, st);
+            // sub-wave rows: k_edge in mask-read mode (below)
         }
     } else if constexpr (MODE != MODE_FWD) {
         if (a.mask_in != nullptr) return hipErrorInvalidValue;

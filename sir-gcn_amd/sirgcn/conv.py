@@ -431,23 +431,38 @@ class SIRConv(nn.Module):
         fused = (self.use_fused and feat_key is feat_query and feat_query.dtype == torch.float32 and feat_query.is_cuda
                  and not torch.is_autocast_enabled() and self.linear_query.weight.dtype == torch.float32)
         if fused:
-            return SIRConvFunction.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
-                                         self.linear_key.weight, self.linear_relation.weight,
-                                         self.linear_relation.bias, plan, self._agg_type, act, slope,
-                                         torch.is_grad_enabled(), self._drop(feat_query.device))
-        if (self.use_fused and feat_key is feat_query and torch.is_autocast_enabled() and H % 4 == 0
+            return self._fused(SIRConvFunction, feat_query, plan, act, slope)
+        if (self.use_fused and feat_key is feat_query and torch.is_autocast_enabled()
                 and feat_query.dtype in (torch.float32, torch.bfloat16, torch.float16)
                 and self.linear_query.weight.dtype == torch.float32):
             dt = torch.get_autocast_dtype("cuda")
             if dt in (torch.bfloat16, torch.float16):
                 with torch.autocast("cuda", enabled=False):
-                    return SIRConvFunction16.apply(feat_query, self.linear_query.weight, self.linear_query.bias,
-                                                   self.linear_key.weight, self.linear_relation.weight,
-                                                   self.linear_relation.bias, plan, self._agg_type, act, slope,
-                                                   torch.is_grad_enabled(), dt, self._drop(feat_query.device))
+                    return self._fused(SIRConvFunction16, feat_query, plan, act, slope, dt)
         QK = self._project(feat_key, feat_query)
         S = EdgeAggregate.apply(QK, plan, H, self._agg_type, act, slope, torch.is_grad_enabled())
         return self._relation(S)
+
+    def _fused(self, fn, X, plan, act, slope, *dt):
+        """The whole-layer Function ``fn`` (SIRConvFunction / SIRConvFunction16).  Widths that are not
+        multiples of 4 (the reference's own H = 75 / 95, zinc/train.py:206, ogbn-arxiv/train.py:303)
+        run on zero-padded copies: the padded columns of Q, K are exactly 0, sigma(0) = 0 for every
+        supported sigma and every gradient reaching them is 0, so the padded layer computes the same
+        values; the pads' autograd slices the gradients back to the parameters' shapes."""
+        W_Q, b_Q, W_K = self.linear_query.weight, self.linear_query.bias, self.linear_key.weight
+        W_R, b_R = self.linear_relation.weight, self.linear_relation.bias
+        (H, d), O = W_Q.shape, W_R.shape[0]
+        Hp, dp, Op = -(-H // 4) * 4, -(-d // 4) * 4, -(-O // 4) * 4
+        if (Hp, dp, Op) != (H, d, O):
+            W_Q = F.pad(W_Q, (0, dp - d, 0, Hp - H))
+            b_Q = F.pad(b_Q, (0, Hp - H)) if b_Q is not None else None
+            W_K = F.pad(W_K, (0, dp - d, 0, Hp - H))
+            W_R = F.pad(W_R, (0, Hp - H, 0, Op - O))
+            b_R = F.pad(b_R, (0, Op - O)) if b_R is not None else None
+            X = F.pad(X, (0, dp - d)) if dp != d else X
+        Y = fn.apply(X, W_Q, b_Q, W_K, W_R, b_R, plan, self._agg_type, act, slope, torch.is_grad_enabled(), *dt,
+                     self._drop(X.device))
+        return Y[:, :O] if Op != O else Y
 
     def extra_repr(self):
         return f"agg_type={self._agg_type!r}"

@@ -67,8 +67,8 @@ def test_argument_checks_are_synchronous_and_reported():
     # leading dimension smaller than H
     assert _fwd(lib, p, p, p, 1, 16, 0, p, 8, p, 16, n, n, 0, 2, p, 16) == 1
     assert b"leading" in lib.sir_last_error()
-    # sign mask is only defined for the ReLU family and 128 < H <= 1024
-    assert _fwd(lib, p, p, p, 1, 64, 0, p, 64, p, 64, n, n, 0, 2, p, 64, mask=p) == 2
+    # sign mask is only defined for the ReLU family, H % 4 == 0 and H <= 1024
+    assert _fwd(lib, p, p, p, 1, 66, 0, p, 66, p, 66, n, n, 0, 2, p, 66, mask=p) == 2
     assert _fwd(lib, p, p, p, 1, 256, 0, p, 256, p, 256, n, n, 0, 3, p, 256, mask=p) == 2
     assert b"sign mask" in lib.sir_last_error()
     # mask-mode src pass needs the permutation
@@ -110,8 +110,11 @@ def test_mask_words_contract():
     lib = _native.load()
     assert lib.sir_mask_words(256, 2) == 4 and lib.sir_mask_words(256, 1) == 4
     assert lib.sir_mask_words(300, 2) == 8 and lib.sir_mask_words(1024, 2) == 16
-    assert lib.sir_mask_words(128, 2) == 0 and lib.sir_mask_words(256, 3) == 0
-    assert lib.sir_mask_words(258, 2) == 0 and lib.sir_mask_words(2048, 2) == 0
+    assert lib.sir_mask_words(256, 3) == 0 and lib.sir_mask_words(2048, 2) == 0
+    assert lib.sir_mask_words(258, 2) == 0 and lib.sir_mask_words(75, 2) == 0
+    # sub-wave rows: an H-bit record of >= 8 bytes (32 lanes: 16 B)
+    assert lib.sir_mask_words(128, 2) == 2 and lib.sir_mask_words(68, 1) == 2 and lib.sir_mask_words(64, 2) == 1
+    assert lib.sir_mask_words(60, 2) == 1 and lib.sir_mask_words(4, 2) == 1 and lib.sir_mask_words(32, 1) == 1
 
 
 def test_empty_work_is_a_no_op():
