@@ -402,7 +402,7 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
                                   f"d_in=H=d_out={H}, agg={args.agg}, LeakyReLU(0.2), {dtn}, feat_dropout={p_drop}"
                                   f"{' (autocast)' if dtn != 'f32' else ''}; fwd+bwd incl. projections",
                       "graph": args.graph, "V": V, "E": E, "hidden": H, "agg": args.agg,
-                      "parallelism": f"edge-cut dst-range x{world}, sparse halo all-to-all" if world > 1
+                      "parallelism": f"edge-cut dst-range x{world}, pipelined sparse halo all-to-alls" if world > 1
                       else "single GPU"}}
     if rehearsal:
         out["rehearsal"] = ("CPU gloo rehearsal of the launcher / partition / exchange plumbing; edge passes on "
@@ -438,12 +438,12 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
         out["projections"] = projections(gemm, args.steps)
     out["design_bytes_per_step"] = design_bytes(kernels, gemm, args.steps, ms)
     if dconv is not None:     # halo exchange volume per rank (rows of H), max over ranks
-        ex = torch.tensor([dg.n_halo, int(dg.send_idx.numel()), edges_local], dtype=torch.float64,
+        ex = torch.tensor([dg.n_halo, dg.exchange_rows()[1], edges_local], dtype=torch.float64,
                           device=dev if args.dist_backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(ex, op=dist.ReduceOp.MAX)
         out["exchange"] = {"halo_rows_max": int(ex[0]), "send_rows_max": int(ex[1]), "local_edges_max": int(ex[2]),
-                           "bytes_per_direction_max": int(ex[0]) * H * s,
+                           "bytes_per_direction_max": int(ex[0]) * H * s, "exchange_chunks": dg.chunks,
                            "dense_allgather_rows": V - min(dg.bounds[i + 1] - dg.bounds[i] for i in range(world))}
     if world == 1 and not args.no_aux:
         out["roofline"]["copy_GBps_measured"] = copy_rate(dev)

@@ -47,8 +47,11 @@ extern "C" {
 
 #define SIR_ABI_VERSION 11
 
-/* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57) */
-enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2 };
+/* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57).  SIR_AGG_ACCUMULATE,
+ * OR'd into the forward's `agg` (SUM / SYM): S[v] = S[v] + the sum over the given items' edges, rows
+ * without items untouched — the segmented forward of the multi-GPU edge-cut (a row's edges in fixed
+ * segments by source owner, each aggregated as its halo rows land; sirgcn/dist.py). */
+enum { SIR_AGG_SUM = 0, SIR_AGG_MEAN = 1, SIR_AGG_SYM = 2, SIR_AGG_ACCUMULATE = 16 };
 /* sigma: the `activation` callable of conv.py:32,45 (ReLU, LeakyReLU(slope), GELU erf / tanh) */
 enum { SIR_ACT_IDENTITY = 0, SIR_ACT_RELU = 1, SIR_ACT_LEAKY_RELU = 2, SIR_ACT_GELU = 3, SIR_ACT_GELU_TANH = 4 };
 /* Storage dtype of every feature matrix of an edge-pass call (Q, K, G, S, dQ, dK, Gm): fp32, or the

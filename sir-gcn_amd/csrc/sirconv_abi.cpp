@@ -117,6 +117,10 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
                      int agg, int act, float slope,
                      void* S, int64_t lds, uint64_t* mask_out, float* partial, void* stream) {
     const char* fn = "sir_edge_agg_fwd";
+    const int accumulate = (agg & SIR_AGG_ACCUMULATE) != 0;
+    agg &= ~SIR_AGG_ACCUMULATE;
+    if (accumulate && agg == SIR_AGG_MEAN)
+        return fail(SIR_EUNSUPPORTED, fn, "SIR_AGG_ACCUMULATE: segment sums of SUM / SYM only (divide afterwards for MEAN)");
     int rc = check_common(fn, rowptr, col, items, n_items, splits, n_splits, H, dtype, agg, act,
                           norm_row, norm_col, S, partial);
     if (rc) return rc;
@@ -131,6 +135,7 @@ int sir_edge_agg_fwd(const int32_t* rowptr, const int32_t* col,
     a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope; a.H = (int)H;
     a.out = S; a.ldo = lds; a.partial = partial; a.Gm = nullptr; a.ldgm = H;
     a.mask_out = mask_out;
+    a.accumulate = accumulate;
     const char* why = nullptr;
     hipError_t err = sir::run_edge(sir::MODE_FWD, dtype, a, agg, act, splits, n_splits, S, lds,
                                    agg == SIR_AGG_MEAN, static_cast<hipStream_t>(stream), &why);

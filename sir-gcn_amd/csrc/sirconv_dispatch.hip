@@ -1,6 +1,4 @@
 // sirconv_dispatch.hip — shape selection, combine kernel launch, and the per-pass dispatch.
-#include <type_traits>
-
 #include "sirconv_edge_impl.h"
 
 namespace sir {
@@ -106,15 +104,15 @@ hipError_t run_colsum(const float* X, int64_t ld, int64_t n_rows, int n_cols, fl
 
 template <int ST, bool MEAN_DIV>
 static hipError_t launch_combine(const int32_t* splits, int64_t n, const float* partial, int H,
-                                 void* out, int64_t ldo, int vw, hipStream_t st, const Drop& drop) {
+                                 void* out, int64_t ldo, int vw, hipStream_t st, const Drop& drop, int accumulate = 0) {
     if (n == 0) return hipSuccess;
     TP<ST>* o = static_cast<TP<ST>*>(out);
     if (vw == 4)
         hipLaunchKernelGGL((k_combine<ST, MEAN_DIV, 4>), dim3((unsigned)n), dim3(1024), 0, st,
-                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo, drop);
+                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo, drop, accumulate);
     else
         hipLaunchKernelGGL((k_combine<ST, MEAN_DIV, 1>), dim3((unsigned)n), dim3(1024), 0, st,
-                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo, drop);
+                           reinterpret_cast<const int4*>(splits), partial, H, o, ldo, drop, accumulate);
     return hipGetLastError();
 }
 
@@ -130,7 +128,8 @@ static hipError_t run_edge_t(int mode, const EdgeArgs& a, int agg, int act, Shap
     }
     if (err != hipSuccess || n_splits == 0) return err;
     return mean_div ? launch_combine<ST, true>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st, a.drop)
-                    : launch_combine<ST, false>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st, a.drop);
+                    : launch_combine<ST, false>(splits, n_splits, a.partial, a.H, out_final, ld_final, s.vw, st, a.drop,
+                                                a.accumulate);
 }
 
 hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
@@ -143,7 +142,9 @@ hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowpt
 
 static bool aligned_to(const void* p, uintptr_t b) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & (b - 1)) == 0; }
 
-// Vector width 4 needs every row start 16-B aligned.
+// Vector width 4 needs every row start 16-B aligned (fp32) / 8-B aligned (16-bit).  (16-bit rows with
+// 8 values per lane on sub-wave rows were measured 2-3x slower on the power-law graph, forward slower on
+// molecule batches too: profiles/r04_ab_vw8_16bit.txt.)
 bool pick_shape(int H, bool vec4_ok, Shape* s) {
     if (H <= 0) return false;
     if (vec4_ok && (H % 4) == 0) {
@@ -202,25 +203,6 @@ hipError_t run_edge_dual(int dtype, const EdgeArgs& a, const int32_t* splits, in
         return hipErrorInvalidValue;
     }
     hipError_t err;
-    if (s.lpr < 64) {
-        // sub-wave rows (H <= 128): the two mask-read passes one after the other (the dQ pass reads
-        // only the mask records, no VALU-heavy select chain to hide under the dK gathers)
-        if ((agg != AGG_SUM && agg != AGG_SYM) || (act != ACT_RELU && act != ACT_LEAKY)) {
-            *why = "the one-launch backward covers SUM/SYM with ReLU/LeakyReLU only";
-            return hipErrorInvalidValue;
-        }
-        auto two = [&](auto stt) -> hipError_t {
-            constexpr int STT = decltype(stt)::value;
-            hipError_t e2 = run_edge_t<STT>(MODE_BWD_DST, a, agg, act, s, splits, n_splits, a.out, a.ldo, false, st);
-            if (e2 != hipSuccess) return e2;
-            return run_edge_t<STT>(MODE_BWD_SRC, b, agg, act, s, splits_s, n_splits_s, b.out, b.ldo, false, st);
-        };
-        switch (dtype) {
-            case ST_BF16: return two(std::integral_constant<int, ST_BF16>());
-            case ST_F16: return two(std::integral_constant<int, ST_F16>());
-            default: return two(std::integral_constant<int, ST_F32>());
-        }
-    }
     switch (dtype) {
         case ST_BF16: err = launch_edge_dual<ST_BF16>(a, b, agg, act, s, st); break;
         case ST_F16: err = launch_edge_dual<ST_F16>(a, b, agg, act, s, st); break;

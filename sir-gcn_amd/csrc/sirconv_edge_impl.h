@@ -248,7 +248,7 @@ __device__ __forceinline__ void writelane(uint32_t& v, uint32_t x, int k) {
 // bit (w * LPR + li) = (z of feature 4 li + w) > 0, i.e. per vector slot w an LPR-bit field of the
 // row's lanes.  The forward extracts each sub-row's field from the wave ballot (shift by the
 // sub-row's first lane), the backward passes read the record with one 8- or 16-B load per lane.
-template <int LPR> constexpr int sub_mask_words() { return LPR >= 16 ? LPR / 8 : 2; }
+template <int LPR, int VW> constexpr int sub_mask_words() { return LPR * VW >= 64 ? LPR * VW / 32 : 2; }
 
 // MK: 0 = no sign mask, 1 = write it (forward, ReLU family), 2 = read it (backward passes of sub-wave
 // rows: no Q / K gathered; the full-wave rows' mask backward is k_edge_mask below)
@@ -268,7 +268,7 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 #pragma unroll
     for (int i = 0; i < UU; ++i) u[i] = (upre != nullptr) ? upre[i] : col[e + i];
     constexpr bool kBufGather = SIR_FWD_BUFGATHER && MODE == MODE_FWD && ST == ST_F32 && VW == 4 && LPR == 64 && MASKW;
-    constexpr int MWS = sub_mask_words<LPR>();
+    constexpr int MWS = sub_mask_words<LPR, VW>();
     uint32_t mr[MASKR ? UU : 1][MWS];
     if constexpr (MASKR) {
         // the batch's mask records (edge position: e + i in the dst CSR; perm[e + i] for the source pass)
@@ -276,7 +276,12 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
         for (int i = 0; i < UU; ++i) {
             const int p = (MODE == MODE_BWD_SRC) ? perm[e + i] : e + i;
             const uint32_t* rp = reinterpret_cast<const uint32_t*>(mask) + (int64_t)p * MWS;
-            if constexpr (MWS == 4) {
+            if constexpr (MWS == 8) {
+                const sir_u4 t = reinterpret_cast<const sir_u4*>(rp)[0];
+                const sir_u4 t2 = reinterpret_cast<const sir_u4*>(rp)[1];
+                mr[i][0] = t.x; mr[i][1] = t.y; mr[i][2] = t.z; mr[i][3] = t.w;
+                mr[i][4] = t2.x; mr[i][5] = t2.y; mr[i][6] = t2.z; mr[i][7] = t2.w;
+            } else if constexpr (MWS == 4) {
                 const sir_u4 t = *reinterpret_cast<const sir_u4*>(rp);
                 mr[i][0] = t.x; mr[i][1] = t.y; mr[i][2] = t.z; mr[i][3] = t.w;
             } else {
@@ -341,18 +346,12 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
         uint32_t wd[UU][MWS];
 #pragma unroll
         for (int i = 0; i < UU; ++i) {
-            uint32_t x[4];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
+            for (int k = 0; k < MWS; ++k) wd[i][k] = 0u;
+#pragma unroll
+            for (int w = 0; w < VW; ++w) {
                 const uint64_t b = __builtin_amdgcn_ballot_w64(li < HC && (rv[0][w] + cv[i][0][w]) > 0.f);
-                x[w] = (uint32_t)(b >> sh) & FM;
-            }
-            if constexpr (LPR == 32) {
-                wd[i][0] = x[0]; wd[i][1] = x[1]; wd[i][2] = x[2]; wd[i][3] = x[3];
-            } else if constexpr (LPR == 16) {
-                wd[i][0] = x[0] | (x[1] << 16); wd[i][1] = x[2] | (x[3] << 16);
-            } else {
-                wd[i][0] = x[0] | (x[1] << LPR) | (x[2] << (2 * LPR)) | (x[3] << (3 * LPR)); wd[i][1] = 0u;
+                wd[i][(w * LPR) / 32] |= ((uint32_t)(b >> sh) & FM) << ((w * LPR) % 32);
             }
         }
         uint32_t* mrec = reinterpret_cast<uint32_t*>(mask) + (int64_t)e * MWS;
@@ -457,24 +456,24 @@ __device__ __forceinline__ void edge_batch(int e, const int* __restrict__ col,
 // MODE_FWD:     R = Q (rows = dst), C = K (gathered by src), out = S
 // MODE_BWD_DST: R = Q, C = K, G = dS rows (row-side), out = dQ, optional Gm = G/deg (MEAN)
 // MODE_BWD_SRC: R = K (rows = src), C = Q (gathered by dst), G = Gd (gathered), out = dK
+// One wave's items (64 / LPR consecutive items, one per sub-row) of a pass; `wave` is the wave's
+// index among the pass's waves.
 template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U, int MK>
-__global__ void __launch_bounds__(256)
-k_edge(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
-       const int4* __restrict__ items, int64_t n_items,
-       const typename Stor<ST>::T* __restrict__ R, int64_t ldr,
-       const typename Stor<ST>::T* __restrict__ C, int64_t ldc,
-       const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
-       const float* __restrict__ norm_row, const float* __restrict__ norm_col,
-       float slope, int H,
-       typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
-       typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask, Drop drop) {
-    drop = drop_resolve(drop);
+__device__ __forceinline__ void
+edge_wave(int64_t wave, const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
+          const int4* __restrict__ items, int64_t n_items,
+          const typename Stor<ST>::T* __restrict__ R, int64_t ldr,
+          const typename Stor<ST>::T* __restrict__ C, int64_t ldc,
+          const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
+          const float* __restrict__ norm_row, const float* __restrict__ norm_col,
+          float slope, int H,
+          typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
+          typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask, const Drop& drop,
+          int accumulate = 0) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LPR;
     const int li = lane - sub * LPR;
-    int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if constexpr (LPR == 64) wave = __builtin_amdgcn_readfirstlane((int)wave);
     const int64_t idx = wave * RPW + sub;
     if (idx >= n_items) return;
     int4 it = items[idx];
@@ -587,6 +586,19 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col, const int* _
 #pragma unroll
                 for (int j = 0; j < NV; ++j) drop_vec<ST, VW>(drop, row, (li + LPR * j) * VW, acc[j]);
             }
+        } else {
+            if (accumulate) {       // segmented forward (sirgcn.dist): S[v] = S[v] + this segment's sum
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    const int c = li + LPR * j;
+                    if (c < HC) {
+                        float prev[VW];
+                        vload_row<ST, VW>(prev, op + c * VW);
+#pragma unroll
+                        for (int w = 0; w < VW; ++w) acc[j][w] = prev[w] + acc[j][w];
+                    }
+                }
+            }
         }
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
@@ -601,6 +613,25 @@ k_edge(const int* __restrict__ rowptr, const int* __restrict__ col, const int* _
             if (c < HC) vstore_part<VW>(pp + c * VW, acc[j]);
         }
     }
+}
+
+template <int ST, int MODE, int ACT, int AGG, int LPR, int NV, int VW, int U, int MK>
+__global__ void __launch_bounds__(256)
+k_edge(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ perm,
+       const int4* __restrict__ items, int64_t n_items,
+       const typename Stor<ST>::T* __restrict__ R, int64_t ldr,
+       const typename Stor<ST>::T* __restrict__ C, int64_t ldc,
+       const typename Stor<ST>::T* __restrict__ G, int64_t ldg,
+       const float* __restrict__ norm_row, const float* __restrict__ norm_col,
+       float slope, int H,
+       typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
+       typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask, Drop drop, int accumulate) {
+    drop = drop_resolve(drop);
+    int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if constexpr (LPR == 64) wave = __builtin_amdgcn_readfirstlane((int)wave);
+    edge_wave<ST, MODE, ACT, AGG, LPR, NV, VW, U, MK>(wave, rowptr, col, perm, items, n_items, R, ldr, C, ldc, G, ldg,
+                                                     norm_row, norm_col, slope, H, out, ldo, partial, Gm, ldgm, mask,
+                                                     drop, accumulate);
 }
 
 // ------------------------------------------------------------------------------ sign-mask backward
@@ -1138,7 +1169,7 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
 template <int ST, bool MEAN_DIV, int VW>
 __global__ void __launch_bounds__(1024)
 k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
-          int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, Drop drop) {
+          int H, typename Stor<ST>::T* __restrict__ out, int64_t ldo, Drop drop, int accumulate) {
     drop = drop_resolve(drop);
     __shared__ float red[1024 * VW];
     const int4 sp = splits[blockIdx.x];
@@ -1187,6 +1218,12 @@ k_combine(const int4* __restrict__ splits, const float* __restrict__ partial,
                 for (int w = 0; w < VW; ++w) r[w] = r[w] / degf;
             }
             if (drop.on()) drop_vec<ST, VW>(drop, sp.x, c * VW, r);      // backward passes only (host)
+            if (accumulate) {           // segmented forward: prior S row + this segment's sum
+                float prev[VW];
+                tload_p<ST, VW, false>(prev, out + (int64_t)sp.x * ldo + c * VW);
+#pragma unroll
+                for (int w = 0; w < VW; ++w) r[w] = prev[w] + r[w];
+            }
             tstore_p<ST, VW, false>(out + (int64_t)sp.x * ldo + c * VW, r);
         }
         __syncthreads();
@@ -1239,14 +1276,15 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     const int64_t waves = (a.n_items + RPW - 1) / RPW;
     const int64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
-    constexpr bool kReluFamily = (ACT == ACT_RELU || ACT == ACT_LEAKY) && (VW == 4) && (LPR == 64 || NV == 1);
+    constexpr bool kReluFamily = (ACT == ACT_RELU || ACT == ACT_LEAKY) && VW == 4 && (LPR == 64 || NV == 1);
     constexpr bool kMaskable = (MODE == MODE_FWD) && kReluFamily;
     if constexpr (kMaskable) {
         if (a.mask_out != nullptr) {
             hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, 1>), dim3((unsigned)blocks), dim3(256), 0, st,
                                a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,
                                cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
-                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out, a.drop);
+                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out, a.drop,
+                               a.accumulate);
             return hipGetLastError();
         }
     } else {
@@ -1258,7 +1296,7 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
                                a.rowptr, a.col, a.perm, reinterpret_cast<const int4*>(a.items), a.n_items,
                                cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
                                a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm,
-                               const_cast<uint64_t*>(a.mask_in), a.drop);
+                               const_cast<uint64_t*>(a.mask_in), a.drop, 0);
             return hipGetLastError();
         }
     }
@@ -1266,7 +1304,8 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, 0>), dim3((unsigned)blocks), dim3(256), 0, st,
                        a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,
                        cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
-                       a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr, a.drop);
+                       a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr, a.drop,
+                       a.accumulate);
     return hipGetLastError();
 }
 
@@ -1310,8 +1349,16 @@ static hipError_t launch_dual_shape(const EdgeArgs& a, const EdgeArgs& b, Shape 
 
 template <int ST>
 static hipError_t launch_edge_dual_st(const EdgeArgs& a, const EdgeArgs& b, int agg, int act, Shape s, hipStream_t st) {
-    if (s.vw != 4 || s.lpr != 64 || (agg != AGG_SUM && agg != AGG_SYM) || (act != ACT_RELU && act != ACT_LEAKY))
+    if (s.vw != 4 || (agg != AGG_SUM && agg != AGG_SYM) || (act != ACT_RELU && act != ACT_LEAKY))
         return hipErrorInvalidValue;
+    if (s.lpr < 64) {
+        // sub-wave rows: the two mask-read passes one after the other (one launch with the waves
+        // interleaved, as for full-wave rows, measured 8 % slower on config 2's molecule batch: the
+        // combined kernel's register budget lowers the occupancy of both latency-bound passes)
+        hipError_t e2 = launch_edge_pass<ST, MODE_BWD_DST>(a, agg, act, s, st);
+        if (e2 != hipSuccess) return e2;
+        return launch_edge_pass<ST, MODE_BWD_SRC>(b, agg, act, s, st);
+    }
     if (act == ACT_RELU)
         return agg == AGG_SUM ? launch_dual_shape<ST, ACT_RELU, AGG_SUM>(a, b, s, st)
                               : launch_dual_shape<ST, ACT_RELU, AGG_SYM>(a, b, s, st);

@@ -1526,16 +1526,20 @@ k_gemm_reduce2(const float* __restrict__ part, int P, int64_t count, int Nc, flo
     const float* src = cs ? cpart : part;
     const int64_t cnt = cs ? (int64_t)Mc : count;
     if (i >= cnt) return;
-    float s = 0.f;
+    // the P split partials in split order: sums of 16, Kahan-added (a column sum of a few hundred
+    // partials of mixed sign loses ~P ulps of the largest partial in a plain sequential sum)
+    float s = 0.f, c = 0.f;
     int q = 0;
     for (; q + 16 <= P; q += 16) {
         float v[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) v[j] = src[(int64_t)(q + j) * cnt + i];
+        float t = 0.f;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) s += v[j];
+        for (int j = 0; j < 16; ++j) t += v[j];
+        kahan_add(s, c, t);
     }
-    for (; q < P; ++q) s += src[(int64_t)q * cnt + i];
+    for (; q < P; ++q) kahan_add(s, c, src[(int64_t)q * cnt + i]);
     if (cs) colsum[i] = s;
     else C[(i / Nc) * ldc + i % Nc] = s;
 }

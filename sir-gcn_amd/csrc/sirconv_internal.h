@@ -32,6 +32,7 @@ struct EdgeArgs {
     const uint64_t* mask_in;     // backward: sign-mask mode (Q/K not read)
     const int* perm;             // BWD_SRC mask mode: src-CSR position -> dst-CSR position
     Drop drop;                   // backward passes: feature dropout on the output rows (sirconv_dropout.h)
+    int accumulate;              // forward: out[v] = out[v] + sum (rows of the items only; segmented forward)
 };
 
 struct Shape {

@@ -232,14 +232,19 @@ def _storage(*ts):
     return STORAGE[dts.pop()]
 
 
-def edge_agg_fwd(csr, Q, K, norm_row, norm_col, agg, act, slope, S, partial, mask_out=None):
+AGG_ACCUMULATE = 16       # SIR_AGG_ACCUMULATE
+
+
+def edge_agg_fwd(csr, Q, K, norm_row, norm_col, agg, act, slope, S, partial, mask_out=None, accumulate=False):
+    """``accumulate``: S[v] += the sum over ``csr.items``' edges (rows without items untouched; SUM / SYM)."""
     lib = load()
     H = S.shape[1]
     with _Timed("sir_edge_agg_fwd", S.device):
         rc = lib.sir_edge_agg_fwd(
             _ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, _ptr(csr.splits), csr.n_splits,
             H, _storage(Q, K, S), _ptr(Q), _ld(Q, H), _ptr(K), _ld(K, H), _ptr(norm_row), _ptr(norm_col),
-            AGG[agg], act, float(slope), _ptr(S), _ld(S, H), _ptr(mask_out), _ptr(partial), _stream(S.device))
+            AGG[agg] | (AGG_ACCUMULATE if accumulate else 0), act, float(slope), _ptr(S), _ld(S, H),
+            _ptr(mask_out), _ptr(partial), _stream(S.device))
     _check(rc, lib)
 
 

@@ -7,36 +7,50 @@ backend ``nccl``):
 * **Partition.** Destination rows [0, V) are cut into ``world`` contiguous ranges holding
   ≈E/world in-edges each (prefix sum of in-degree).  Rank p owns rows [r_p, r_{p+1}): their
   features X, Q, S, Y, the in-edges into them (so S needs no reduction) and dX.
-* **Halo layout.** A message u→v needs K[u].  Rank p's *halo* is the set of remote sources
-  of its in-edges, sorted by global id (hence grouped by owner rank).  K lives in one buffer
-  ``K_ext = [own rows | halo rows]`` and the edge columns are remapped once, at plan time, to
-  positions in it, so the single-GPU kernels run unchanged on ``K_ext``.
-* **Forward exchange: one sparse all-to-all.**  Each rank projects K for its own rows, packs
-  the rows each peer needs (``send_idx``) and one ``all_to_all_single`` (RCCL alltoallv over
-  the xGMI mesh) fills every rank's halo.  On the power-law S2 graph at 8 ranks this moves
-  1.15 M rows per rank instead of the 1.77 M a dense all-gather moves (35% less), and at every
-  world size only rows somebody reads.  It runs on RCCL's stream, overlapped with the Q GEMM.
-* **Backward exchange: the transpose.**  The dK pass runs over the rank's local edges grouped
-  by source (own + halo rows) and yields partial dK for own and halo sources; the halo part
-  goes back to the owners by the reverse all-to-all (overlapped with the dQ pass and the
-  independent GEMMs) and is added in ascending peer order — deterministic.
+* **Halo layout.** A message u→v needs K[u].  Rank p's *halo* is the set of remote sources of its
+  in-edges.  Each owner's block of it (the rows rank p requests from that owner, ascending id) is cut
+  into ``chunks`` equal parts, and the halo is stored CHUNK-MAJOR: ``K_ext = [own rows | chunk 0 |
+  chunk 1 | ...]``, each chunk holding its part of every owner's block in owner order.  Edge
+  columns are remapped once, at plan time, to positions in ``K_ext``, so the single-GPU kernels run
+  on it unchanged.
+* **Forward: a pipelined exchange.**  K is projected for the own rows, and the halo arrives as
+  ``chunks`` sparse all-to-alls (RCCL alltoallv over the xGMI mesh: every chunk moves 1/chunks of
+  the rows of EVERY peer, so each one uses all links at once), all queued at once on RCCL's stream.
+  The edges of each destination row are stored in segments by source — own sources first, then the
+  edges whose halo row is in chunk 0, 1, ... — and the edge pass runs segment by segment: the own
+  segment (under the Q GEMM and the first chunk), then segment c+1 as soon as chunk c has landed
+  (``SIR_AGG_ACCUMULATE``: S[v] += the segment's sum).  Every row sums its segments in the same
+  fixed order, so the result is deterministic (not bit-identical to one GPU, whose rows sum in edge
+  id order: tests hold it to the parity bar).  On the power-law S2 graph the halo is 1.15 M rows per
+  rank at 8 ranks against the 1.77 M a dense all-gather moves.
+* **Backward: the transpose, also pipelined.**  The dK pass runs first over the HALO rows of
+  ``K_ext``, chunk by chunk, each chunk's partial dK sent back to its owners (reverse alltoallv) as
+  soon as it is computed; the dQ pass and the dK pass over the own rows (one launch, as on one GPU),
+  the dW_R / dX_Q / dW_Q GEMMs then run under the exchange.  Received rows are added per chunk and
+  peer in a fixed order (deterministic; no reduce-scatter of a dense [V, H] buffer).
 * **Weight gradients**: one all-reduce of a flat buffer (``allreduce_grads``).
-* **Backward edge passes**: in sign-mask mode ONE launch (dQ waves beside dK waves, as on one GPU;
-  MEAN on G / deg); the halo dK exchange follows it, under the independent GEMMs.
+* **Feature dropout** (``conv.py:35,60-61``, training with p > 0): Q and K draw hashed masks from
+  two device seeds in the GEMM epilogues.  The backward edge passes run without it and the owner
+  applies the masks to its own dQ / dK rows once complete (``sir_dropout_apply``): a halo row's dK
+  partial is summed over ranks before the mask of its owner can apply.
 * **Autocast** (``DistSIRConvFunction16``): 16-bit K_ext rows, edge passes and both exchanges in
   the 16-bit type — half the wire bytes.
-* ``sym`` needs GLOBAL out-degrees: own-row out-degree histograms are completed by the same
-  reverse exchange and forwarded to the halos (plan time, once).
+* ``sym`` needs GLOBAL out-degrees: own-row out-degree histograms are completed by the same reverse
+  exchange and forwarded to the halos (plan time, once).
 
 The per-rank edge work uses the same kernels/ABI as one GPU (``_native``).  A different
 ``backend`` object with the same three edge functions can be injected (the CPU gloo tests do).
 """
+import dataclasses
+
 import torch
 import torch.distributed as dist
 
 from . import _native, linalg
 from .conv import EdgeAggregate, _slots, _tn, _weight_and_bias_grad, _weight_and_bias_grad16, activation_code
 from .graph import DEFAULT_CHUNK, build_plans_native, build_row_csr
+
+DEFAULT_EXCHANGE_CHUNKS = 4
 
 
 def _host_staged(group, t):
@@ -82,111 +96,225 @@ def partition_rows(in_deg, world):
     return bounds
 
 
+def _range_items(rows, begin, end, chunk):
+    """Work items {row, e_begin, e_end, slot} over explicit edge ranges [begin, end) of ``rows``
+    (ascending), ranges longer than ``chunk`` split into slotted items, and their splits {row,
+    slot_begin, n_slots, degree} — ``graph.plan_from_rowptr`` for one segment of every row."""
+    dev = rows.device
+    deg = end - begin
+    nch = torch.clamp((deg + chunk - 1) // chunk, min=1)
+    n_items = int(nch.sum().item()) if rows.numel() else 0
+    idx = torch.repeat_interleave(torch.arange(rows.numel(), device=dev), nch)
+    first = torch.cumsum(nch, 0) - nch
+    k = torch.arange(n_items, device=dev) - first[idx]
+    eb = begin[idx] + k * chunk
+    ee = torch.minimum(eb + chunk, end[idx])
+    split_row = nch > 1
+    split_item = split_row[idx]
+    slot = torch.full((n_items,), -1, dtype=torch.int64, device=dev)
+    n_slots = int(split_item.sum().item()) if n_items else 0
+    if n_slots:
+        slot[split_item] = torch.arange(n_slots, device=dev)
+    items = torch.stack([rows[idx], eb, ee, slot], 1).to(torch.int32).contiguous()
+    srow = torch.nonzero(split_row).flatten()
+    splits = None
+    if srow.numel():
+        s_n = nch[srow]
+        s_begin = torch.cumsum(s_n, 0) - s_n
+        splits = torch.stack([rows[srow], s_begin, s_n, deg[srow]], 1).to(torch.int32).contiguous()
+    return items, splits, n_items, int(srow.numel()), n_slots
+
+
+def _row_slice(csr, r0, r1):
+    """The work items (and split rows) of rows [r0, r1) of a plan: a view of ``csr`` (items and
+    splits are sorted by row; slots keep their global numbering, so the full partial buffer serves)."""
+    it = csr.items[:, 0].contiguous()
+    bnd = torch.tensor([r0, r1], dtype=it.dtype, device=it.device)
+    a, b = (int(x) for x in torch.searchsorted(it, bnd).tolist())
+    sp, ns = None, 0
+    if csr.n_splits:
+        sr = csr.splits[:, 0].contiguous()
+        c, d = (int(x) for x in torch.searchsorted(sr, bnd.to(sr.dtype)).tolist())
+        if d > c:
+            sp, ns = csr.splits[c:d], d - c
+    return dataclasses.replace(csr, items=csr.items[a:b], n_items=b - a, splits=sp, n_splits=ns)
+
+
 class DistGraph:
-    """One rank's share of a dst-range edge-cut, its halo exchange plan and kernel plans.
+    """One rank's share of a dst-range edge-cut, its chunked halo exchange plan and kernel plans.
 
     ``src``/``dst`` may be the global edge list or any superset of this rank's in-edges; edges
     whose destination is outside [row_begin, row_end) are ignored.  Collective at construction
-    (every rank of ``group`` must build its DistGraph together).
+    (every rank of ``group`` must build its DistGraph together, with the same ``chunks``).
 
-    Kernel-facing attributes: ``dst`` (RowCSR over own rows, col = K_ext positions), ``src``
-    (RowCSR over K_ext rows, col = own rows, ``perm`` into ``dst``), ``norms(agg)``.
-    Exchange plan: ``recv_splits`` (halo rows per owner), ``send_splits`` / ``send_idx`` (own
-    rows each peer reads, in the peer's halo order)."""
+    Kernel-facing attributes: ``dst`` (RowCSR over own rows, col = K_ext positions; each row's
+    edges in segment order), ``src`` (RowCSR over K_ext rows, col = own rows, ``perm`` into
+    ``dst``), ``segments`` (the forward's per-segment views of ``dst``), ``src_halo`` / ``src_own``
+    (the dK pass's per-chunk / own-row views of ``src``), ``norms(agg)``.
+    Exchange plan, per chunk c: ``recv_splits[c]`` (halo rows per owner), ``send_splits[c]`` /
+    ``send_idx[c]`` (own rows each peer reads, in the peer's halo order), ``halo_off[c]``."""
 
     def __init__(self, src, dst, num_nodes, bounds, rank, world, device, chunk=DEFAULT_CHUNK,
-                 group=None):
+                 group=None, chunks=None):
         self.num_nodes, self.rank, self.world = int(num_nodes), rank, world
         self.device = torch.device(device)
         self.bounds = list(bounds)
         self.row_begin, self.row_end = bounds[rank], bounds[rank + 1]
-        self.n_rows = self.row_end - self.row_begin
+        self.n_rows = n = self.row_end - self.row_begin
         self.group = group
+        C = (DEFAULT_EXCHANGE_CHUNKS if chunks is None else int(chunks)) if world > 1 else 0
+        self.chunks = C
         dev = self.device
         src = torch.as_tensor(src, dtype=torch.int64).to(dev)
         dst = torch.as_tensor(dst, dtype=torch.int64).to(dev)
         sel = (dst >= self.row_begin) & (dst < self.row_end)
         lsrc, ldst = src[sel], dst[sel] - self.row_begin          # edge-id order preserved
-        self.num_local_edges = int(lsrc.numel())
+        self.num_local_edges = E = int(lsrc.numel())
         local = (lsrc >= self.row_begin) & (lsrc < self.row_end)
         halo = torch.unique(lsrc[~local])                          # sorted -> grouped by owner
-        self.halo_ids = halo
         self.n_halo = int(halo.numel())
-        self.n_ext = self.n_rows + self.n_halo
+        self.n_ext = n + self.n_halo
         bt = torch.tensor(self.bounds, dtype=torch.int64, device=dev)
         owner = torch.searchsorted(bt, halo, right=True) - 1
-        self.recv_splits = torch.bincount(owner, minlength=world).cpu().tolist() if self.n_halo else [0] * world
-        col = torch.where(local, lsrc - self.row_begin,
-                          self.n_rows + torch.searchsorted(halo, lsrc).clamp_(max=max(self.n_halo - 1, 0)))
-        # ---- who reads my rows: exchange halo requests (plan time) ----
-        if world > 1:
-            rc = torch.tensor(self.recv_splits, dtype=torch.int64, device=dev)
-            sc = torch.empty_like(rc)
-            all_to_all_rows(sc, rc, [1] * world, [1] * world, group=group)
-            self.send_splits = sc.cpu().tolist()
-            req = torch.empty(sum(self.send_splits), dtype=torch.int64, device=dev)
-            all_to_all_rows(req, halo.contiguous(), self.send_splits, self.recv_splits, group=group)
-            self.send_idx = (req - self.row_begin).contiguous()
+        # ---- chunk-major halo order: chunk c of owner q = positions [c L_q / C, (c+1) L_q / C) ----
+        if self.n_halo:
+            cnt = torch.bincount(owner, minlength=world)
+            start = torch.cumsum(cnt, 0) - cnt
+            pos = torch.arange(self.n_halo, device=dev) - start[owner]
+            hchunk = (pos * C) // cnt[owner]
+            key = hchunk * world + owner
+            order = torch.argsort(key, stable=True)
+            new_pos = torch.empty_like(order)
+            new_pos[order] = torch.arange(self.n_halo, device=dev)
+            rs = torch.bincount(key, minlength=C * world).view(C, world).cpu().tolist()
+            self.halo_ids = halo[order]
         else:
-            self.send_splits = [0] * world
-            self.send_idx = torch.zeros(0, dtype=torch.int64, device=dev)
-        if self.send_idx.numel():
-            lo, hi = int(self.send_idx.min()), int(self.send_idx.max())
-            if lo < 0 or hi >= self.n_rows:
-                raise RuntimeError(f"rank {rank}: peers requested rows outside [0, {self.n_rows})")
-        self._send_parts = list(torch.split(self.send_idx, self.send_splits))
+            rs = [[0] * world for _ in range(C)]
+            self.halo_ids = halo
+        self.recv_splits = rs
+        off = [0]
+        for c in range(C):
+            off.append(off[-1] + sum(rs[c]))
+        self.halo_off = off
+        # ---- who reads my rows: exchange the requests once, split them by the same rule ----
+        self.send_splits = [[0] * world for _ in range(C)]
+        self.send_idx = [torch.zeros(0, dtype=torch.int64, device=dev) for _ in range(C)]
+        if world > 1:
+            req_cnt = torch.bincount(owner, minlength=world)
+            sc_t = torch.empty_like(req_cnt)
+            all_to_all_rows(sc_t, req_cnt, [1] * world, [1] * world, group=group)
+            sc = sc_t.cpu().tolist()
+            req = torch.empty(sum(sc), dtype=torch.int64, device=dev)
+            all_to_all_rows(req, halo.contiguous(), sc, req_cnt.cpu().tolist(), group=group)
+            parts = list(torch.split(req, sc))
+            for c in range(C):
+                idx_c = []
+                for q in range(world):
+                    L = sc[q]
+                    a, b = -(-c * L // C), -(-(c + 1) * L // C)   # positions with (pos * C) // L == c
+                    self.send_splits[c][q] = b - a
+                    idx_c.append(parts[q][a:b] - self.row_begin)
+                self.send_idx[c] = torch.cat(idx_c).contiguous()
+            allidx = torch.cat(self.send_idx)
+            if allidx.numel():
+                lo, hi = int(allidx.min()), int(allidx.max())
+                if lo < 0 or hi >= n:
+                    raise RuntimeError(f"rank {rank}: peers requested rows outside [0, {n})")
+        self._send_parts = [list(torch.split(self.send_idx[c], self.send_splits[c])) for c in range(C)]
+        # the backward's received dK partials, one buffer after dK_ext: chunk c at recv_off[c]; the own
+        # rows' complete dK is ONE segment sum over [own partial, chunk 0 peers 0.., chunk 1 ...] per row
+        # (a gather: no atomics, fixed order) — recv_plan rows = own rows, col = row positions in
+        # [dK_ext | received]
+        roff = [0]
+        for c in range(C):
+            roff.append(roff[-1] + int(self.send_idx[c].numel()))
+        self.recv_off = roff
+        tgt = torch.cat([torch.arange(n, device=dev)] + [t for t in self.send_idx])
+        pos = torch.cat([torch.arange(n, device=dev), self.n_ext + torch.arange(roff[-1], device=dev)])
+        self.recv_plan = build_row_csr(tgt, pos, n, chunk)
+        # ---- edge columns in K_ext, segments (0: own source, 1 + c: halo chunk c) ----
+        if self.n_halo:
+            hp = torch.searchsorted(halo, lsrc).clamp_(max=self.n_halo - 1)
+            col = torch.where(local, lsrc - self.row_begin, n + new_pos[hp])
+            seg = torch.where(local, torch.zeros_like(lsrc), 1 + hchunk[hp])
+        else:
+            col = lsrc - self.row_begin
+            seg = torch.zeros_like(lsrc)
+        NS = C + 1
+        so = torch.argsort(seg, stable=True)     # the row sort below keeps (segment, edge id) order inside a row
+        col, ldst, seg = col[so], ldst[so], seg[so]
         # ---- kernel plans over the K_ext layout ----
         if dev.type == "cuda":
-            self.dst, self.src = build_plans_native(col, ldst, self.n_rows, self.n_ext, chunk)
+            self.dst, self.src = build_plans_native(col, ldst, n, self.n_ext, chunk)
         else:
-            self.dst = build_row_csr(ldst, col, self.n_rows, chunk)
+            self.dst = build_row_csr(ldst, col, n, chunk)
             self.src = build_row_csr(col, ldst, self.n_ext, chunk)
-            E = self.num_local_edges
             pos_in_dst = torch.empty(E, dtype=torch.int64, device=dev)
             pos_in_dst[self.dst.eid] = torch.arange(E, device=dev)
             self.src.perm = pos_in_dst[self.src.eid].to(torch.int32).contiguous()
+        # forward segments: per (row, segment) edge ranges of the dst CSR
+        cnt_rs = torch.bincount(ldst * NS + seg, minlength=n * NS)[:n * NS].view(n, NS)
+        rp = self.dst.rowptr[:-1].to(torch.int64)
+        ends = rp[:, None] + torch.cumsum(cnt_rs, 1)
+        begins = ends - cnt_rs
+        self.segments = []
+        for s in range(NS):
+            r = torch.arange(n, device=dev) if s == 0 else torch.nonzero(cnt_rs[:, s]).flatten()
+            it, sp, ni, ns, nsl = _range_items(r, begins[r, s], ends[r, s], chunk)
+            self.segments.append(dataclasses.replace(self.dst, items=it, n_items=ni, splits=sp, n_splits=ns,
+                                                     n_slots=nsl))
+        self.src_own = _row_slice(self.src, 0, n)
+        self.src_halo = [_row_slice(self.src, n + off[c], n + off[c + 1]) for c in range(C)]
         self.in_deg = (self.dst.rowptr[1:] - self.dst.rowptr[:-1]).to(torch.int64)
         self.local_out_deg = (self.src.rowptr[1:] - self.src.rowptr[:-1]).to(torch.int64)
         self._out_deg = None
         self._norms = {}
-        self._deg_f = None       # fp32 in-degree of own rows (the one-launch MEAN backward)
+        self._deg_f = None       # fp32 in-degree of own rows (MEAN)
 
     @classmethod
-    def from_global(cls, src, dst, num_nodes, rank, world, device, chunk=DEFAULT_CHUNK, group=None):
+    def from_global(cls, src, dst, num_nodes, rank, world, device, chunk=DEFAULT_CHUNK, group=None, chunks=None):
         in_deg = torch.bincount(torch.as_tensor(dst, dtype=torch.int64), minlength=num_nodes)
-        return cls(src, dst, num_nodes, partition_rows(in_deg, world), rank, world, device, chunk, group)
+        return cls(src, dst, num_nodes, partition_rows(in_deg, world), rank, world, device, chunk, group, chunks)
 
-    # ---- exchanges (rows of [n, F] tensors) ----
-    def gather_halo(self, own, halo_out, async_op=False):
-        """halo_out[i] ← owner's own[...] row of halo node i (forward all-to-all)."""
-        if self.world == 1:
-            return None
-        send = own.index_select(0, self.send_idx)
-        return all_to_all_rows(halo_out, send, self.recv_splits, self.send_splits, self.group, async_op)
+    # ---- exchanges (rows of [n, F] tensors), one chunk at a time ----
+    def halo_rows(self, c):
+        """K_ext row range of halo chunk c."""
+        return self.n_rows + self.halo_off[c], self.n_rows + self.halo_off[c + 1]
 
-    def scatter_halo(self, halo_in, recv_out, async_op=False):
-        """Reverse all-to-all: recv_out (send_idx order) ← peers' halo rows of my nodes."""
-        if self.world == 1:
-            return None
-        return all_to_all_rows(recv_out, halo_in.contiguous(), self.send_splits, self.recv_splits, self.group,
+    def gather_chunk(self, c, own, ext, async_op=False):
+        """ext[halo chunk c] ← the owners' rows of ``own`` (forward alltoallv)."""
+        a, b = self.halo_rows(c)
+        send = own.index_select(0, self.send_idx[c])
+        return all_to_all_rows(ext[a:b], send, self.recv_splits[c], self.send_splits[c], self.group, async_op)
+
+    def scatter_chunk(self, c, ext, recv, async_op=False):
+        """Reverse alltoallv of chunk c: recv (send_idx[c] order) ← the peers' halo rows of my nodes."""
+        a, b = self.halo_rows(c)
+        return all_to_all_rows(recv, ext[a:b].contiguous(), self.send_splits[c], self.recv_splits[c], self.group,
                                async_op)
 
-    def add_received(self, own, recv):
-        """own[send_idx[q]] += recv[q] for peers q in ascending order (deterministic: indices are
+    def add_received(self, c, own, recv):
+        """own[send_idx[c][q]] += recv rows of peer q, peers in ascending order (deterministic: indices are
         unique within one peer's slice)."""
-        for idx, part in zip(self._send_parts, torch.split(recv, self.send_splits)):
+        for idx, part in zip(self._send_parts[c], torch.split(recv, self.send_splits[c])):
             if idx.numel():
                 own.index_add_(0, idx, part)
+
+    def gather_halo(self, own, ext):
+        """ext[n:] ← the owners' rows of ``own``, every chunk (synchronous)."""
+        for c in range(self.chunks):
+            self.gather_chunk(c, own, ext)
 
     def out_deg(self):
         """GLOBAL out-degree of every K_ext row (own + halo)."""
         if self._out_deg is None:
             deg = self.local_out_deg.clone()
-            if self.world > 1:
-                recv = torch.empty(self.send_idx.numel(), dtype=torch.int64, device=self.device)
-                self.scatter_halo(deg[self.n_rows:], recv)
-                self.add_received(deg[:self.n_rows], recv)
-                self.gather_halo(deg[:self.n_rows], deg[self.n_rows:])
+            n = self.n_rows
+            for c in range(self.chunks):
+                recv = torch.empty(self.send_idx[c].numel(), dtype=torch.int64, device=self.device)
+                self.scatter_chunk(c, deg, recv)
+                self.add_received(c, deg[:n], recv)
+            self.gather_halo(deg[:n], deg)
             self._out_deg = deg
         return self._out_deg
 
@@ -209,92 +337,140 @@ class DistGraph:
             self._norms["sym"] = (in_norm, out_norm)
         return self._norms["sym"]
 
+    def deg_f(self):
+        """fp32 max(in-degree, 1) of the own rows, [n, 1] (MEAN)."""
+        if self._deg_f is None:
+            self._deg_f = self.in_deg.clamp(min=1).to(torch.float32)[:, None]
+        return self._deg_f
+
     def exchange_rows(self):
         """Rows this rank receives / sends per forward exchange (for reporting)."""
-        return self.n_halo, int(self.send_idx.numel())
+        return self.n_halo, int(sum(int(t.numel()) for t in self.send_idx))
 
 
 def _workspace(plan, H, device):
-    n = max(plan.dst.n_slots, plan.src.n_slots)
+    n = max(plan.dst.n_slots, plan.src.n_slots, *(s.n_slots for s in plan.segments))
     return torch.empty((max(n, 1) * H,), device=device, dtype=torch.float32) if n else None
 
 
-def _edge_backward_exchange(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recv):
-    """dQ (own rows) and dK_ext (own + halo sources) of the local edges, then the reverse
-    all-to-all of the halo dK rows into ``recv`` — started asynchronously and returned, so the
-    caller's independent GEMMs run under it.
-
-    Sign-mask mode on the native backend: both passes in ONE launch (``sir_edge_agg_bwd``, the
-    single-GPU layer's backward; MEAN on G / deg formed first — every in-edge of an own row is
-    local, so deg is the local CSR's), the exchange after it.  Recompute mode (other backends,
-    sigma without a mask): the dK pass first (MEAN: after the dQ pass, which writes G / deg) and
-    the dQ pass under the exchange."""
+def _segmented_forward(backend, dg, Q, K_ext, agg, act, slope, S, mask, works):
+    """S = update_all(...) over the rank's in-edges, segment by segment as the halo chunks land:
+    the own segment writes every row, halo segment c + 1 adds its sum after waiting for chunk c
+    (``works[c]``; None: already complete).  MEAN divides once, after the last segment."""
     in_norm, out_norm = dg.norms(agg)
-    n = dg.n_rows
-    if mask is not None and backend is _native and EdgeAggregate.dual:
-        if agg == "mean":
-            if dg._deg_f is None:
-                rp = dg.dst.rowptr
-                dg._deg_f = (rp[1:] - rp[:-1]).clamp(min=1).to(torch.float32)[:, None]
-            G = torch.div(G, dg._deg_f, out=torch.empty_like(G))   # fp32 math, one rounding to G's dtype
-            agg = "sum"
-        _native.edge_agg_bwd(dg.dst, dg.src, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK_ext,
-                             _slots(dg.dst, H, G.device), _slots(dg.src, H, G.device))
-        return dg.scatter_halo(dK_ext[n:], recv, async_op=True)
+    a = "sum" if agg == "mean" else agg
+    partial = _workspace(dg, Q.shape[1], Q.device)
+    for s, seg in enumerate(dg.segments):
+        if s > 0 and works[s - 1] is not None:
+            works[s - 1].wait()
+        backend.edge_agg_fwd(seg, Q, K_ext, in_norm, out_norm, a, act, slope, S, partial, mask, accumulate=s > 0)
+    if agg == "mean":
+        S.copy_(S / dg.deg_f())      # fp32 division, one rounding to S's dtype (DGL fn.mean)
+
+
+def _chunked_backward(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recvs):
+    """dK over the halo rows chunk by chunk, each chunk's rows sent back to their owners as soon as
+    they are complete (returns the pending works), then dQ and the own rows' dK — in one launch in
+    sign-mask mode on the native backend — under the exchange.  MEAN runs on G / deg (both passes
+    read exactly those values, as the single-GPU layer does)."""
+    in_norm, out_norm = dg.norms(agg)
+    if agg == "mean":
+        G = (G / dg.deg_f()).to(G.dtype)
+        agg = "sum"
     partial = _workspace(dg, H, G.device)
-    Gm = None
-    if agg == "mean":     # the dK pass reads G / deg, written by the dQ pass
-        Gm = torch.empty((n, H), device=G.device, dtype=G.dtype)
-        backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, Gm, partial, mask)
-    backend.edge_agg_bwd_src(dg.src, K_ext, Q, Gm if Gm is not None else G, out_norm, in_norm,
-                             agg, act, slope, dK_ext, partial, mask)
-    work = dg.scatter_halo(dK_ext[n:], recv, async_op=True)
-    if agg != "mean":     # overlaps the reverse exchange
+    partial_s = _slots(dg.src, H, G.device)
+    works = []
+    for c in range(dg.chunks):
+        backend.edge_agg_bwd_src(dg.src_halo[c], K_ext, Q, G, out_norm, in_norm, agg, act, slope, dK_ext,
+                                 partial_s, mask)
+        works.append(dg.scatter_chunk(c, dK_ext, recvs[c], async_op=True))
+    if mask is not None and backend is _native and EdgeAggregate.dual:
+        _native.edge_agg_bwd(dg.dst, dg.src_own, G, mask, in_norm, out_norm, agg, act, slope, dQ, dK_ext,
+                             partial, partial_s)
+    else:
         backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, None, partial, mask)
-    return work
+        backend.edge_agg_bwd_src(dg.src_own, K_ext, Q, G, out_norm, in_norm, agg, act, slope, dK_ext, partial_s,
+                                 mask)
+    return works
+
+
+def _backward_buffers(dg, H, dev, dtype):
+    """dK_ext and the chunks' receive buffers as slices of ONE buffer [n_ext + received rows, H]."""
+    big = torch.empty((dg.n_ext + dg.recv_off[-1], H), device=dev, dtype=dtype)
+    recvs = [big[dg.n_ext + dg.recv_off[c]:dg.n_ext + dg.recv_off[c + 1]] for c in range(dg.chunks)]
+    return big, big[:dg.n_ext], recvs
+
+
+def _complete_dk(dg, big, recvs, works, backend):
+    """dK of the own rows = own partial + every peer's halo partial, in a fixed order (own, then chunk by
+    chunk, peers ascending): one native segment sum gathering the rows of ``big`` (fp32), else per chunk
+    and peer index_add (unique indices per call: deterministic)."""
+    for c in range(dg.chunks):
+        if works[c] is not None:
+            works[c].wait()
+    n = dg.n_rows
+    if backend is _native and big.dtype == torch.float32 and dg.chunks:
+        dK = torch.empty((n, big.shape[1]), device=big.device, dtype=big.dtype)
+        rp = dg.recv_plan
+        part = torch.empty((rp.n_slots * big.shape[1],), device=big.device) if rp.n_slots else None
+        _native.segment_sum(rp, big, dK, perm=rp.col, partial=part)
+        return dK
+    dK = big[:n]
+    for c in range(dg.chunks):
+        dg.add_received(c, dK, recvs[c])
+    return dK
+
+
+def _drops(drop):
+    """(Q drop, K drop) of a (seeds, p) pair: two independent device seeds (or ints)."""
+    if drop is None:
+        return None, None
+    seeds, p = drop
+    if isinstance(seeds, torch.Tensor):
+        return (seeds[0:1], p), (seeds[1:2], p)
+    return (int(seeds), p), ((int(seeds) * 0x9E3779B97F4A7C15 + 1) % (1 << 62), p)
 
 
 class DistSIRConvFunction(torch.autograd.Function):
-    """One rank's share of the whole layer, hand-scheduled around the two exchanges.
+    """One rank's share of the whole layer, hand-scheduled around the two pipelined exchanges.
 
-    forward : K_own = X W_K^T -> all-to-all(halo K) ‖ Q = X W_Q^T + b_Q -> S (edge kernels over
-              K_ext) -> Y = S W_R^T + b_R
-    backward: G = dY W_R -> dK pass (own + halo sources) -> reverse all-to-all of halo dK ‖
-              dQ pass, dW_R, db_R, dX = dQ W_Q, dW_Q, db_Q -> dK_own += received ->
-              dX += dK W_K, dW_K.  Weight gradients are this rank's partial sums."""
+    forward : K_own = X W_K^T -> ``chunks`` halo alltoallvs queued ‖ Q = X W_Q^T + b_Q, own-source
+              segment -> halo segments as their chunks land -> Y = S W_R^T + b_R
+    backward: G = dY W_R -> dK of halo chunk c -> its reverse alltoallv (each as soon as computed) ‖
+              dQ pass + own-row dK, dW_R, db_R, dX = dQ W_Q, dW_Q, db_Q -> dK_own += received ->
+              dX += dK W_K, dW_K.  Weight gradients are this rank's partial sums.
+    ``drop``: (two device seeds, p) of the Q / K feature dropout (conv.py:60-61), or None."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on=True):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on=True, drop=None):
         H = W_Q.shape[0]
         n = dg.n_rows
         dev = X.device
         X = X.contiguous()
+        dq, dk = _drops(drop)
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
-        linalg.mm_wt(X, W_K, out=K_ext[:n])
-        work = dg.gather_halo(K_ext[:n], K_ext[n:], async_op=True)
-        Q = linalg.mm_wt(X, W_Q, b_Q)
-        if work is not None:
-            work.wait()
-        in_norm, out_norm = dg.norms(agg)
+        linalg.mm_wt(X, W_K, out=K_ext[:n], drop=dk)
+        works = [dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True) for c in range(dg.chunks)]
+        Q = linalg.mm_wt(X, W_Q, b_Q, drop=dq)
         S = torch.empty((n, H), device=dev, dtype=torch.float32)
-        partial = _workspace(dg, H, dev)
         training = grad_on and any(ctx.needs_input_grad[:6])     # grad mode passed in (see conv.py)
         nw = _native.mask_words(H, act) if (use_mask and training and backend is _native) else 0
         mask = torch.empty((max(dg.dst.col.numel(), 1) * nw,), device=dev, dtype=torch.int64) if nw else None
-        backend.edge_agg_fwd(dg.dst, Q, K_ext, in_norm, out_norm, agg, act, slope, S, partial, mask)
+        _segmented_forward(backend, dg, Q, K_ext, agg, act, slope, S, mask, works)
         Y = linalg.mm_wt(S, W_R, b_R)
         if mask is not None:
             ctx.save_for_backward(X, W_Q, W_K, W_R, S, mask)
         else:
             ctx.save_for_backward(X, W_Q, W_K, W_R, S, Q, K_ext)
         ctx.masked = mask is not None
-        ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend = dg, agg, act, slope, backend
+        ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend, ctx.drop = dg, agg, act, slope, backend, (dq, dk)
         ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
         return Y
 
     @staticmethod
     def backward(ctx, dY):
         dg, agg, act, slope, backend = ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend
+        dq, dk = ctx.drop
         if ctx.masked:
             X, W_Q, W_K, W_R, S, mask = ctx.saved_tensors
             Q = K_ext = None
@@ -307,62 +483,58 @@ class DistSIRConvFunction(torch.autograd.Function):
         dY = dY.contiguous()
         G = linalg.mm_w(dY, W_R)
         dQ = torch.empty((n, H), device=dev, dtype=torch.float32)
-        dK_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
-        recv = torch.empty((dg.send_idx.numel(), H), device=dev, dtype=torch.float32)
-        work = _edge_backward_exchange(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recv)
+        big, dK_ext, recvs = _backward_buffers(dg, H, dev, torch.float32)
+        works = _chunked_backward(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recvs)
+        if dq is not None:
+            _native.dropout_apply(dQ, dq)
         dW_R, db_R = _weight_and_bias_grad(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
         dX = linalg.mm_w(dQ, W_Q) if ctx.needs_input_grad[0] else None
         dW_Q, db_Q = _weight_and_bias_grad(dQ, X, ctx.needs_input_grad[1], ctx.has_bq and ctx.needs_input_grad[2])
-        if work is not None:
-            work.wait()
-        dK = dK_ext[:n]
-        if dg.world > 1:
-            dg.add_received(dK, recv)
+        dK = _complete_dk(dg, big, recvs, works, backend)
+        if dk is not None:
+            _native.dropout_apply(dK, dk)
         if dX is not None:
             dX += linalg.mm_w(dK, W_K)
         dW_K = _tn(dK, X) if ctx.needs_input_grad[3] else None
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None
 
 
 class DistSIRConvFunction16(torch.autograd.Function):
     """:class:`DistSIRConvFunction` under autocast (bf16 / fp16 ``dt``, the reference's AMP path):
     the single-GPU ``SIRConvFunction16`` dataflow per rank — 16-bit projections on the native
     16-bit MFMA GEMMs (X.to(dt) fused into the first one), 16-bit ``K_ext`` rows and edge passes
-    (fp32 math inside) — with both halo exchanges in the 16-bit storage type: half the xGMI bytes
-    of the fp32 layer.  The received dK rows are added in that type (one more rounding per peer
-    than the single-GPU sum; within the AMP tolerance)."""
+    (fp32 math inside) — with both pipelined halo exchanges in the 16-bit storage type: half the
+    xGMI bytes of the fp32 layer.  The received dK rows are added in that type (one more rounding
+    per peer than the single-GPU sum; within the AMP tolerance)."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on, dt):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on, dt, drop=None):
         H = W_Q.shape[0]
         n = dg.n_rows
         dev = X.device
         X = X.contiguous()
+        dq, dk = _drops(drop)
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=dt)
         if X.dtype == dt:
             Xh = X
-            linalg.mm16_wt(X, W_K, None, dt, out=K_ext[:n])
+            linalg.mm16_wt(X, W_K, None, dt, out=K_ext[:n], drop=dk)
         else:       # X.to(dt) fused into the K GEMM's loads; the rounded X (for dW) written by it
             Xh = torch.empty(X.shape, dtype=dt, device=dev)
-            linalg.mm16_wt(X, W_K, None, dt, acopy=Xh, out=K_ext[:n])
-        work = dg.gather_halo(K_ext[:n], K_ext[n:], async_op=True)
-        Q = linalg.mm16_wt(Xh, W_Q, b_Q, dt)
-        if work is not None:
-            work.wait()
-        in_norm, out_norm = dg.norms(agg)
+            linalg.mm16_wt(X, W_K, None, dt, acopy=Xh, out=K_ext[:n], drop=dk)
+        works = [dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True) for c in range(dg.chunks)]
+        Q = linalg.mm16_wt(Xh, W_Q, b_Q, dt, drop=dq)
         S = torch.empty((n, H), device=dev, dtype=dt)
-        partial = _workspace(dg, H, dev)
         training = grad_on and any(ctx.needs_input_grad[:6])
         nw = _native.mask_words(H, act) if (use_mask and training and backend is _native) else 0
         mask = torch.empty((max(dg.dst.col.numel(), 1) * nw,), device=dev, dtype=torch.int64) if nw else None
-        backend.edge_agg_fwd(dg.dst, Q, K_ext, in_norm, out_norm, agg, act, slope, S, partial, mask)
+        _segmented_forward(backend, dg, Q, K_ext, agg, act, slope, S, mask, works)
         Y = linalg.mm16_wt(S, W_R, b_R, dt)
         if mask is not None:
             ctx.save_for_backward(Xh, W_Q, W_K, W_R, S, mask)
         else:
             ctx.save_for_backward(Xh, W_Q, W_K, W_R, S, Q, K_ext)
         ctx.masked = mask is not None
-        ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend = dg, agg, act, slope, backend
+        ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend, ctx.drop = dg, agg, act, slope, backend, (dq, dk)
         ctx.x_dtype, ctx.dt = X.dtype, dt
         ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
         return Y
@@ -370,6 +542,7 @@ class DistSIRConvFunction16(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dY):
         dg, agg, act, slope, backend, dt = ctx.dg, ctx.agg, ctx.act, ctx.slope, ctx.backend, ctx.dt
+        dq, dk = ctx.drop
         if ctx.masked:
             Xh, W_Q, W_K, W_R, S, mask = ctx.saved_tensors
             Q = K_ext = None
@@ -382,9 +555,10 @@ class DistSIRConvFunction16(torch.autograd.Function):
         dY = dY.contiguous().to(dt)
         G = linalg.mm16_w(dY, W_R, dt)
         dQ = torch.empty((n, H), device=dev, dtype=dt)
-        dK_ext = torch.empty((dg.n_ext, H), device=dev, dtype=dt)
-        recv = torch.empty((dg.send_idx.numel(), H), device=dev, dtype=dt)
-        work = _edge_backward_exchange(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recv)
+        big, dK_ext, recvs = _backward_buffers(dg, H, dev, dt)
+        works = _chunked_backward(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recvs)
+        if dq is not None:
+            _native.dropout_apply(dQ, dq)
         dW_R = db_R = None
         if ctx.needs_input_grad[4] or ctx.needs_input_grad[5]:
             dW_R, db_R = _weight_and_bias_grad16(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
@@ -392,21 +566,20 @@ class DistSIRConvFunction16(torch.autograd.Function):
         dW_Q = db_Q = None
         if ctx.needs_input_grad[1] or (ctx.has_bq and ctx.needs_input_grad[2]):
             dW_Q, db_Q = _weight_and_bias_grad16(dQ, Xh, True, ctx.has_bq and ctx.needs_input_grad[2])
-        if work is not None:
-            work.wait()
-        dK = dK_ext[:n]
-        if dg.world > 1:
-            dg.add_received(dK, recv)
+        dK = _complete_dk(dg, big, recvs, works, backend)
+        if dk is not None:
+            _native.dropout_apply(dK, dk)
         if dX is not None:
             dX += linalg.mm16_w(dK, W_K, dt, out_dtype=torch.float32)
             dX = dX.to(ctx.x_dtype)
         dW_K = _weight_and_bias_grad16(dK, Xh, True, False)[0] if ctx.needs_input_grad[3] else None
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None, None
 
 
 class DistEdgeAggregate(torch.autograd.Function):
-    """Modular variant (dropout / autocast): S_local = update_all(...) over the local in-edges
-    from Q (own rows) and K (own rows); the halo exchange runs inside."""
+    """Modular variant (layers the fused Functions do not take: other dtypes, tuple features): S_local
+    = update_all(...) over the local in-edges from Q (own rows) and K (own rows), with the same
+    pipelined exchanges inside."""
 
     @staticmethod
     def forward(ctx, Q, K_local, dg, H, agg, act, slope, backend, use_mask, grad_on=True):
@@ -414,16 +587,14 @@ class DistEdgeAggregate(torch.autograd.Function):
         n = dg.n_rows
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
         K_ext[:n] = K_local
-        dg.gather_halo(K_ext[:n], K_ext[n:])
-        in_norm, out_norm = dg.norms(agg)
+        works = [dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True) for c in range(dg.chunks)]
         S = torch.empty((n, H), device=dev, dtype=torch.float32)
-        partial = _workspace(dg, H, dev)
         nw = _native.mask_words(H, act) if (use_mask and backend is _native) else 0
         mask = None
         if nw and grad_on and (Q.requires_grad or K_local.requires_grad):
             mask = torch.empty((max(dg.dst.col.numel(), 1) * nw,), device=dev, dtype=torch.int64)
         Qc = Q.contiguous().float()
-        backend.edge_agg_fwd(dg.dst, Qc, K_ext, in_norm, out_norm, agg, act, slope, S, partial, mask)
+        _segmented_forward(backend, dg, Qc, K_ext, agg, act, slope, S, mask, works)
         if mask is not None:
             ctx.save_for_backward(mask)
         else:
@@ -436,7 +607,6 @@ class DistEdgeAggregate(torch.autograd.Function):
     def backward(ctx, dS):
         dg, H, agg, act, slope, backend = ctx.dg, ctx.H, ctx.agg, ctx.act, ctx.slope, ctx.backend
         dev = dS.device
-        n = dg.n_rows
         G = dS.contiguous().float()
         if ctx.masked:
             (mask,) = ctx.saved_tensors
@@ -444,19 +614,10 @@ class DistEdgeAggregate(torch.autograd.Function):
         else:
             Q, K_ext = ctx.saved_tensors
             mask = None
-        in_norm, out_norm = dg.norms(agg)
-        partial = _workspace(dg, H, dev)
-        dQ = torch.empty((n, H), device=dev, dtype=torch.float32)
-        Gm = torch.empty((n, H), device=dev, dtype=torch.float32) if agg == "mean" else None
-        backend.edge_agg_bwd_dst(dg.dst, Q, K_ext, G, in_norm, out_norm, agg, act, slope, dQ, Gm, partial, mask)
-        dK_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
-        backend.edge_agg_bwd_src(dg.src, K_ext, Q, Gm if Gm is not None else G, out_norm, in_norm,
-                                 agg, act, slope, dK_ext, partial, mask)
-        dK = dK_ext[:n]
-        if dg.world > 1:
-            recv = torch.empty((dg.send_idx.numel(), H), device=dev, dtype=torch.float32)
-            dg.scatter_halo(dK_ext[n:], recv)
-            dg.add_received(dK, recv)
+        dQ = torch.empty((dg.n_rows, H), device=dev, dtype=torch.float32)
+        big, dK_ext, recvs = _backward_buffers(dg, H, dev, torch.float32)
+        works = _chunked_backward(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recvs)
+        dK = _complete_dk(dg, big, recvs, works, backend)
         return dQ, dK, None, None, None, None, None, None, None, None
 
 
@@ -474,6 +635,16 @@ class DistSIRConv(torch.nn.Module):
         self.backend = backend if backend is not None else _native
         self.use_mask = use_mask
 
+    def _drop(self, device):
+        """(two seeds, p) of this forward's Q / K dropout (conv.py:35,60-61), or None: drawn on the
+        device from torch's CUDA generator (graph-safe), on the host for CPU rehearsals."""
+        c = self.conv
+        if not (c.training and c.dropout.p > 0):
+            return None
+        if device.type != "cuda":
+            return int(torch.randint(0, 2 ** 62, (1,)).item()), float(c.dropout.p)
+        return torch.randint(0, 2 ** 62, (2,), device=device, dtype=torch.int64), float(c.dropout.p)
+
     def forward(self, dgraph, feat):
         c = self.conv
         if c._agg_type not in ("sum", "mean", "sym"):
@@ -483,14 +654,14 @@ class DistSIRConv(torch.nn.Module):
         act, slope = activation_code(c.activation)
         H = c.linear_query.out_features
         fused = (self.use_fused and feat.dtype == torch.float32 and not torch.is_autocast_enabled()
-                 and not (c.training and c.dropout.p > 0) and c.linear_query.weight.dtype == torch.float32)
+                 and c.linear_query.weight.dtype == torch.float32)
         if fused:
             return DistSIRConvFunction.apply(feat, c.linear_query.weight, c.linear_query.bias, c.linear_key.weight,
                                              c.linear_relation.weight, c.linear_relation.bias, dgraph,
                                              c._agg_type, act, slope, self.backend, self.use_mask,
-                                             torch.is_grad_enabled())
+                                             torch.is_grad_enabled(), self._drop(feat.device))
         if (self.use_fused and feat.is_cuda and torch.is_autocast_enabled() and H % 4 == 0
-                and not (c.training and c.dropout.p > 0) and c.linear_query.weight.dtype == torch.float32
+                and c.linear_query.weight.dtype == torch.float32
                 and feat.dtype in (torch.float32, torch.bfloat16, torch.float16)):
             dt = torch.get_autocast_dtype("cuda")
             if dt in (torch.bfloat16, torch.float16):
@@ -498,7 +669,8 @@ class DistSIRConv(torch.nn.Module):
                     return DistSIRConvFunction16.apply(feat, c.linear_query.weight, c.linear_query.bias,
                                                        c.linear_key.weight, c.linear_relation.weight,
                                                        c.linear_relation.bias, dgraph, c._agg_type, act, slope,
-                                                       self.backend, self.use_mask, torch.is_grad_enabled(), dt)
+                                                       self.backend, self.use_mask, torch.is_grad_enabled(), dt,
+                                                       self._drop(feat.device))
         Q = c.dropout(c.linear_query(feat))
         K = c.dropout(c.linear_key(feat))
         S = DistEdgeAggregate.apply(Q, K, dgraph, H, c._agg_type, act, slope, self.backend, self.use_mask,

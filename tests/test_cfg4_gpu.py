@@ -145,11 +145,11 @@ def test_cfg4_S2_layer_deterministic_mask_equals_recompute_and_parity(s2, agg):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("agg", ["sum"])
 def test_cfg4_S2_edge_cut_8_ranks_vs_single_gpu(s2, agg):
-    """The edge-cut layer (sirgcn.dist, the scaling config) on the S2 graph over 8 ranks — one
-    thread per rank on the one GPU (tests/thread_comm.py), every exchange on device tensors —
-    against the single-GPU layer: Y bit-identical (each own row sums its in-edges in the same order,
-    the GEMMs are row-wise); dX and the weight gradients (rank partials summed) per tensor against
-    the fp64 reference on the single-GPU layer's projection values."""
+    """The edge-cut layer (sirgcn.dist, the scaling config: pipelined chunked exchanges, segmented
+    forward) on the S2 graph over 8 ranks — one thread per rank on the one GPU (tests/thread_comm.py),
+    every exchange on device tensors — run twice (bit-identical: fixed segment and peer orders), and
+    Y, dX and the weight gradients (rank partials summed) per tensor against the fp64 reference on the
+    single-GPU layer's projection values (the edge-cut's own QK equals it: the GEMMs are row-wise)."""
     from sirgcn.dist import DistGraph, DistSIRConvFunction, partition_rows
     from thread_comm import FakeCtx, ThreadComm, run_ranks
     g, X, dY = s2
@@ -162,8 +162,12 @@ def test_cfg4_S2_edge_cut_8_ranks_vs_single_gpu(s2, agg):
     comms = ThreadComm.make(world)
     bounds = partition_rows(torch.bincount(dst, minlength=V), world)
 
+    dgs = {}
+
     def fn(r):
-        dg = DistGraph(src, dst, V, bounds, r, world, DEV, group=comms[r])
+        if r not in dgs:
+            dgs[r] = DistGraph(src, dst, V, bounds, r, world, DEV, group=comms[r])
+        dg = dgs[r]
         ctx = FakeCtx((True,) * 6 + (False,) * 7)
         sl = slice(dg.row_begin, dg.row_end)
         with torch.no_grad():
@@ -173,10 +177,12 @@ def test_cfg4_S2_edge_cut_8_ranks_vs_single_gpu(s2, agg):
         return dg.n_halo, Y, grads[:6]
 
     outs = run_ranks(world, fn)
+    again = run_ranks(world, fn)
+    for a, b in zip(outs, again):
+        assert torch.equal(a[1], b[1]) and all(torch.equal(x, y) for x, y in zip(a[2], b[2]) if x is not None)
+    del again
     assert all(o[0] > 0 for o in outs)
-    Y = torch.cat([o[1] for o in outs])
-    assert torch.equal(Y, one["Y"]), "edge-cut Y differs from the single-GPU layer"
-    got = {"dX": torch.cat([o[2][0] for o in outs])}
+    got = {"Y": torch.cat([o[1] for o in outs]), "dX": torch.cat([o[2][0] for o in outs])}
     for i, k in enumerate(("dW_Q", "db_Q", "dW_K", "dW_R", "db_R"), start=1):
         got[k] = sum(o[2][i].double() for o in outs)
     del outs

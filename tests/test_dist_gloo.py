@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, agg, outdir, fused=True):
+def _worker(rank, world, port, agg, outdir, fused=True, chunks=None):
     for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -40,7 +40,7 @@ def _worker(rank, world, port, agg, outdir, fused=True):
     dY = torch.randn(V, O, generator=torch.Generator().manual_seed(2))
     torch.manual_seed(3)
     conv = SIRConv(d, H, O, nn.LeakyReLU(0.2), 0, agg_type=agg)
-    dg = DistGraph.from_global(src, dst, V, rank, world, "cpu", chunk=64)
+    dg = DistGraph.from_global(src, dst, V, rank, world, "cpu", chunk=64, chunks=chunks)
     dconv = DistSIRConv(conv, backend=cpu_edge_backend)
     dconv.use_fused = fused
     r0, r1 = dg.row_begin, dg.row_end
@@ -51,20 +51,21 @@ def _worker(rank, world, port, agg, outdir, fused=True):
     torch.save({"r0": r0, "r1": r1, "Y": Y.detach(), "dX": Xl.grad, "E_local": dg.num_local_edges,
                 "bounds": dg.bounds, "grads": {n: p.grad for n, p in conv.named_parameters()},
                 "halo": dg.halo_ids, "recv_splits": dg.recv_splits, "send_splits": dg.send_splits,
-                "send_idx": dg.send_idx, "out_deg": dg.out_deg()},
+                "send_idx": dg.send_idx, "halo_off": dg.halo_off, "out_deg": dg.out_deg()},
                os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,agg,fused", [(2, "sum", True), (2, "sym", True), (3, "mean", True),
-                                             (4, "sym", True), (3, "sum", False), (2, "mean", False)])
-def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg, fused):
+@pytest.mark.parametrize("world,agg,fused,chunks", [(2, "sum", True, None), (2, "sym", True, 1), (3, "mean", True, 3),
+                                                    (4, "sym", True, None), (3, "sum", False, 2),
+                                                    (2, "mean", False, 7)])
+def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg, fused, chunks):
     import oracle
     from sirgcn.synth import powerlaw_edges
     from torch import nn
     from sirgcn import SIRConv
-    mp.spawn(_worker, args=(world, _free_port(), agg, str(tmp_path), fused), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), agg, str(tmp_path), fused, chunks), nprocs=world, join=True)
     parts = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     V, E, d, H, O = 500, 6000, 16, 40, 12
     src, dst = powerlaw_edges(V, E, 0.8, seed=7)
@@ -80,24 +81,30 @@ def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg, fused):
     assert all(parts[i]["r1"] == parts[i + 1]["r0"] for i in range(world - 1))
     assert sum(p["E_local"] for p in parts) == E
     assert max(p["E_local"] for p in parts) <= E / world + int(torch.bincount(dst, minlength=V).max())
-    # halo exchange plan: every rank's halo = its distinct remote sources, grouped by owner;
-    # what owner q sends to rank p is exactly p's halo slice owned by q, in the same order
+    # halo exchange plan: every rank's halo = its distinct remote sources, stored chunk-major (each
+    # chunk: a part of every owner's block, owners in order); what owner q sends to rank p in chunk c
+    # is exactly p's chunk-c slice owned by q, in the same order
+    C = len(parts[0]["recv_splits"])
+    assert C == (chunks if chunks is not None else 4)
     for p, part in enumerate(parts):
         r0, r1 = part["r0"], part["r1"]
         sel = (dst >= r0) & (dst < r1)
         s_ = src[sel]
         want = torch.unique(s_[(s_ < r0) | (s_ >= r1)])
-        assert torch.equal(part["halo"], want)
-        off = 0
-        for q in range(world):
-            n = part["recv_splits"][q]
-            mine = part["halo"][off:off + n]
-            off += n
-            if n:
-                assert int(mine.min()) >= parts[q]["r0"] and int(mine.max()) < parts[q]["r1"]
-            so = sum(parts[q]["send_splits"][:p])
-            sent = parts[q]["send_idx"][so:so + parts[q]["send_splits"][p]] + parts[q]["r0"]
-            assert torch.equal(sent, mine)
+        assert torch.equal(torch.sort(part["halo"]).values, want)
+        for c in range(C):
+            off = part["halo_off"][c]
+            for q in range(world):
+                n = part["recv_splits"][c][q]
+                mine = part["halo"][off:off + n]
+                off += n
+                if n:
+                    assert int(mine.min()) >= parts[q]["r0"] and int(mine.max()) < parts[q]["r1"]
+                    assert torch.all(mine[1:] > mine[:-1])
+                so = sum(parts[q]["send_splits"][c][:p])
+                sent = parts[q]["send_idx"][c][so:so + parts[q]["send_splits"][c][p]] + parts[q]["r0"]
+                assert torch.equal(sent, mine)
+            assert off == part["halo_off"][c + 1]
         # global out-degree of own + halo rows
         gdeg = torch.bincount(src, minlength=V)
         ext = torch.cat([torch.arange(r0, r1), part["halo"]])
@@ -200,7 +207,7 @@ def test_edge_cut_async_exchange_waits_before_use(agg):
         return Y, DistSIRConvFunction.backward(ctx, dY[dg.row_begin:dg.row_end]), comms[r].works
 
     outs = run_ranks(world, fn)
-    assert all(o[2] == 2 for o in outs)          # one async exchange forward, one backward, per rank
+    assert all(o[2] == 8 for o in outs)          # four async chunk exchanges forward, four backward, per rank
     Y = torch.cat([o[0] for o in outs])
     dX = torch.cat([o[1][0] for o in outs])
     assert torch.isfinite(Y).all() and torch.isfinite(dX).all()

@@ -165,3 +165,54 @@ def test_dist_layer_routes_autocast_to_the_16bit_function(monkeypatch):
            "dW_R": conv.linear_relation.weight.grad, "db_R": conv.linear_relation.bias.grad}
     _vs_amp_reference({k: v.clone() for k, v in got.items()}, conv, src, dst, V, X, dY, w, "sym",
                       torch.bfloat16, 2e-2)
+
+
+@pytest.mark.parametrize("world,agg", [(3, "sum"), (2, "sym")])
+def test_edge_cut_training_dropout_vs_explicit_mask(world, agg):
+    """Training-mode feature dropout in the fused edge-cut function (conv.py:35,60-61; the reference
+    trains with p = 0.2, ogbn-arxiv/train.py:303): Q and K masks from two device seeds per rank in
+    the GEMM epilogues, the owners' masks applied to dQ / dK after the exchange — against the
+    reference dataflow with the same masks applied explicitly (fp32 reference and fp64 truth)."""
+    from conftest import assert_parity
+    V, E, H = 2500, 50000, 256
+    p = 0.2
+    src, dst, X, dY, conv, w = _problem(V, E, 64, H, 32, agg, seed=11)
+    comms = ThreadComm.make(world)
+    bounds = partition_rows(torch.bincount(dst, minlength=V), world)
+    seeds = [torch.tensor([1000 + 2 * r, 1001 + 2 * r], device=DEV) for r in range(world)]
+
+    def fn(r):
+        dg = DistGraph(src, dst, V, bounds, r, world, DEV, group=comms[r])
+        ctx = FakeCtx((True,) * 6 + (False,) * 8)
+        sl = slice(dg.row_begin, dg.row_end)
+        with torch.no_grad():
+            Y = DistSIRConvFunction.forward(ctx, X[sl], *w, dg, agg, _native.ACT_LEAKY, 0.2, _native, True, True,
+                                            (seeds[r], p))
+            g = DistSIRConvFunction.backward(ctx, dY[sl])
+        torch.cuda.synchronize()
+        n = dg.n_rows
+        mq = _native.dropout_apply(torch.ones(n, H, device=DEV), (seeds[r][0:1], p))
+        mk = _native.dropout_apply(torch.ones(n, H, device=DEV), (seeds[r][1:2], p))
+        return Y, g, mq, mk
+
+    outs = run_ranks(world, fn)
+    Mk = torch.cat([torch.cat([o[2], o[3]], 1) for o in outs]).cpu()
+    assert 0.15 < float((Mk == 0).float().mean()) < 0.25
+    got = {"Y": torch.cat([o[0] for o in outs]).cpu(), "dX": torch.cat([o[1][0] for o in outs]).cpu()}
+    for i, k in enumerate(("dW_Q", "db_Q", "dW_K", "dW_R", "db_R"), start=1):
+        got[k] = sum(o[1][i].double() for o in outs).cpu()
+
+    def ref(dtype):
+        t = lambda x: x.detach().cpu().to(dtype).requires_grad_(True)
+        X64, WQ, bQ, WK, WR, bR = (t(x) for x in (X, *w))
+        M = Mk.to(dtype)
+        Q = (X64 @ WQ.t() + bQ) * M[:, :H]
+        K = (X64 @ WK.t()) * M[:, H:]
+        S = oracle.edge_agg_fwd(src, dst, V, Q, K, agg, "leaky", 0.2)
+        Y = S @ WR.t() + bR
+        Y.backward(dY.cpu().to(dtype))
+        return {"Y": Y.detach(), "dX": X64.grad, "dW_Q": WQ.grad, "db_Q": bQ.grad, "dW_K": WK.grad,
+                "dW_R": WR.grad, "db_R": bR.grad}
+    r32, r64 = ref(torch.float32), ref(torch.float64)
+    for k, v in got.items():
+        assert_parity(v, r32[k], r64[k], 1e-5, f"edge-cut dropout x{world} {agg} {k}", strict=(k == "Y"))

@@ -41,8 +41,14 @@ def main():
     a = ap.parse_args()
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[a.dtype]
     dcode = _native.STORAGE[tdt]
-    V, E, alpha = NAMED[a.graph]
-    src, dst = powerlaw_edges(V, E, alpha, seed=0)
+    if a.graph == "mol":             # config 2's ZINC-shaped batch of 10,000 molecules (~2 in-edges per row)
+        from sirgcn.synth import molecule_batch
+        g0 = molecule_batch(10_000, 23, seed=0)
+        src, dst = g0.edges()
+        V, E = g0.num_nodes(), int(src.numel())
+    else:
+        V, E, alpha = NAMED[a.graph]
+        src, dst = powerlaw_edges(V, E, alpha, seed=0)
     dev = "cuda"
     plan = GraphPlan(src, dst, V, dev, chunk=a.chunk)
     H = a.H
