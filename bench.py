@@ -479,6 +479,7 @@ def roofline_fwd(args, kernels, V, E, V_src, H, s, world):
     uniq = fwd_unique_bytes(V_src, V, E, H, s)
     ach = alg / t / 1e9
     traffic = None
+    traffic_source = None
     dts = args.dtype or "f32"
     pmc_file = args.pmc_file or os.path.join(ROOT, "profiles", f"pmc_traffic_{args.graph}"
                                              f"{'' if dts == 'f32' else '_' + dts}.json")
@@ -489,6 +490,15 @@ def roofline_fwd(args, kernels, V, E, V_src, H, s, world):
         if (rec and world == 1 and pmc.get("graph") == args.graph and pmc.get("agg") == args.agg
                 and pmc.get("H") == H and pmc.get("dtype", "f32") == (args.dtype or "f32")):
             traffic = rec["hbm_bytes_per_launch"]      # L2<->fabric bytes (Infinity-Cache hits included)
+            # which build the counters were taken on, against the build being timed: the counter
+            # bytes stand while the edge kernels' sources are unchanged
+            from sirgcn import _native
+            took = pmc.get("build") or {}
+            now = _native.build_id()
+            traffic_source = {"file": os.path.relpath(pmc_file, ROOT), "counters_build": took or "not recorded",
+                              "timed_build": now,
+                              "same_edge_kernels": (took.get("edge_source_hash") == now["edge_source_hash"])
+                              if took else None}
     except (OSError, ValueError):
         pass
     frac_alg = ach / HBM_PEAK_GBS
@@ -501,7 +511,7 @@ def roofline_fwd(args, kernels, V, E, V_src, H, s, world):
            "achieved": round(phys if phys else ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round((phys if phys else ach) / HBM_PEAK_GBS, 4),
            "frac_basis": "counter (HBM-side bytes from PMC)" if phys else "algorithmic (no PMC file for this config)",
-           "traffic": traffic, "algorithmic_bytes": alg, "ms_per_launch": k["ms"],
+           "traffic": traffic, "traffic_source": traffic_source, "algorithmic_bytes": alg, "ms_per_launch": k["ms"],
            "achieved_algorithmic": round(ach, 1), "frac_algorithmic": round(frac_alg, 4),
            "bytes_formula": "SURVEY 8(d): E*(s_i + H*s) + V*(2*H*s + s_i)",
            "unique_bytes": uniq, "frac_unique": round(uniq / t / 1e9 / HBM_PEAK_GBS, 4),

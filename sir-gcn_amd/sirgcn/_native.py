@@ -149,6 +149,30 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
+EDGE_SOURCES = ("sirconv_edge_impl.h", "sirconv_dropout.h", "sirconv_internal.h", "sirconv_dispatch.hip",
+                "sirconv_fwd_f32.hip", "sirconv_fwd_bf16.hip", "sirconv_fwd_f16.hip",
+                "sirconv_bwd_dual_f32.hip", "sirconv_bwd_dual_bf16.hip", "sirconv_bwd_dual_f16.hip")
+
+
+def edge_source_hash():
+    """Fingerprint of the sources the edge-aggregation kernels are compiled from (the kernels the
+    PMC traffic files of profiles/ describe): a counter file stays valid while this is unchanged."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in EDGE_SOURCES:
+        p = os.path.join(CSRC, name)
+        if not os.path.exists(p):
+            return None
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id():
+    """{library source hash, edge-kernel source hash} of this tree."""
+    return {"source_hash": source_hash(), "edge_source_hash": edge_source_hash()}
+
+
 def load():
     """Load (once) and return the ctypes handle; raise loudly if absent."""
     global _lib

@@ -16,10 +16,10 @@ backend ``nccl``):
 * **Forward: a pipelined exchange.**  K is projected for the own rows, and the halo arrives as
   ``chunks`` sparse all-to-alls (RCCL alltoallv over the xGMI mesh: every chunk moves 1/chunks of
   the rows of EVERY peer, so each one uses all links at once), all queued at once on RCCL's stream.
-  The edges of each destination row are stored in segments by source — own sources first, then the
-  edges whose halo row is in chunk 0, 1, ... — and the edge pass runs segment by segment: the own
-  segment (under the Q GEMM and the first chunk), then segment c+1 as soon as chunk c has landed
-  (``SIR_AGG_ACCUMULATE``: S[v] += the segment's sum).  Every row sums its segments in the same
+  The edges of each destination row are stored in segments by source — own sources and halo chunk
+  0 first, then the edges whose halo row is in chunk 1, 2, ... — and the edge pass runs segment by
+  segment as the chunks land (``SIR_AGG_ACCUMULATE``: S[v] += the segment's sum); chunk 0 lands
+  under the Q GEMM and the packing of the later chunks.  Every row sums its segments in the same
   fixed order, so the result is deterministic (not bit-identical to one GPU, whose rows sum in edge
   id order: tests hold it to the parity bar).  On the power-law S2 graph the halo is 1.15 M rows per
   rank at 8 ranks against the 1.77 M a dense all-gather moves.
@@ -232,15 +232,16 @@ class DistGraph:
         tgt = torch.cat([torch.arange(n, device=dev)] + [t for t in self.send_idx])
         pos = torch.cat([torch.arange(n, device=dev), self.n_ext + torch.arange(roff[-1], device=dev)])
         self.recv_plan = build_row_csr(tgt, pos, n, chunk)
-        # ---- edge columns in K_ext, segments (0: own source, 1 + c: halo chunk c) ----
+        # ---- edge columns in K_ext, segments (0: own source AND halo chunk 0, which lands under the
+        # Q GEMM and the packing of the later chunks; c >= 1: halo chunk c) ----
         if self.n_halo:
             hp = torch.searchsorted(halo, lsrc).clamp_(max=self.n_halo - 1)
             col = torch.where(local, lsrc - self.row_begin, n + new_pos[hp])
-            seg = torch.where(local, torch.zeros_like(lsrc), 1 + hchunk[hp])
+            seg = torch.where(local, torch.zeros_like(lsrc), hchunk[hp])
         else:
             col = lsrc - self.row_begin
             seg = torch.zeros_like(lsrc)
-        NS = C + 1
+        NS = max(C, 1)
         so = torch.argsort(seg, stable=True)     # the row sort below keeps (segment, edge id) order inside a row
         col, ldst, seg = col[so], ldst[so], seg[so]
         # ---- kernel plans over the K_ext layout ----
@@ -355,14 +356,17 @@ def _workspace(plan, H, device):
 
 def _segmented_forward(backend, dg, Q, K_ext, agg, act, slope, S, mask, works):
     """S = update_all(...) over the rank's in-edges, segment by segment as the halo chunks land:
-    the own segment writes every row, halo segment c + 1 adds its sum after waiting for chunk c
-    (``works[c]``; None: already complete).  MEAN divides once, after the last segment."""
+    segment 0 (own sources and halo chunk 0) writes every row, segment c >= 1 adds its sum; each
+    waits for its chunk (``works[c]``; None: already complete).  One segment per chunk, the own
+    sources riding with chunk 0: chunk 0 lands while the Q GEMM and the packing of the later chunks
+    run, and every extra segment costs a read-modify-write of S (tools/dist_model.py: -2 % per
+    step at 8 ranks).  MEAN divides once, after the last segment."""
     in_norm, out_norm = dg.norms(agg)
     a = "sum" if agg == "mean" else agg
     partial = _workspace(dg, Q.shape[1], Q.device)
     for s, seg in enumerate(dg.segments):
-        if s > 0 and works[s - 1] is not None:
-            works[s - 1].wait()
+        if s < len(works) and works[s] is not None:
+            works[s].wait()
         backend.edge_agg_fwd(seg, Q, K_ext, in_norm, out_norm, a, act, slope, S, partial, mask, accumulate=s > 0)
     if agg == "mean":
         S.copy_(S / dg.deg_f())      # fp32 division, one rounding to S's dtype (DGL fn.mean)
@@ -434,8 +438,8 @@ def _drops(drop):
 class DistSIRConvFunction(torch.autograd.Function):
     """One rank's share of the whole layer, hand-scheduled around the two pipelined exchanges.
 
-    forward : K_own = X W_K^T -> ``chunks`` halo alltoallvs queued ‖ Q = X W_Q^T + b_Q, own-source
-              segment -> halo segments as their chunks land -> Y = S W_R^T + b_R
+    forward : K_own = X W_K^T -> ``chunks`` halo alltoallvs queued ‖ Q = X W_Q^T + b_Q -> segment c
+              (0: own sources + chunk 0) as chunk c lands -> Y = S W_R^T + b_R
     backward: G = dY W_R -> dK of halo chunk c -> its reverse alltoallv (each as soon as computed) ‖
               dQ pass + own-row dK, dW_R, db_R, dX = dQ W_Q, dW_Q, db_Q -> dK_own += received ->
               dX += dK W_K, dW_K.  Weight gradients are this rank's partial sums.

@@ -19,7 +19,16 @@ import json
 import os
 from collections import defaultdict
 
-PASSES = {0: "sir_edge_agg_fwd", 1: "sir_edge_agg_bwd_dst", 2: "sir_edge_agg_bwd_src"}
+def build_id():
+    """The library / edge-kernel source hashes of the tree the counters were taken on (bench.py
+    names them beside the traffic it reads from this file)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sir-gcn_amd"))
+    from sirgcn import _native
+    return _native.build_id()
+
+
+PASSES = {0:"sir_edge_agg_fwd", 1: "sir_edge_agg_bwd_dst", 2: "sir_edge_agg_bwd_src"}
 
 
 def pass_of(short):
@@ -89,6 +98,7 @@ def main():
                      + ("" if a.dtype == "f32" else "; 16-bit storage gathers 8 B per lane, a width the x2 "
                         "correction is not calibrated for (MI355X_MICROARCH.md): fetch bytes are an upper "
                         "bound, fetch_kib_raw the lower one"),
+           "build": build_id(),
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = sorted(fetch.get(k, [0.0]))
