@@ -15,7 +15,7 @@
  *    GEMMs sir_gemm_nt / sir_gemm_nt_direct / sir_gemm_tn and the 16-bit (autocast) ones, the
  *    bias gradients sir_col_sum, the Q/K feature dropout sir_dropout_t (conv.py:35,60-61);
  *  - agg='max' and the per-edge Linear sigma (conv.py:46-47): sir_edge_mlp_* / sir_edge_max_*;
- *    the edge-materialised helpers (sir_edge_gather_add, sir_segment_*);
+ *    the edge-materialised helpers (sir_edge_gather_add / _act, sir_segment_*);
  *  - GraphNorm (models/norm.py:7-29): sir_graph_norm_fwd / _bwd;
  *  - the graph input (DGL's CSC build for batched graphs): sir_csr_build / sir_csr_perm.
  *
@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 11
+#define SIR_ABI_VERSION 12
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57).  SIR_AGG_ACCUMULATE,
  * OR'd into the forward's `agg` (SUM / SYM): S[v] = S[v] + the sum over the given items' edges, rows
@@ -224,6 +224,13 @@ int sir_edge_agg_bwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
 int sir_edge_gather_add(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
                         int64_t F, const float* Q, int64_t ldq, const float* K, int64_t ldk,
                         float* Z, int64_t ldz, void* stream);
+
+/* A[e] = act(Q[row(e)] + K[col[e]]), act = SIR_ACT_IDENTITY / _RELU / _LEAKY_RELU (slope): the
+ * materialised max backward's activations in one pass (conv.py:45-47; for the ReLU family sign(A)
+ * = sign(z), so sigma' is taken from A and z is never stored).  ABI 12. */
+int sir_edge_gather_act(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                        int64_t F, const float* Q, int64_t ldq, const float* K, int64_t ldk, int act, float slope,
+                        float* A, int64_t lda, void* stream);
 
 /* out[row] = sum_{e in row} c_e * X[idx(e)],  idx(e) = perm ? perm[e] : e,
  * c_e = norm_col[col[e]] * norm_row[row] when norm_row != NULL (the sym norm product, conv.py:45),

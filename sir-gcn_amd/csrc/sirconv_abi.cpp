@@ -282,6 +282,23 @@ int sir_edge_gather_add(const int32_t* rowptr, const int32_t* col, const int32_t
     return finish(fn, sir::run_gather_add(a, static_cast<hipStream_t>(stream)), "unsupported F / alignment");
 }
 
+int sir_edge_gather_act(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                        int64_t F, const float* Q, int64_t ldq, const float* K, int64_t ldk, int act, float slope,
+                        float* A, int64_t lda, void* stream) {
+    const char* fn = "sir_edge_gather_act";
+    int rc = check_generic(fn, n_items, F, items);
+    if (rc) return rc;
+    if (act != SIR_ACT_IDENTITY && act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU)
+        return fail(SIR_EINVAL, fn, "act must be identity, ReLU or LeakyReLU");
+    if (ldq < F || ldk < F || lda < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if (n_items > 0 && (Q == nullptr || K == nullptr)) return fail(SIR_EINVAL, fn, "NULL Q/K");
+    sir::GenericArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.F = (int)F;
+    a.X = Q; a.ldx = ldq; a.X2 = K; a.ldx2 = ldk; a.out = A; a.ldo = lda;
+    return finish(fn, sir::run_gather_add(a, static_cast<hipStream_t>(stream), act, slope),
+                  "unsupported F / alignment");
+}
+
 int sir_segment_sum(const int32_t* rowptr, const int32_t* col, const int32_t* perm,
                     const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
                     int64_t F, const float* X, int64_t ldx, const float* norm_row, const float* norm_col,

@@ -561,6 +561,195 @@ k_mlp_fwd16p(const int* __restrict__ rowptr, const int* __restrict__ col, const 
     }
 }
 
+// Pipelined persistent form (H <= 256, F <= 256; the S1 / S2 max shape): k_mlp_fwd16p's register-
+// resident weights, with the block's stream of 32-edge tiles (item after item, b, b + grid, ...)
+// software-pipelined so that no gather latency is exposed: while tile i is multiplied and reduced,
+// the K rows of tile i + 1 (and its Q row, its norms) are in flight in registers, and the column
+// indices of tile i + 2 are loaded one tile earlier still (each wave takes its rows' source ids from
+// that vector by v_readlane).  k_mlp_fwd16p issued each tile's gathers and waited for them right
+// away (one memory latency per tile on a CU holding one block).  Per tile and edge the arithmetic,
+// its order and the reduction order are k_mlp_fwd16p's: the results are bit-identical.
+template <int ACT1, int ACT2, int RED, int NGT>
+__global__ void __launch_bounds__(512)
+k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_t n_items, const float* __restrict__ Q,
+             int64_t ldq, const float* __restrict__ K, int64_t ldk, const float* __restrict__ norm_row,
+             const float* __restrict__ norm_col, float slope, int H, int F, const h8v* __restrict__ Wp16,
+             const float* __restrict__ winv, const float* __restrict__ bias, float* __restrict__ out, int64_t ldo,
+             int* __restrict__ arg, int64_t lda, float* __restrict__ pval, int* __restrict__ parg) {
+    constexpr int NW = 8, RPW = 4;
+    constexpr int NG = NGT;
+    constexpr int C4 = (NG * 16 + 255) / 256;       // float4 chunks of 256 features per row (1 up to H = 256)
+    static_assert(C4 == 1, "H <= 256");
+    __shared__ __attribute__((aligned(16))) char img[NG * 2048];
+    __shared__ float sInv[32], sC[32];
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ntile = (F + 31) / 32;
+    const bool has_t = w < ntile;
+    const int n = 32 * w + (l & 31);
+    const float bbv = (bias != nullptr && n < F) ? bias[n] : 0.f;
+    const float iwv = (n < F) ? winv[n] : 0.f;
+    h8v whi[NG], wlo[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (has_t) {
+            whi[g] = Wp16[(((int64_t)w * NG + g) * 2 + 0) * 64 + l];
+            wlo[g] = Wp16[(((int64_t)w * NG + g) * 2 + 1) * 64 + l];
+        } else {
+            whi[g] = h8v{};
+            wlo[g] = h8v{};
+        }
+    }
+    const int fo = mlp_fimg(l & 31, l >> 5);
+    const int k4 = 4 * l;
+    // tile cursor (wave-uniform): item index, its row / end / slot, the tile's first edge; a cursor past
+    // the last item reads row 0, edge 0 (valid addresses; nothing of it is used)
+    struct Cur { int64_t itx; int row, e0, e1, slot, t0; };
+    auto first_of = [&](int64_t itx) {
+        Cur c;
+        if (itx < n_items) {
+            const int4 it = uniform_item(items, itx);
+            c = Cur{itx, it.x, it.y, it.z, it.w, it.y};
+        } else {
+            c = Cur{n_items, 0, 0, 0, -1, 0};
+        }
+        return c;
+    };
+    auto advance = [&](const Cur& c) {   // the next tile: the next 32 edges of the item, or the block's next item
+        if (c.itx < n_items && c.t0 + 32 < c.e1) {
+            Cur d = c;
+            d.t0 += 32;
+            return d;
+        }
+        return first_of(c.itx < n_items ? c.itx + gridDim.x : n_items);
+    };
+    // lane l (mod 32) of the tile's column vector: col[t0 + min(l, nv - 1)], col[0] for an empty tile
+    auto load_col = [&](const Cur& c) {
+        const int nv = c.e1 - c.t0 < 32 ? c.e1 - c.t0 : 32;
+        const int li = l & 31;
+        return col[nv > 0 ? c.t0 + (li < nv ? li : nv - 1) : 0];
+    };
+    float4 kv[RPW];
+    float4 q4;
+    float cn = 0.f;
+    auto gather = [&](const Cur& c, int colv) {
+#pragma unroll
+        for (int ii = 0; ii < RPW; ++ii) {
+            const int u = __builtin_amdgcn_readlane(colv, w + NW * ii);
+            kv[ii] = (k4 < H) ? *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        q4 = (k4 < H) ? *reinterpret_cast<const float4*>(Q + (int64_t)c.row * ldq + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (RED == AGG_SYM) cn = norm_col[colv] * norm_row[c.row];   // conv.py:45 operand order
+    };
+
+    Cur cur = first_of(blockIdx.x);
+    Cur n1 = advance(cur);
+    int colv_n1 = load_col(n1);
+    gather(cur, load_col(cur));
+    float racc = 0.f, best = -INFINITY;
+    int bidx = INT_MAX;
+    while (cur.itx < n_items) {
+        const int nv = (cur.e1 - cur.t0) < 32 ? (cur.e1 - cur.t0) : 32;
+        // ---- stage tile cur (its rows are in kv / q4) into the LDS image
+#pragma unroll
+        for (int ii = 0; ii < RPW; ++ii) {
+            const int i = w + NW * ii;
+            const bool ok = i < nv && k4 < H;
+            float4 a4;
+            a4.x = ok ? act_f<ACT1>(q4.x + kv[ii].x, slope) : 0.f;
+            a4.y = ok ? act_f<ACT1>(q4.y + kv[ii].y, slope) : 0.f;
+            a4.z = ok ? act_f<ACT1>(q4.z + kv[ii].z, slope) : 0.f;
+            a4.w = ok ? act_f<ACT1>(q4.w + kv[ii].w, slope) : 0.f;
+            float m = fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w)));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+            const int se = mlp_scale_exp(m);
+            const float sc = mlp_pow2(se);
+            if (k4 < NG * 16) {
+                const float y[4] = {a4.x * sc, a4.y * sc, a4.z * sc, a4.w * sc};
+                _Float16 hv[4], lv[4];
+#pragma unroll
+                for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
+                const int g = k4 >> 4, h = (k4 >> 3) & 1, j8 = k4 & 7;
+                char* d = img + g * 2048 + mlp_fimg(i, h) + j8 * 2;
+                *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
+                *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
+            }
+            if (l == 0) sInv[i] = mlp_pow2(-se);
+        }
+        if (w == 0 && l < 32) sC[l] = (l < nv) ? ((RED == AGG_SYM) ? cn : 1.f) : 0.f;
+        __syncthreads();
+        // ---- tile n1's rows in flight from here to the next stage; tile n2's column ids one tile earlier
+        const Cur n2 = advance(n1);
+        const int colv_n2 = load_col(n2);
+        gather(n1, colv_n1);
+        if (has_t) {
+            mf16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const h8v ahi = *reinterpret_cast<const h8v*>(img + g * 2048 + fo);
+                const h8v alo = *reinterpret_cast<const h8v*>(img + g * 2048 + 1024 + fo);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = drow(r, l);
+                if (i < nv) {
+                    const float m = act_f<ACT2>(acc[r] * sInv[i] * iwv + bbv, slope);
+                    if constexpr (RED == 3) {
+                        if (m > best) { best = m; bidx = cur.t0 + i; }    // strict >: first wins
+                    } else {
+                        racc += sC[i] * m;
+                    }
+                }
+            }
+            if (n1.itx != cur.itx) {                 // the item's last tile: combine the half-waves, store
+                const int row = cur.row, slot = cur.slot;
+                if constexpr (RED == 3) {
+                    const float ob = __shfl_xor(best, 32);
+                    const int oi = __shfl_xor(bidx, 32);
+                    if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+                    if (l < 32 && n < F) {
+                        const bool any = bidx != INT_MAX;
+                        if (slot < 0) {
+                            out[(int64_t)row * ldo + n] = any ? best : 0.f;
+                            arg[(int64_t)row * lda + n] = any ? bidx : -1;
+                        } else {
+                            pval[(int64_t)slot * F + n] = best;
+                            parg[(int64_t)slot * F + n] = bidx;
+                        }
+                    }
+                } else {
+                    const float other = __shfl_xor(racc, 32);
+                    float v = (l < 32) ? racc + other : other + racc;
+                    if (l < 32 && n < F) {
+                        if (slot < 0) {
+                            if constexpr (RED == AGG_MEAN) {
+                                const int d = cur.e1 - cur.e0;
+                                v = v / (float)(d > 1 ? d : 1);
+                            }
+                            out[(int64_t)row * ldo + n] = v;
+                        } else {
+                            pval[(int64_t)slot * F + n] = v;
+                        }
+                    }
+                }
+                racc = 0.f;
+                best = -INFINITY;
+                bidx = INT_MAX;
+            }
+        }
+        __syncthreads();
+        cur = n1;
+        n1 = n2;
+        colv_n1 = colv_n2;
+    }
+}
+
 // max: combine the chunk partials of split rows in chunk (= edge) order, strict > (first wins)
 __global__ void k_mlp_max_combine(const int4* __restrict__ splits, int F, const float* __restrict__ pval,
                                   const int* __restrict__ parg, float* __restrict__ Y, int64_t ldy,
@@ -822,11 +1011,34 @@ int64_t mlp_pack16_bytes(int H, int F) {
 // profiles/r03_ab_mlp_resident.txt: the W stream from L2 was not the bound), so NG = 16 stays per-item
 #define SIR_MLP_RESIDENT 1
 #endif
+#ifndef SIR_MLP_PIPE
+#define SIR_MLP_PIPE 1          // 1: H in {64, 128, 256}, F <= 256 on the pipelined k_mlp_fwd16q
+#endif
 template <int ACT1, int ACT2, int RED>
 hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
     const int NG = mlp_ng(a.H), FP = (a.F + 31) / 32 * 32;
     const h8v* w16 = static_cast<const h8v*>(p16);
     const float* winv = reinterpret_cast<const float*>(static_cast<const char*>(p16) + (int64_t)FP * NG * 64);
+    if (SIR_MLP_PIPE && a.col != nullptr && a.F <= 256 && (NG == 4 || NG == 8 || NG == 16)) {
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        // resident blocks only (a persistent block never yields its CU): NG = 4 takes 120 VGPRs (two
+        // 512-thread blocks per CU), NG = 8 / 16 152 / 216 (one)
+        const int64_t cap = (int64_t)ncu * (NG == 4 ? 2 : 1);
+        const int64_t nb = a.n_items < cap ? a.n_items : cap;
+        const dim3 g((unsigned)nb);
+#define SIR_MLP_FWD16Q(NGV)                                                                                         \
+        hipLaunchKernelGGL((k_mlp_fwd16q<ACT1, ACT2, RED, NGV>), g, dim3(512), 0, st, a.col,                           \
+                           reinterpret_cast<const int4*>(a.items), a.n_items, a.Q, a.ldq, a.K, a.ldk, a.norm_row,      \
+                           a.norm_col, a.slope, a.H, a.F, w16, winv, a.bias, a.out, a.ldo, a.arg, a.lda, a.pval, a.parg)
+        if (NG == 4) SIR_MLP_FWD16Q(4);
+        else if (NG == 8) SIR_MLP_FWD16Q(8);
+        else SIR_MLP_FWD16Q(16);
+#undef SIR_MLP_FWD16Q
+        return hipGetLastError();
+    }
     if (SIR_MLP_RESIDENT && a.F <= 256 && (NG == 4 || NG == 8)) {
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) != hipSuccess ||

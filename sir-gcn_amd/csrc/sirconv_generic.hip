@@ -51,11 +51,12 @@ __device__ __forceinline__ int64_t wave_id() {
 }
 
 // ---------------------------------------------------------------------------------------- gather
-template <int NV, int VW>
+// ACT: ACT_IDENTITY (Z = the sum), ACT_RELU / ACT_LEAKY (A = sigma of it: torch's relu / leaky_relu)
+template <int NV, int VW, int ACT>
 __global__ void __launch_bounds__(256)
 k_gather_add(const int* __restrict__ col, const int4* __restrict__ items, int64_t n_items, int F,
              const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
-             float* __restrict__ Z, int64_t ldz) {
+             float* __restrict__ Z, int64_t ldz, float slope) {
     const int64_t w = wave_id();
     if (w >= n_items) return;
     const Item it = load_item(items, w);
@@ -76,7 +77,11 @@ k_gather_add(const int* __restrict__ col, const int4* __restrict__ items, int64_
                 float k[VW];
                 ld<VW>(k, K + (int64_t)u * ldk + c * VW);
 #pragma unroll
-                for (int x = 0; x < VW; ++x) k[x] = q[j][x] + k[x];       // eq[v] + ek[u] (conv.py:45)
+                for (int x = 0; x < VW; ++x) {
+                    k[x] = q[j][x] + k[x];                                 // eq[v] + ek[u] (conv.py:45)
+                    if constexpr (ACT == ACT_RELU) k[x] = k[x] > 0.f ? k[x] : 0.f;
+                    else if constexpr (ACT == ACT_LEAKY) k[x] = k[x] > 0.f ? k[x] : k[x] * slope;
+                }
                 st<VW>(Z + (int64_t)e * ldz + c * VW, k);
             }
         }
@@ -351,16 +356,23 @@ bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p
 
 }  // namespace
 
-hipError_t run_gather_add(const GenericArgs& a, hipStream_t st) {
+hipError_t run_gather_add(const GenericArgs& a, hipStream_t st, int act, float slope) {
     GShape s;
     const bool v4 = al16(a.X) && al16(a.X2) && al16(a.out) && a.ldx % 4 == 0 && a.ldx2 % 4 == 0 && a.ldo % 4 == 0;
     if (!gshape(a.F, v4, &s)) return hipErrorInvalidValue;
+    if (act != ACT_IDENTITY && act != ACT_RELU && act != ACT_LEAKY) return hipErrorInvalidValue;
     if (a.n_items == 0) return hipSuccess;
     gdispatch(s, [&](auto nv_, auto vw_) {
         constexpr int NV_ = decltype(nv_)::value, VW_ = decltype(vw_)::value;
-        hipLaunchKernelGGL((k_gather_add<NV_, VW_>), dim3(blocks_for(a.n_items)), dim3(256), 0, st,
-                                        a.col, reinterpret_cast<const int4*>(a.items), a.n_items, a.F,
-                                        a.X, a.ldx, a.X2, a.ldx2, a.out, a.ldo);
+        const dim3 grid(blocks_for(a.n_items));
+#define SIR_GATHER(ACTV)                                                                                        \
+        hipLaunchKernelGGL((k_gather_add<NV_, VW_, ACTV>), grid, dim3(256), 0, st, a.col,                       \
+                           reinterpret_cast<const int4*>(a.items), a.n_items, a.F, a.X, a.ldx, a.X2, a.ldx2, a.out, \
+                           a.ldo, slope)
+        if (act == ACT_RELU) SIR_GATHER(ACT_RELU);
+        else if (act == ACT_LEAKY) SIR_GATHER(ACT_LEAKY);
+        else SIR_GATHER(ACT_IDENTITY);
+#undef SIR_GATHER
     });
     return hipGetLastError();
 }

@@ -79,7 +79,7 @@ struct GenericArgs {
     int* parg;
 };
 
-hipError_t run_gather_add(const GenericArgs& a, hipStream_t st);
+hipError_t run_gather_add(const GenericArgs& a, hipStream_t st, int act = ACT_IDENTITY, float slope = 0.f);
 hipError_t run_seg_sum(const GenericArgs& a, hipStream_t st);
 hipError_t run_edge_bcast(const GenericArgs& a, hipStream_t st);
 hipError_t run_seg_max(const GenericArgs& a, hipStream_t st);

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("SIRGCN_LIB") or os.path.join(os.path.dirname(os.path.
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 11
+ABI_VERSION = 12
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -33,6 +33,7 @@ SIGNATURES = {
     "sir_graph_norm_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I64,
                                           _P, _P, _P, _P]),
     "sir_edge_gather_add": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P]),
+    "sir_edge_gather_act": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _I64, _P]),
     "sir_segment_sum": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64,
                                        _P, _P]),
     "sir_edge_broadcast": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64, _P]),
@@ -319,6 +320,17 @@ def edge_gather_add(csr, Q, K, Z):
     with _Timed("sir_edge_gather_add", Z.device):
         rc = lib.sir_edge_gather_add(_ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, F,
                                      _ptr(Q), _ld(Q, F), _ptr(K), _ld(K, F), _ptr(Z), _ld(Z, F), _stream(Z.device))
+    _check(rc, lib)
+
+
+def edge_gather_act(csr, Q, K, act, slope, A):
+    """A[e] = act(Q[row(e)] + K[col[e]]) for act in {identity, ReLU, LeakyReLU} (dst-CSR edge order)."""
+    lib = load()
+    F = A.shape[1]
+    with _Timed("sir_edge_gather_act", A.device):
+        rc = lib.sir_edge_gather_act(_ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, F,
+                                     _ptr(Q), _ld(Q, F), _ptr(K), _ld(K, F), int(act), float(slope), _ptr(A),
+                                     _ld(A, F), _stream(A.device))
     _check(rc, lib)
 
 

@@ -194,17 +194,25 @@ class EdgeMaxLinear(torch.autograd.Function):
         if fused and max_bwd_fused(H, O):
             dQK, dW, db = _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope)
             return dQK, dW, (db if ctx.has_b else None), None, None, None, None
-        # the arg edges' activations are needed for dW_R: recompute z_e once (no copy kept from the forward)
-        Z = torch.empty((E, H), device=dev, dtype=torch.float32)
-        _native.edge_gather_add(plan.dst, QK[:, :H], QK[:, H:], Z)
-        A = _act(Z, act1, slope)
+        # the arg edges' activations are needed for dW_R: recompute them once (no copy kept from the
+        # forward).  ReLU family: A = sigma(z) straight from the gather (sign(A) = sign(z), so sigma' is
+        # read off A below and z is never stored); other sigmas: z, then sigma(z)
+        relu_family = act1 in (_native.ACT_RELU, _native.ACT_LEAKY)
+        if relu_family:
+            A = torch.empty((E, H), device=dev, dtype=torch.float32)
+            _native.edge_gather_act(plan.dst, QK[:, :H], QK[:, H:], act1, slope, A)
+            Z = A
+        else:
+            Z = torch.empty((E, H), device=dev, dtype=torch.float32)
+            _native.edge_gather_add(plan.dst, QK[:, :H], QK[:, H:], Z)
+            A = _act(Z, act1, slope)
         dM = torch.empty((E, O), device=dev, dtype=torch.float32)
         _native.segment_max_bwd(plan.dst, arg, dY, dM)                 # dY to the first arg-max edge
         dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
         del A
         dA = linalg.mm_w(dM, W)                                        # [E, H]
         del dM
-        dZ = _act_bwd(Z, dA, act1, slope)
+        dZ = _act_bwd(Z, dA, act1, slope, is_result=relu_family)
         del Z, dA
         dQK = torch.empty_like(QK)
         n_slots = max(plan.dst.n_slots, plan.src.n_slots)
@@ -264,13 +272,14 @@ def _act(z, code, slope):
     return z.clone()
 
 
-def _act_bwd(z, g, code, slope):
+def _act_bwd(z, g, code, slope, is_result=False):
     """sigma'(z) * g with torch's own backward kernels (the ops autograd runs: one fused pass over
-    the [E, H] tensors instead of compare + multiply + select, ~3x fewer bytes)."""
+    the [E, H] tensors instead of compare + multiply + select, ~3x fewer bytes).  ``is_result``: ``z``
+    holds sigma(z) (ReLU family: the same sign, so the same sigma'), computed in place into ``g``."""
     if code == _native.ACT_RELU:
         return torch.ops.aten.threshold_backward(g, z, 0.0)
     if code == _native.ACT_LEAKY:
-        return torch.ops.aten.leaky_relu_backward(g, z, slope, False)
+        return torch.ops.aten.leaky_relu_backward(g, z, slope, is_result)
     if code in (_native.ACT_GELU, _native.ACT_GELU_TANH):
         zz = z.detach().requires_grad_(True)
         with torch.enable_grad():

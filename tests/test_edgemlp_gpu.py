@@ -269,3 +269,22 @@ def test_max_backward_routes_agree(fused, monkeypatch):
     for k in a:
         e = (a[k] - b[k]).norm() / b[k].norm().clamp_min(1e-30)
         assert e < 1e-5, (k, float(e))
+
+
+@pytest.mark.parametrize("act,slope", [(_native.ACT_RELU, 0.0), (_native.ACT_LEAKY, 0.2), (_native.ACT_IDENTITY, 0.0)])
+@pytest.mark.parametrize("H", [256, 37])
+def test_edge_gather_act_bit_exact(act, slope, H):
+    """sir_edge_gather_act: A[e] = act(Q[v] + K[u]) in dst-CSR edge order equals torch's own ops on the
+    gathered sum bit for bit (the materialised max backward reads sigma' off A)."""
+    from sirgcn.graph import get_plan
+    src, dst, V, gen = _graph(11)
+    plan = get_plan(Graph(src, dst, V), torch.device(DEV))
+    QK = torch.randn(V, 2 * H, generator=gen).to(DEV)
+    E = plan.dst.col.numel()
+    A = torch.empty(E, H, device=DEV)
+    _native.edge_gather_act(plan.dst, QK[:, :H], QK[:, H:], act, slope, A)
+    rows = torch.repeat_interleave(torch.arange(V, device=DEV), (plan.dst.rowptr[1:] - plan.dst.rowptr[:-1]).long())
+    z = QK[rows, :H] + QK[plan.dst.col.long(), H:]
+    ref = {_native.ACT_RELU: torch.relu, _native.ACT_LEAKY: lambda t: torch.nn.functional.leaky_relu(t, slope),
+           _native.ACT_IDENTITY: lambda t: t}[act](z)
+    assert torch.equal(A, ref)
