@@ -1333,7 +1333,7 @@ k_gemm_nt_s(const float* __restrict__ A, int64_t lda, int64_t M, int K, const u4
 // reads after its sibling come from L2 / the Infinity Cache.  Same chunks, running-scale rule, MFMA
 // order per accumulator and epilogue arithmetic as k_gemm_nt_p: bit-identical results.
 #ifndef SIR_NT_WS
-#define SIR_NT_WS 1             // the default route (env SIR_NT_WS_MODE): 0 k_gemm_nt_p, 1 / 2 k_gemm_nt_ws with 32 / 64 rows per wave
+#define SIR_NT_WS 0             // the default route (env SIR_NT_WS_MODE): 0 k_gemm_nt_p, 1 / 2 k_gemm_nt_ws with 32 / 64 rows per wave
 #endif
 constexpr int WS_SLAB_BYTES = 131072;
 #ifndef WS_NS

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python tools/gemm_ab.py --rounds 7 --only QK,Y,G,dX \
-    --libs p=sir-gcn_amd/lib/libsirconv_p.so ws=sir-gcn_amd/lib/libsirconv.so ns3=sir-gcn_amd/lib/libsirconv_ns3.so ns4=sir-gcn_amd/lib/libsirconv_ns4.so \
+    --libs p=sir-gcn_amd/lib/libsirconv.so ws=sir-gcn_amd/lib/libsirconv_ws.so ns3=sir-gcn_amd/lib/libsirconv_ns3.so ns4=sir-gcn_amd/lib/libsirconv_ns4.so \
     2>&1 | tee gpurun_out/r04_ab_ws.txt &&
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gemm_gpu.py -k "nt" \
     2>&1 | tee gpurun_out/r04_ws_tests.txt &&
