@@ -394,6 +394,14 @@ int sir_gemm_pack(const float* W, int64_t ldw, int64_t N, int64_t K, int trans, 
 int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
                 const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream);
 
+/* C = sigma'(gate) * (A B^T) with B packed as for sir_gemm_nt: gate [M, N] with C's leading dimension
+ * (the activation's input z or output sigma(z): the same sign for the ReLU family); act =
+ * SIR_ACT_RELU (gate > 0 ? x : 0) or SIR_ACT_LEAKY_RELU (gate > 0 ? x : x * slope) — torch's
+ * threshold / leaky_relu backward fused into the GEMM's epilogue (the materialised max backward's
+ * dZ = sigma'(z) * (dM W_R), conv.py:46-47).  ABI 12. */
+int sir_gemm_nt_dact(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
+                     const float* gate, int act, float slope, float* C, int64_t ldc, void* stream);
+
 /* Small batches (config 5's 1.6k-node molecule batches): C[M, N] = A[M, K] B^T + bias with the
  * weight read as fp32 straight from W (B[n][k] = W[n*ldw + k], trans = 0, or W[k*ldw + n], trans =
  * 1) — no packing pass per weight update; both operands split in the kernel, each with running

@@ -611,6 +611,25 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
     return finish(fn, err, nullptr);
 }
 
+int sir_gemm_nt_dact(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
+                     const float* gate, int act, float slope, float* C, int64_t ldc, void* stream) {
+    const char* fn = "sir_gemm_nt_dact";
+    if (M < 0 || N <= 0 || K <= 0 || N > 65536 || K > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if ((M + 255) / 256 * ((N + 127) / 128) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
+    if (K % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldc % 4 != 0 || lda < K || ldc < N)
+        return fail(SIR_EINVAL, fn, "K, N, lda, ldc must be multiples of 4 (lda >= K, ldc >= N)");
+    if (lda > SIR_GEMM_MAX_LD || ldc > SIR_GEMM_MAX_LD) return fail(SIR_EINVAL, fn, "lda / ldc too large");
+    if (act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU) return fail(SIR_EINVAL, fn, "act must be ReLU or LeakyReLU");
+    if (M > 0 && (A == nullptr || C == nullptr || packed == nullptr || gate == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(gate) |
+          reinterpret_cast<uintptr_t>(packed)) & 15u) != 0)
+        return fail(SIR_EINVAL, fn, "A, C, gate and packed must be 16-B aligned");
+    hipError_t err = sir::run_gemm_nt(A, lda, M, (int)K, packed, (int)N, nullptr, C, ldc, static_cast<hipStream_t>(stream),
+                                      sir::Drop(), gate, act == SIR_ACT_RELU ? 1 : 0, slope);
+    return finish(fn, err, nullptr);
+}
+
 int sir_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int64_t K, const float* W, int64_t ldw, int trans,
                        int64_t N, const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream) {
     const char* fn = "sir_gemm_nt_direct";

@@ -103,6 +103,19 @@ __device__ inline void drop4(const Drop& d, int64_t row, int n, float4& o) {
     o.w = drop_keep(d, rh, c + 3) ? o.w * d.scale : 0.f;
 }
 
+// sigma'(z) * x from the sign of the gate (z or sigma(z): the same sign for the ReLU family)
+__device__ inline float gate_dact(float g, float x, int relu, float slope) {
+    return g > 0.f ? x : (relu ? 0.f : x * slope);
+}
+// in place: C = sigma'(gate) * C (the gated GEMM's epilogue for the routes without it)
+__global__ void __launch_bounds__(256)
+k_gate_dact(float* __restrict__ C, int64_t ldc, const float* __restrict__ gate, int64_t M, int N, int relu, float slope) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= M * N) return;
+    const int64_t r = i / N, c = i % N;
+    C[r * ldc + c] = gate_dact(gate[r * ldc + c], C[r * ldc + c], relu, slope);
+}
+
 #ifndef SIR_SPLIT_MIX
 #define SIR_SPLIT_MIX 1         // TN loaders: 1 = the split by v_fma_mix (2 VALU per element), 0 = plain C (~4.5)
 #endif                          // (the NT kernels keep the C form: the asm one costs them a spill in the loop)
@@ -541,11 +554,16 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #endif
 constexpr int NT_P_NMAX = 512;
 
-template <int NCT>
+// GATE: C = sigma'(gate) * (A B^T) (gate [M, N] with C's leading dimension; ReLU: gate > 0 ? x : 0,
+// LeakyReLU: gate > 0 ? x : x * slope — torch's threshold / leaky_relu backward with the activation's
+// output or input as `gate`: the same sign): the materialised max backward's dZ = sigma'(z) * (dM W_R)
+// in the GEMM's epilogue instead of an [E, H] elementwise pass
+template <int NCT, bool GATE>
 __global__ void __launch_bounds__(512)
 k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
-            int64_t ldc, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop) {
+            int64_t ldc, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop, const float* __restrict__ gate,
+            int gate_relu, float gate_slope) {
     drop = drop_resolve(drop);
     constexpr int WF = 4, TDT = 4, TFT = 2;
     constexpr int NT = 512, BD = 256, BF = 256, TPR = NT / BD, FPT = KC / TPR, WPT = BF * 8 / NT;
@@ -736,6 +754,7 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
         const uint32_t ldc4 = (uint32_t)ldc * 4u;
         const uint32_t nrec = (uint32_t)p.rows * ldc4;
         const rsrc_t crs = mk_rsrc(C + p.d0 * ldc, (SIR_ABL_NT & 2) ? 0u : nrec);
+        const rsrc_t grs = mk_rsrc(GATE ? gate + p.d0 * ldc : C, GATE ? nrec : 0u);
         const float* sc = fin + slot * BD;
         char* const wrow = img + ((wq / WF) * 32 + rq) * PITCH + (f_wq + 4 * hq) * 4;
 #pragma unroll
@@ -761,10 +780,17 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int ir = wq + 8 * i, c16 = lq;                 // image row, 16-B piece of it
-                const u4v v = *reinterpret_cast<const u4v*>(img + ir * PITCH + c16 * 16);
+                u4v v = *reinterpret_cast<const u4v*>(img + ir * PITCH + c16 * 16);
                 const int ml = (ir >> 5) * (TDT * 32) + 32 * b + (ir & 31);
                 const int n = p.f0 + 4 * c16;
                 const uint32_t off = (n < N) ? (uint32_t)ml * ldc4 + (uint32_t)c16 * 16u : nrec;
+                if constexpr (GATE) {
+                    const u4v gv = __builtin_amdgcn_raw_buffer_load_b128(grs, off, p.f0 * 4, 0);
+                    v.x = __float_as_uint(gate_dact(__uint_as_float(gv.x), __uint_as_float(v.x), gate_relu, gate_slope));
+                    v.y = __float_as_uint(gate_dact(__uint_as_float(gv.y), __uint_as_float(v.y), gate_relu, gate_slope));
+                    v.z = __float_as_uint(gate_dact(__uint_as_float(gv.z), __uint_as_float(v.z), gate_relu, gate_slope));
+                    v.w = __float_as_uint(gate_dact(__uint_as_float(gv.w), __uint_as_float(v.w), gate_relu, gate_slope));
+                }
                 __builtin_amdgcn_raw_buffer_store_b128(v, crs, off, p.f0 * 4, 0);
                 // a 16-byte store reads its data VGPRs over several cycles (see below)
                 __builtin_amdgcn_sched_barrier(0);
@@ -1786,8 +1812,37 @@ hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, v
 }
 
 hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
-                       const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
+                       const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop, const float* gate,
+                       int gate_relu, float gate_slope) {
     if (M == 0 || N == 0) return hipSuccess;
+    if (gate != nullptr) {     // fused in k_gemm_nt_p's epilogue; any other route applies it afterwards
+        const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
+        if (M >= gemm_small_rows() && N > 128 && np <= NT_P_NMAX && K % KC == 0 && (kc == 4 || kc == 8 || kc == 16)) {
+            const u4v* wp = static_cast<const u4v*>(packed);
+            const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
+            constexpr int BD = 256, BF = 256;
+            const int nft = (N + BF - 1) / BF;
+            const int64_t ntiles = (M + BD - 1) / BD * nft;
+            int dev = 0, ncu = 256;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                ncu = 256;
+            if (ntiles < (int64_t)1 << 30) {
+                const int tpb = (int)((ntiles + ncu - 1) / ncu);
+                const int nblk = (int)((ntiles + tpb - 1) / tpb);
+                auto kern = kc == 4 ? k_gemm_nt_p<4, true> : (kc == 8 ? k_gemm_nt_p<8, true> : k_gemm_nt_p<16, true>);
+                hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, ldc,
+                                   nft, (int)ntiles, tpb, drop, gate, gate_relu, gate_slope);
+                return hipGetLastError();
+            }
+        }
+        hipError_t err = run_gemm_nt(A, lda, M, K, packed, N, bias, C, ldc, st, drop, nullptr, 0, 0.f);
+        if (err != hipSuccess) return err;
+        const int64_t cnt = M * N;
+        hipLaunchKernelGGL(k_gate_dact, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, C, ldc, gate, M, N,
+                           gate_relu, gate_slope);
+        return hipGetLastError();
+    }
     const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
     const u4v* wp = static_cast<const u4v*>(packed);
     const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
@@ -1827,9 +1882,9 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
         if (ntiles < (int64_t)1 << 30) {
             const int tpb = (int)((ntiles + ncu - 1) / ncu);
             const int nblk = (int)((ntiles + tpb - 1) / tpb);
-            auto kern = kc == 4 ? k_gemm_nt_p<4> : (kc == 8 ? k_gemm_nt_p<8> : k_gemm_nt_p<16>);
+            auto kern = kc == 4 ? k_gemm_nt_p<4, false> : (kc == 8 ? k_gemm_nt_p<8, false> : k_gemm_nt_p<16, false>);
             hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, ldc,
-                               nft, (int)ntiles, tpb, drop);
+                               nft, (int)ntiles, tpb, drop, nullptr, 0, 0.f);
             return hipGetLastError();
         }
     }

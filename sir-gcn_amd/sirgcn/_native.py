@@ -45,6 +45,7 @@ SIGNATURES = {
     "sir_gemm_pack_bytes": (ctypes.c_int64, [_I64, _I64]),
     "sir_gemm_pack": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _P, _P]),
     "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P, _P]),
+    "sir_gemm_nt_dact": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _I, _F, _P, _I64, _P]),
     "sir_gemm_nt_direct": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, ctypes.c_int, _I64, _P, _P, _I64, _P, _P]),
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
     "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
@@ -462,6 +463,23 @@ def gemm_nt(A, packed, bias=None, out=None, drop=None):
     with _Timed(f"sir_gemm_nt K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + N))):
         rc = lib.sir_gemm_nt(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(bias), _ptr(out), out.stride(0),
                              _drop(drop), _stream(A.device))
+    _check(rc, lib)
+    return out
+
+
+def gemm_nt_dact(A, packed, gate, act, slope, out=None):
+    """C = sigma'(gate) * (A B^T) (``sir_gemm_nt_dact``: the ReLU family's backward in the GEMM epilogue;
+    ``gate`` = the activation's input or output, C's shape and leading dimension)."""
+    lib = load()
+    pk, N, K = packed
+    M = A.shape[0]
+    assert A.dim() == 2 and A.shape[1] == K and A.stride(1) == 1
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    assert gate.shape == out.shape and gate.stride() == out.stride()
+    with _Timed(f"sir_gemm_nt_dact K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + 2 * N))):
+        rc = lib.sir_gemm_nt_dact(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(gate), int(act), float(slope),
+                                  _ptr(out), out.stride(0), _stream(A.device))
     _check(rc, lib)
     return out
 

@@ -209,11 +209,15 @@ class EdgeMaxLinear(torch.autograd.Function):
         dM = torch.empty((E, O), device=dev, dtype=torch.float32)
         _native.segment_max_bwd(plan.dst, arg, dY, dM)                 # dY to the first arg-max edge
         dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
-        del A
-        dA = linalg.mm_w(dM, W)                                        # [E, H]
-        del dM
-        dZ = _act_bwd(Z, dA, act1, slope, is_result=relu_family)
-        del Z, dA
+        if relu_family:     # dZ = sigma'(z) * (dM W_R) with sigma' read off A in the GEMM's epilogue
+            dZ = linalg.mm_w_dact(dM, W, A, act1, slope)
+            del A, Z, dM
+        else:
+            del A
+            dA = linalg.mm_w(dM, W)                                    # [E, H]
+            del dM
+            dZ = _act_bwd(Z, dA, act1, slope)
+            del Z, dA
         dQK = torch.empty_like(QK)
         n_slots = max(plan.dst.n_slots, plan.src.n_slots)
         part = torch.empty((max(n_slots, 1) * H,), device=dev, dtype=torch.float32) if n_slots else None

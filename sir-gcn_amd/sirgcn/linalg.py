@@ -77,6 +77,19 @@ def mm_w(A, W):
     return torch.mm(A, W)
 
 
+def mm_w_dact(A, W, gate, act, slope):
+    """sigma'(gate) * (A W) for the ReLU family (W [K, N]; ``gate`` the activation's input or output,
+    same sign): native with the activation backward in the GEMM epilogue when the operands allow,
+    else torch's mm + threshold / leaky_relu backward."""
+    if (USE_NATIVE and _ok(A) and _w_ok(W, W.shape[1]) and _ok(gate) and gate.shape == (A.shape[0], W.shape[1])
+            and gate.stride(0) == W.shape[1]):
+        return _native.gemm_nt_dact(A, _native.gemm_pack(W.contiguous(), trans=True), gate, act, slope)
+    g = torch.mm(A, W)
+    if act == _native.ACT_RELU:
+        return torch.ops.aten.threshold_backward(g, gate, 0.0)
+    return torch.ops.aten.leaky_relu_backward(g, gate, slope, False)
+
+
 def _tn_ok(t):
     return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and t.shape[0] >= MIN_ROWS
             and 0 < t.shape[1] <= MAX_DIM and t.stride(0) <= MAX_LD)

@@ -420,3 +420,21 @@ def test_gemm_nt_direct_dropout_epilogue_and_errors():
     assert abs(frac - p) < 0.01, frac
     with pytest.raises(RuntimeError, match="multiples of 4"):
         _native.gemm_nt_direct(torch.zeros(10, 6, device=DEV), torch.zeros(8, 6, device=DEV))
+
+
+@pytest.mark.parametrize("M,K,N", [(40000, 256, 256), (20000, 512, 256), (20000, 256, 64), (3000, 256, 256)])
+@pytest.mark.parametrize("act,slope", [(_native.ACT_LEAKY, 0.2), (_native.ACT_RELU, 0.0)])
+def test_gemm_nt_dact_equals_gemm_then_activation_backward(M, K, N, act, slope):
+    """sir_gemm_nt_dact (sigma'(gate) applied in k_gemm_nt_p's epilogue, or after the GEMM on the other
+    routes) is bit-identical to the native packed-weight GEMM followed by torch's threshold /
+    leaky_relu backward."""
+    from sirgcn import linalg
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(K, N, device="cuda", generator=g) / K ** 0.5
+    gate = torch.randn(M, N, device="cuda", generator=g)
+    got = linalg.mm_w_dact(A, W, gate, act, slope)
+    ref = _native.gemm_nt(A, _native.gemm_pack(W, trans=True))
+    ref = (torch.ops.aten.threshold_backward(ref, gate, 0.0) if act == _native.ACT_RELU
+           else torch.ops.aten.leaky_relu_backward(ref, gate, slope, False))
+    assert torch.equal(got, ref)
