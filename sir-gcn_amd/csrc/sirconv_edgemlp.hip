@@ -561,6 +561,20 @@ k_mlp_fwd16p(const int* __restrict__ rowptr, const int* __restrict__ col, const 
     }
 }
 
+// max over the 64 lanes (non-negative values: exact in any order): DPP within each 16-lane row, then
+// the four rows' maxima by v_readlane — no LDS round trip (ds_bpermute) per level
+__device__ __forceinline__ float wave_max64(float m) {
+    m = fmaxf(m, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, m), 0xB1, 0xF, 0xF, false)));
+    m = fmaxf(m, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, m), 0x4E, 0xF, 0xF, false)));
+    m = fmaxf(m, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, m), 0x141, 0xF, 0xF, false)));
+    m = fmaxf(m, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, m), 0x140, 0xF, 0xF, false)));
+    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, m), 0));
+    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, m), 16));
+    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, m), 32));
+    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, m), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
 // Pipelined persistent form (H <= 256, F <= 256; the S1 / S2 max shape): k_mlp_fwd16p's register-
 // resident weights, with the block's stream of 32-edge tiles (item after item, b, b + grid, ...)
 // software-pipelined so that no gather latency is exposed: while tile i is multiplied and reduced,
@@ -569,7 +583,7 @@ k_mlp_fwd16p(const int* __restrict__ rowptr, const int* __restrict__ col, const 
 // that vector by v_readlane).  k_mlp_fwd16p issued each tile's gathers and waited for them right
 // away (one memory latency per tile on a CU holding one block).  Per tile and edge the arithmetic,
 // its order and the reduction order are k_mlp_fwd16p's: the results are bit-identical.
-template <int ACT1, int ACT2, int RED, int NGT>
+template <int ACT1, int ACT2, int RED, int NGT, bool HF>
 __global__ void __launch_bounds__(512)
 k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_t n_items, const float* __restrict__ Q,
              int64_t ldq, const float* __restrict__ K, int64_t ldk, const float* __restrict__ norm_row,
@@ -581,7 +595,8 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
     constexpr int C4 = (NG * 16 + 255) / 256;       // float4 chunks of 256 features per row (1 up to H = 256)
     static_assert(C4 == 1, "H <= 256");
     __shared__ __attribute__((aligned(16))) char img[NG * 2048];
-    __shared__ float sInv[32], sC[32];
+    __shared__ __attribute__((aligned(16))) float sInv[32];
+    __shared__ __attribute__((aligned(16))) float sC[32];
     const int l = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ntile = (F + 31) / 32;
@@ -602,16 +617,33 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
     }
     const int fo = mlp_fimg(l & 31, l >> 5);
     const int k4 = 4 * l;
-    // tile cursor (wave-uniform): item index, its row / end / slot, the tile's first edge; a cursor past
-    // the last item reads row 0, edge 0 (valid addresses; nothing of it is used)
-    struct Cur { int64_t itx; int row, e0, e1, slot, t0; };
-    auto first_of = [&](int64_t itx) {
+    // HF: H == 16 NG == 64 * 4 (H = 256, the S1 / S2 shape): every lane's 4 features exist, no masked load
+    const bool kin = HF || k4 < H;
+    // The block's items b, b + grid, ... come 64 at a time as one vector load (lane j: the block's
+    // item 64 q + j), two batches held, read by v_readlane: no scalar load (and no lgkmcnt wait that
+    // the LDS reads of the MFMA phase would share) per tile.
+    auto load_batch = [&](int q) {
+        const int64_t itx = blockIdx.x + (int64_t)(64 * q + l) * gridDim.x;
+        return itx < n_items ? items[itx] : make_int4(0, 0, 0, -1);
+    };
+    int bq = 0;
+    int4 ib0 = load_batch(0), ib1 = load_batch(1);
+    // tile cursor (wave-uniform): the block's item ordinal k, its row / edges / slot, the tile's first
+    // edge; a cursor past the last item reads row 0, edge 0 (valid addresses; nothing of it is used)
+    struct Cur { int k; int64_t itx; int row, e0, e1, slot, t0; };
+    auto first_of = [&](int k) {
+        const int64_t itx = blockIdx.x + (int64_t)k * gridDim.x;
         Cur c;
         if (itx < n_items) {
-            const int4 it = uniform_item(items, itx);
-            c = Cur{itx, it.x, it.y, it.z, it.w, it.y};
+            const int j = k & 63;
+            const bool in0 = (k >> 6) == bq;
+            const int x = __builtin_amdgcn_readlane(in0 ? ib0.x : ib1.x, j);
+            const int y = __builtin_amdgcn_readlane(in0 ? ib0.y : ib1.y, j);
+            const int z = __builtin_amdgcn_readlane(in0 ? ib0.z : ib1.z, j);
+            const int wv = __builtin_amdgcn_readlane(in0 ? ib0.w : ib1.w, j);
+            c = Cur{k, itx, x, y, z, wv, y};
         } else {
-            c = Cur{n_items, 0, 0, 0, -1, 0};
+            c = Cur{k, n_items, 0, 0, 0, -1, 0};
         }
         return c;
     };
@@ -621,7 +653,7 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
             d.t0 += 32;
             return d;
         }
-        return first_of(c.itx < n_items ? c.itx + gridDim.x : n_items);
+        return first_of(c.itx < n_items ? c.k + 1 : c.k);
     };
     // lane l (mod 32) of the tile's column vector: col[t0 + min(l, nv - 1)], col[0] for an empty tile
     auto load_col = [&](const Cur& c) {
@@ -636,13 +668,13 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
 #pragma unroll
         for (int ii = 0; ii < RPW; ++ii) {
             const int u = __builtin_amdgcn_readlane(colv, w + NW * ii);
-            kv[ii] = (k4 < H) ? *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            kv[ii] = kin ? *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        q4 = (k4 < H) ? *reinterpret_cast<const float4*>(Q + (int64_t)c.row * ldq + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        q4 = kin ? *reinterpret_cast<const float4*>(Q + (int64_t)c.row * ldq + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (RED == AGG_SYM) cn = norm_col[colv] * norm_row[c.row];   // conv.py:45 operand order
     };
 
-    Cur cur = first_of(blockIdx.x);
+    Cur cur = first_of(0);
     Cur n1 = advance(cur);
     int colv_n1 = load_col(n1);
     gather(cur, load_col(cur));
@@ -654,18 +686,16 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
 #pragma unroll
         for (int ii = 0; ii < RPW; ++ii) {
             const int i = w + NW * ii;
-            const bool ok = i < nv && k4 < H;
+            const bool ok = i < nv && kin;
             float4 a4;
             a4.x = ok ? act_f<ACT1>(q4.x + kv[ii].x, slope) : 0.f;
             a4.y = ok ? act_f<ACT1>(q4.y + kv[ii].y, slope) : 0.f;
             a4.z = ok ? act_f<ACT1>(q4.z + kv[ii].z, slope) : 0.f;
             a4.w = ok ? act_f<ACT1>(q4.w + kv[ii].w, slope) : 0.f;
-            float m = fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w)));
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+            const float m = wave_max64(fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w))));
             const int se = mlp_scale_exp(m);
             const float sc = mlp_pow2(se);
-            if (k4 < NG * 16) {
+            if (NG * 16 >= 256 || k4 < NG * 16) {
                 const float y[4] = {a4.x * sc, a4.y * sc, a4.z * sc, a4.w * sc};
                 _Float16 hv[4], lv[4];
 #pragma unroll
@@ -695,16 +725,27 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
             }
+            // branch-free: the lane's 16 edge rows are 8 g + 4 (l / 32) + (0..3), g = 0..3 — their scales
+            // (and c_e) come as four 16-B LDS reads; rows past the tile's last edge are masked by select
+            const int hb = 4 * (l >> 5);
+            float4 inv4[4], c4[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                inv4[g] = *reinterpret_cast<const float4*>(sInv + 8 * g + hb);
+                if constexpr (RED != 3) c4[g] = *reinterpret_cast<const float4*>(sC + 8 * g + hb);
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int i = drow(r, l);
-                if (i < nv) {
-                    const float m = act_f<ACT2>(acc[r] * sInv[i] * iwv + bbv, slope);
-                    if constexpr (RED == 3) {
-                        if (m > best) { best = m; bidx = cur.t0 + i; }    // strict >: first wins
-                    } else {
-                        racc += sC[i] * m;
-                    }
+                const float iv = r % 4 == 0 ? inv4[r / 4].x : r % 4 == 1 ? inv4[r / 4].y : r % 4 == 2 ? inv4[r / 4].z : inv4[r / 4].w;
+                const float m = act_f<ACT2>(acc[r] * iv * iwv + bbv, slope);
+                if constexpr (RED == 3) {
+                    const bool take = i < nv && m > best;         // strict >: first wins
+                    best = take ? m : best;
+                    bidx = take ? cur.t0 + i : bidx;
+                } else {
+                    const float cv = r % 4 == 0 ? c4[r / 4].x : r % 4 == 1 ? c4[r / 4].y : r % 4 == 2 ? c4[r / 4].z : c4[r / 4].w;
+                    racc += (i < nv) ? cv * m : 0.f;
                 }
             }
             if (n1.itx != cur.itx) {                 // the item's last tile: combine the half-waves, store
@@ -747,6 +788,11 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
         cur = n1;
         n1 = n2;
         colv_n1 = colv_n2;
+        if ((cur.k >> 6) > bq) {             // cur entered the second batch: n2 (<= cur + 2 items) stays within it
+            ++bq;
+            ib0 = ib1;
+            ib1 = load_batch(bq + 1);
+        }
     }
 }
 
@@ -1012,30 +1058,29 @@ int64_t mlp_pack16_bytes(int H, int F) {
 #define SIR_MLP_RESIDENT 1
 #endif
 #ifndef SIR_MLP_PIPE
-#define SIR_MLP_PIPE 1          // 1: H in {64, 128, 256}, F <= 256 on the pipelined k_mlp_fwd16q
+#define SIR_MLP_PIPE 1          // 1: 128 < H <= 256, F <= 256 on k_mlp_fwd16q (S1 max forward 13.74 -> 10.27 ms,
+                                // profiles/r04_ab_mlp_fwd.txt; at H <= 128 k_mlp_fwd16p stays faster)
 #endif
 template <int ACT1, int ACT2, int RED>
 hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
     const int NG = mlp_ng(a.H), FP = (a.F + 31) / 32 * 32;
     const h8v* w16 = static_cast<const h8v*>(p16);
     const float* winv = reinterpret_cast<const float*>(static_cast<const char*>(p16) + (int64_t)FP * NG * 64);
-    if (SIR_MLP_PIPE && a.col != nullptr && a.F <= 256 && (NG == 4 || NG == 8 || NG == 16)) {
+    if (SIR_MLP_PIPE && a.col != nullptr && a.F <= 256 && NG == 16) {
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
-        // resident blocks only (a persistent block never yields its CU): NG = 4 takes 120 VGPRs (two
-        // 512-thread blocks per CU), NG = 8 / 16 152 / 216 (one)
-        const int64_t cap = (int64_t)ncu * (NG == 4 ? 2 : 1);
+        // resident blocks only (a persistent block never yields its CU): one 512-thread block per CU
+        const int64_t cap = (int64_t)ncu;
         const int64_t nb = a.n_items < cap ? a.n_items : cap;
         const dim3 g((unsigned)nb);
-#define SIR_MLP_FWD16Q(NGV)                                                                                         \
-        hipLaunchKernelGGL((k_mlp_fwd16q<ACT1, ACT2, RED, NGV>), g, dim3(512), 0, st, a.col,                           \
+#define SIR_MLP_FWD16Q(NGV, HFV)                                                                                    \
+        hipLaunchKernelGGL((k_mlp_fwd16q<ACT1, ACT2, RED, NGV, HFV>), g, dim3(512), 0, st, a.col,                      \
                            reinterpret_cast<const int4*>(a.items), a.n_items, a.Q, a.ldq, a.K, a.ldk, a.norm_row,      \
                            a.norm_col, a.slope, a.H, a.F, w16, winv, a.bias, a.out, a.ldo, a.arg, a.lda, a.pval, a.parg)
-        if (NG == 4) SIR_MLP_FWD16Q(4);
-        else if (NG == 8) SIR_MLP_FWD16Q(8);
-        else SIR_MLP_FWD16Q(16);
+        if (a.H == 256) SIR_MLP_FWD16Q(16, true);
+        else SIR_MLP_FWD16Q(16, false);
 #undef SIR_MLP_FWD16Q
         return hipGetLastError();
     }

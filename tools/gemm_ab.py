@@ -23,8 +23,9 @@ from sirgcn import _native  # noqa: E402
 def open_lib(path):
     lib = ctypes.CDLL(path)
     for name, (res, args) in _native.SIGNATURES.items():
-        f = getattr(lib, name)
-        f.restype, f.argtypes = res, args
+        f = getattr(lib, name, None)        # an older A/B build may lack newer entry points
+        if f is not None:
+            f.restype, f.argtypes = res, args
     return lib
 
 
