@@ -594,9 +594,10 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
     constexpr int NG = NGT;
     constexpr int C4 = (NG * 16 + 255) / 256;       // float4 chunks of 256 features per row (1 up to H = 256)
     static_assert(C4 == 1, "H <= 256");
-    __shared__ __attribute__((aligned(16))) char img[NG * 2048];
-    __shared__ __attribute__((aligned(16))) float sInv[32];
-    __shared__ __attribute__((aligned(16))) float sC[32];
+    // two LDS images: tile i is multiplied out of one while tile i + 1 is staged into the other
+    __shared__ __attribute__((aligned(16))) char img[2][NG * 2048];
+    __shared__ __attribute__((aligned(16))) float sInv[2][32];
+    __shared__ __attribute__((aligned(16))) float sC[2][32];
     const int l = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ntile = (F + 31) / 32;
@@ -673,16 +674,10 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
         q4 = kin ? *reinterpret_cast<const float4*>(Q + (int64_t)c.row * ldq + k4) : make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (RED == AGG_SYM) cn = norm_col[colv] * norm_row[c.row];   // conv.py:45 operand order
     };
-
-    Cur cur = first_of(0);
-    Cur n1 = advance(cur);
-    int colv_n1 = load_col(n1);
-    gather(cur, load_col(cur));
-    float racc = 0.f, best = -INFINITY;
-    int bidx = INT_MAX;
-    while (cur.itx < n_items) {
-        const int nv = (cur.e1 - cur.t0) < 32 ? (cur.e1 - cur.t0) : 32;
-        // ---- stage tile cur (its rows are in kv / q4) into the LDS image
+    // stage tile c (its rows in kv / q4 / cn) into image buffer bf: a = act1(q + k), one power-of-two
+    // scale per edge row (its max over the 64 lanes), fp16 hi / lo pieces in fragment order
+    auto stage = [&](int bf, const Cur& c) {
+        const int nv = (c.e1 - c.t0) < 32 ? (c.e1 - c.t0) : 32;
 #pragma unroll
         for (int ii = 0; ii < RPW; ++ii) {
             const int i = w + NW * ii;
@@ -701,38 +696,57 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
 #pragma unroll
                 for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
                 const int g = k4 >> 4, h = (k4 >> 3) & 1, j8 = k4 & 7;
-                char* d = img + g * 2048 + mlp_fimg(i, h) + j8 * 2;
+                char* d = img[bf] + g * 2048 + mlp_fimg(i, h) + j8 * 2;
                 *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
                 *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
             }
-            if (l == 0) sInv[i] = mlp_pow2(-se);
+            if (l == 0) sInv[bf][i] = mlp_pow2(-se);
         }
-        if (w == 0 && l < 32) sC[l] = (l < nv) ? ((RED == AGG_SYM) ? cn : 1.f) : 0.f;
-        __syncthreads();
-        // ---- tile n1's rows in flight from here to the next stage; tile n2's column ids one tile earlier
-        const Cur n2 = advance(n1);
-        const int colv_n2 = load_col(n2);
-        gather(n1, colv_n1);
+        if (w == 0 && l < 32) sC[bf][l] = (l < nv) ? ((RED == AGG_SYM) ? cn : 1.f) : 0.f;
+    };
+
+    Cur cur = first_of(0);
+    Cur n1 = advance(cur);
+    Cur n2 = advance(n1);
+    int colv_n2 = load_col(n2);
+    gather(cur, load_col(cur));
+    const int colv_n1 = load_col(n1);
+    stage(0, cur);
+    gather(n1, colv_n1);
+    __syncthreads();
+    float racc = 0.f, best = -INFINITY;
+    int bidx = INT_MAX;
+    int bf = 0;
+    while (cur.itx < n_items) {
+        const int nv = (cur.e1 - cur.t0) < 32 ? (cur.e1 - cur.t0) : 32;
+        // ---- tile cur's MFMAs (image bf) and tile n1's staging (image bf ^ 1, rows in kv) in one block:
+        // the staging VALU / LDS writes fill the MFMA issue gaps
+        // (unconditional: a wave past F multiplies its zero weights — no branch splits the block)
+        mf16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const h8v ahi = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + fo);
+            const h8v alo = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + 1024 + fo);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
+        }
+        stage(bf ^ 1, n1);
+        // ---- tile n2's rows in flight from here to the next iteration's staging; n3's column ids
+        const Cur n3 = advance(n2);
+        const int colv_n3 = load_col(n3);
+        gather(n2, colv_n2);
         if (has_t) {
-            mf16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                const h8v ahi = *reinterpret_cast<const h8v*>(img + g * 2048 + fo);
-                const h8v alo = *reinterpret_cast<const h8v*>(img + g * 2048 + 1024 + fo);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
-            }
             // branch-free: the lane's 16 edge rows are 8 g + 4 (l / 32) + (0..3), g = 0..3 — their scales
             // (and c_e) come as four 16-B LDS reads; rows past the tile's last edge are masked by select
             const int hb = 4 * (l >> 5);
             float4 inv4[4], c4[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                inv4[g] = *reinterpret_cast<const float4*>(sInv + 8 * g + hb);
-                if constexpr (RED != 3) c4[g] = *reinterpret_cast<const float4*>(sC + 8 * g + hb);
+                inv4[g] = *reinterpret_cast<const float4*>(sInv[bf] + 8 * g + hb);
+                if constexpr (RED != 3) c4[g] = *reinterpret_cast<const float4*>(sC[bf] + 8 * g + hb);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -787,8 +801,10 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
         __syncthreads();
         cur = n1;
         n1 = n2;
-        colv_n1 = colv_n2;
-        if ((cur.k >> 6) > bq) {             // cur entered the second batch: n2 (<= cur + 2 items) stays within it
+        n2 = n3;
+        colv_n2 = colv_n3;
+        bf ^= 1;
+        if ((cur.k >> 6) > bq) {             // cur entered the second batch: n3 (<= cur + 3 items) stays within it
             ++bq;
             ib0 = ib1;
             ib1 = load_batch(bq + 1);
@@ -1058,7 +1074,7 @@ int64_t mlp_pack16_bytes(int H, int F) {
 #define SIR_MLP_RESIDENT 1
 #endif
 #ifndef SIR_MLP_PIPE
-#define SIR_MLP_PIPE 1          // 1: 128 < H <= 256, F <= 256 on k_mlp_fwd16q (S1 max forward 13.74 -> 10.27 ms,
+#define SIR_MLP_PIPE 1          // 1: 128 < H <= 256, F <= 256 on k_mlp_fwd16q (S1 max forward 13.69 -> 10.02 ms,
                                 // profiles/r04_ab_mlp_fwd.txt; at H <= 128 k_mlp_fwd16p stays faster)
 #endif
 template <int ACT1, int ACT2, int RED>
