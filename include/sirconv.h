@@ -282,6 +282,18 @@ int sir_edge_mlp_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
                      const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda,
                      float* pval, int32_t* parg, void* stream);
 
+/* The same forward over the dst-CSR edge STREAM (H = 256, F <= 256: the S1 / S2 max shape): 32-edge
+ * MFMA tiles are consecutive windows of each block's edge range, so short rows share a tile.
+ * erow[e] = destination row of dst-CSR edge e (n_edges entries); work = sir_edge_mlp_stream_work_bytes(F)
+ * bytes (per-block boundary partials).  Same outputs as sir_edge_mlp_fwd (MAX: bit-identical values
+ * and first arg-max edges; the sum family adds each row's terms in edge order).  ABI 12. */
+int64_t sir_edge_mlp_stream_work_bytes(int64_t F);
+int sir_edge_mlp_fwd_stream(const int32_t* rowptr, const int32_t* col, const int32_t* erow, int64_t n_rows,
+                            int64_t n_edges, int64_t H, int64_t F, const float* Q, int64_t ldq, const float* K,
+                            int64_t ldk, const float* norm_row, const float* norm_col, int agg, int act1, float slope,
+                            int act2, const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg,
+                            int64_t lda, void* work, void* stream);
+
 /* Backward of the SUM / MEAN / SYM form (H, F <= 256): the destination pass writes dQ [rows, H] and one
  * partial [dW (FP x HP) | db (FP)] row per block into wpart (FP = F rounded up to 32, HP = H rounded up
  * to 8; sir_edge_mlp_bwd_parts(n_items, H, F) rows of FP*HP + FP floats: sum them in row order, e.g.

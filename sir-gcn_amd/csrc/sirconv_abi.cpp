@@ -417,6 +417,40 @@ int sir_edge_mlp_fwd(const int32_t* rowptr, const int32_t* col, const int32_t* i
     return finish(fn, sir::run_mlp_fwd(a, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
 }
 
+int64_t sir_edge_mlp_stream_work_bytes(int64_t F) {
+    if (F <= 0 || F > 512) return 0;
+    return sir::mlp_stream_work_bytes((int)F);
+}
+
+int sir_edge_mlp_fwd_stream(const int32_t* rowptr, const int32_t* col, const int32_t* erow, int64_t n_rows,
+                            int64_t n_edges, int64_t H, int64_t F, const float* Q, int64_t ldq, const float* K,
+                            int64_t ldk, const float* norm_row, const float* norm_col, int agg, int act1, float slope,
+                            int act2, const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg,
+                            int64_t lda, void* work, void* stream) {
+    const char* fn = "sir_edge_mlp_fwd_stream";
+    if (H != 256 || F <= 0 || F > 256) return fail(SIR_EUNSUPPORTED, fn, "H = 256, F <= 256");
+    if (n_rows < 0 || n_edges < 0 || n_edges >= INT32_MAX) return fail(SIR_EINVAL, fn, "bad sizes");
+    if (agg != SIR_AGG_SUM && agg != SIR_AGG_MEAN && agg != SIR_AGG_SYM && agg != SIR_AGG_MAX)
+        return fail(SIR_EINVAL, fn, "agg");
+    if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH || act2 < SIR_ACT_IDENTITY || act2 > SIR_ACT_GELU_TANH)
+        return fail(SIR_EINVAL, fn, "act");
+    if (n_rows > 0 && (rowptr == nullptr || out == nullptr || ldo < F || packed == nullptr || work == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer / ldo");
+    if (n_edges > 0 && (col == nullptr || erow == nullptr || Q == nullptr || K == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL col / erow / Q / K");
+    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || !al16(Q) || !al16(K))
+        return fail(SIR_EUNSUPPORTED, fn, "Q/K rows must be 16-B aligned (ld % 4 == 0, ld >= H)");
+    if (agg == SIR_AGG_MAX && n_rows > 0 && (arg == nullptr || lda < F)) return fail(SIR_EINVAL, fn, "MAX needs arg");
+    if (agg == SIR_AGG_SYM && n_edges > 0 && (norm_row == nullptr || norm_col == nullptr))
+        return fail(SIR_EINVAL, fn, "SYM needs norm_row and norm_col");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr; a.col = col; a.erow = erow; a.n_rows = n_rows; a.n_edges = n_edges;
+    a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope;
+    a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.bias = bias;
+    a.out = out; a.ldo = ldo; a.arg = arg; a.lda = lda; a.work = work;
+    return finish(fn, sir::run_mlp_fwd_stream(a, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
+}
+
 int64_t sir_edge_mlp_bwd_parts(int64_t n_items, int64_t H, int64_t F) {
     if (H <= 0 || F <= 0 || H > 256 || F > 256) return 0;
     return sir::mlp_bwd_blocks(n_items, (int)H, (int)F);

@@ -812,6 +812,272 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
     }
 }
 
+
+// ------------------------------------------------------------------------------ forward, edge stream
+// The same per-edge layer with the 32-edge MFMA tiles taken from the dst-CSR edge STREAM instead of
+// per work item: block b owns edges [E b / nb, E (b + 1) / nb), its tiles are consecutive 32-edge
+// windows of it, so a tile holds the edges of several short rows (S1: median in-degree 8 — the
+// per-item tiles of k_mlp_fwd16q were 47 % full) and a long row runs through several tiles.  Each
+// edge brings its own Q row (erow: the row of every edge).  After the MFMAs every wave writes its
+// 32 features x 32 edges of m (c_e m for the sum family) to an LDS tile [feature][edge], and lane n
+// walks the tile's edges in order, reducing runs of equal row (max: strict >, first arg-max wins;
+// sum: in edge order) and storing a row when its run ends.  A row cut by the block's first or last
+// edge writes its partial to the block's slot 2b / 2b + 1 (with its row id in prow), and
+// k_mlp_stream_combine merges the slots of each row in block (= edge) order; rows with no edge are
+// written by k_mlp_empty_rows.  H = 256 (the S1 / S2 shape), F <= 256; the rest is k_mlp_fwd16q's
+// pipeline (weights in registers, two images, next tile's gathers in flight).
+template <int ACT1, int ACT2, int RED>
+__global__ void __launch_bounds__(512)
+k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const int* __restrict__ rowptr, int64_t E,
+             const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
+             const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope, int F,
+             const h8v* __restrict__ Wp16, const float* __restrict__ winv, const float* __restrict__ bias,
+             float* __restrict__ out, int64_t ldo, int* __restrict__ arg, int64_t lda, float* __restrict__ pval,
+             int* __restrict__ parg, int* __restrict__ prow) {
+    constexpr int NW = 8, RPW = 4, NG = 16, MP = 36;   // MP: pitch of the m tile (floats), bank-rotating
+    __shared__ __attribute__((aligned(16))) char img[2][NG * 2048];
+    __shared__ __attribute__((aligned(16))) float sInv[2][32];
+    __shared__ __attribute__((aligned(16))) float sC[2][32];
+    __shared__ __attribute__((aligned(16))) float mt[NW][32 * MP];
+    const int l = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x, nb = gridDim.x;
+    const int64_t eb = E * b / nb, ee = E * (b + 1) / nb;
+    if (threadIdx.x == 0) { prow[2 * b] = -1; prow[2 * b + 1] = -1; }
+    if (eb >= ee) return;                                    // block-uniform, before any barrier
+    const int row_before = eb > 0 ? erow[eb - 1] : -1;       // a run continuing from the previous block
+    const int row_after = ee < E ? erow[ee] : -1;            // ... into the next block
+    const int n = 32 * w + (l & 31);
+    const bool fo_ok = (l < 32) && n < F;                    // the lane that owns feature n's walk / stores
+    const float bbv = (bias != nullptr && n < F) ? bias[n] : 0.f;
+    const float iwv = (n < F) ? winv[n] : 0.f;
+    h8v whi[NG], wlo[NG];
+    const bool has_t = w < (F + 31) / 32;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (has_t) {
+            whi[g] = Wp16[(((int64_t)w * NG + g) * 2 + 0) * 64 + l];
+            wlo[g] = Wp16[(((int64_t)w * NG + g) * 2 + 1) * 64 + l];
+        } else {
+            whi[g] = h8v{};
+            wlo[g] = h8v{};
+        }
+    }
+    const int fo = mlp_fimg(l & 31, l >> 5);
+    const int k4 = 4 * l;
+    const int T = (int)((ee - eb + 31) / 32);
+    // lane l (mod 32) of tile j's column / row vectors (clamped: any index is a valid edge)
+    auto tile_t0 = [&](int j) { return eb + 32 * (int64_t)j; };
+    auto tile_nv = [&](int j) { const int64_t r = ee - tile_t0(j); return r <= 0 ? 0 : (r < 32 ? (int)r : 32); };
+    auto edge_of = [&](int j) {
+        const int nv = tile_nv(j);
+        const int li = l & 31;
+        const int64_t e = nv > 0 ? tile_t0(j) + (li < nv ? li : nv - 1) : ee - 1;
+        return e;
+    };
+    float4 kv[RPW], qv[RPW];
+    float cn = 0.f;
+    auto gather = [&](int colv, int rowv) {
+#pragma unroll
+        for (int ii = 0; ii < RPW; ++ii) {
+            const int u = __builtin_amdgcn_readlane(colv, w + NW * ii);
+            const int r = __builtin_amdgcn_readlane(rowv, w + NW * ii);
+            kv[ii] = *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k4);
+            qv[ii] = *reinterpret_cast<const float4*>(Q + (int64_t)r * ldq + k4);
+        }
+        if constexpr (RED == AGG_SYM) cn = norm_col[colv] * norm_row[rowv];   // conv.py:45 operand order
+    };
+    auto stage = [&](int bf, int nv) {
+#pragma unroll
+        for (int ii = 0; ii < RPW; ++ii) {
+            const int i = w + NW * ii;
+            const bool ok = i < nv;
+            float4 a4;
+            a4.x = ok ? act_f<ACT1>(qv[ii].x + kv[ii].x, slope) : 0.f;
+            a4.y = ok ? act_f<ACT1>(qv[ii].y + kv[ii].y, slope) : 0.f;
+            a4.z = ok ? act_f<ACT1>(qv[ii].z + kv[ii].z, slope) : 0.f;
+            a4.w = ok ? act_f<ACT1>(qv[ii].w + kv[ii].w, slope) : 0.f;
+            const float m = wave_max64(fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w))));
+            const int se = mlp_scale_exp(m);
+            const float sc = mlp_pow2(se);
+            const float y[4] = {a4.x * sc, a4.y * sc, a4.z * sc, a4.w * sc};
+            _Float16 hv[4], lv[4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
+            const int g = k4 >> 4, h = (k4 >> 3) & 1, j8 = k4 & 7;
+            char* d = img[bf] + g * 2048 + mlp_fimg(i, h) + j8 * 2;
+            *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
+            *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
+            if (l == 0) sInv[bf][i] = mlp_pow2(-se);
+        }
+        if (w == 0 && l < 32) sC[bf][l] = (l < nv) ? ((RED == AGG_SYM) ? cn : 1.f) : 0.f;
+    };
+
+    int colv0 = col[edge_of(0)], rowv0 = erow[edge_of(0)];
+    int colv1 = col[edge_of(1)], rowv1 = erow[edge_of(1)];
+    int colv2 = col[edge_of(2)], rowv2 = erow[edge_of(2)];
+    gather(colv0, rowv0);
+    stage(0, tile_nv(0));
+    gather(colv1, rowv1);
+    __syncthreads();
+    float racc = 0.f, best = -INFINITY;
+    int bidx = INT_MAX;
+    bool first_run = true;
+    int bf = 0;
+    float* const mw = mt[w];
+    for (int j = 0; j < T; ++j) {
+        const int nv = tile_nv(j);
+        const int64_t t0 = tile_t0(j);
+        mf16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const h8v ahi = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + fo);
+            const h8v alo = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + 1024 + fo);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
+        }
+        stage(bf ^ 1, tile_nv(j + 1));
+        const int colv3 = col[edge_of(j + 3)], rowv3 = erow[edge_of(j + 3)];
+        gather(colv2, rowv2);
+        // ---- m (or c_e m) of this wave's 32 features x the tile's 32 edges -> mw[feature][edge]
+        {
+            const int hb = 4 * (l >> 5);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 iv = *reinterpret_cast<const float4*>(sInv[bf] + 8 * g + hb);
+                float4 o;
+                o.x = act_f<ACT2>(acc[4 * g + 0] * iv.x * iwv + bbv, slope);
+                o.y = act_f<ACT2>(acc[4 * g + 1] * iv.y * iwv + bbv, slope);
+                o.z = act_f<ACT2>(acc[4 * g + 2] * iv.z * iwv + bbv, slope);
+                o.w = act_f<ACT2>(acc[4 * g + 3] * iv.w * iwv + bbv, slope);
+                if constexpr (RED != 3) {
+                    const float4 cv = *reinterpret_cast<const float4*>(sC[bf] + 8 * g + hb);
+                    o.x = cv.x * o.x; o.y = cv.y * o.y; o.z = cv.z * o.z; o.w = cv.w * o.w;
+                }
+                *reinterpret_cast<float4*>(mw + (l & 31) * MP + 8 * g + hb) = o;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): this wave's tile writes done
+        __builtin_amdgcn_wave_barrier();
+        float mv[32];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(mw + (l & 31) * MP + 4 * q);
+            mv[4 * q + 0] = v.x; mv[4 * q + 1] = v.y; mv[4 * q + 2] = v.z; mv[4 * q + 3] = v.w;
+        }
+        const int next_first = (j + 1 < T) ? __builtin_amdgcn_readlane(rowv1, 0) : row_after;
+        // ---- walk the tile's edges in order; a run of equal rows ends where the row changes
+#pragma unroll
+        for (int e = 0; e < 32; ++e) {
+            if (e < nv) {
+                const float v = mv[e];
+                if constexpr (RED == 3) {
+                    const bool take = v > best;           // strict >: the first arg-max edge wins
+                    best = take ? v : best;
+                    bidx = take ? (int)(t0 + e) : bidx;
+                } else {
+                    racc += v;
+                }
+                const int re = __builtin_amdgcn_readlane(rowv0, e);
+                const int rn = (e + 1 < nv) ? __builtin_amdgcn_readlane(rowv0, (e + 1) & 31) : next_first;
+                if (rn != re || (e + 1 == nv && t0 + nv == ee)) {
+                    const bool last_in_block = t0 + e + 1 == ee;
+                    const bool cut0 = first_run && re == row_before;
+                    const bool cut1 = last_in_block && re == row_after;
+                    if (cut0 || cut1) {
+                        const int slot = cut0 ? 2 * b : 2 * b + 1;
+                        if (fo_ok) {
+                            pval[(int64_t)slot * F + n] = RED == 3 ? best : racc;
+                            if constexpr (RED == 3) parg[(int64_t)slot * F + n] = bidx;
+                        }
+                        if (w == 0 && l == 0) prow[slot] = re;
+                    } else if (fo_ok) {
+                        if constexpr (RED == 3) {
+                            const bool any = bidx != INT_MAX;
+                            out[(int64_t)re * ldo + n] = any ? best : 0.f;
+                            arg[(int64_t)re * lda + n] = any ? bidx : -1;
+                        } else {
+                            float vv = racc;
+                            if constexpr (RED == AGG_MEAN) {
+                                const int d = rowptr[re + 1] - rowptr[re];
+                                vv = vv / (float)(d > 1 ? d : 1);
+                            }
+                            out[(int64_t)re * ldo + n] = vv;
+                        }
+                    }
+                    racc = 0.f;
+                    best = -INFINITY;
+                    bidx = INT_MAX;
+                    first_run = false;
+                }
+            }
+        }
+        __syncthreads();
+        colv0 = colv1; rowv0 = rowv1;
+        colv1 = colv2; rowv1 = rowv2;
+        colv2 = colv3; rowv2 = rowv3;
+        bf ^= 1;
+    }
+}
+
+// rows without an edge: out = 0 (and arg = -1 for MAX), as DGL's reduce leaves them
+__global__ void __launch_bounds__(256)
+k_mlp_empty_rows(const int* __restrict__ rowptr, int64_t n_rows, int F, float* __restrict__ out, int64_t ldo,
+                 int* __restrict__ arg, int64_t lda) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_rows || rowptr[r + 1] != rowptr[r]) return;
+    for (int f = threadIdx.x & 63; f < F; f += 64) {
+        out[r * ldo + f] = 0.f;
+        if (arg != nullptr) arg[r * lda + f] = -1;
+    }
+}
+
+// merge the boundary slots of the stream forward: slots in block order, runs of equal row merged (MAX:
+// strict >, the earlier slot = the earlier edges wins ties; sum family: added in slot order)
+template <int RED>
+__global__ void __launch_bounds__(256)
+k_mlp_stream_combine(const float* __restrict__ pval, const int* __restrict__ parg, const int* __restrict__ prow,
+                     int n_slots, int F, const int* __restrict__ rowptr, float* __restrict__ out, int64_t ldo,
+                     int* __restrict__ arg, int64_t lda) {
+    for (int f = threadIdx.x; f < F; f += 256) {
+        int cur = -1, ba = INT_MAX;
+        float bv = 0.f;
+        for (int s = 0; s <= n_slots; ++s) {
+            const int r = s < n_slots ? prow[s] : -2;
+            if (r == -1) continue;
+            if (r != cur) {
+                if (cur >= 0) {
+                    if constexpr (RED == 3) {
+                        out[(int64_t)cur * ldo + f] = ba != INT_MAX ? bv : 0.f;
+                        arg[(int64_t)cur * lda + f] = ba != INT_MAX ? ba : -1;
+                    } else {
+                        float v = bv;
+                        if constexpr (RED == AGG_MEAN) {
+                            const int d = rowptr[cur + 1] - rowptr[cur];
+                            v = v / (float)(d > 1 ? d : 1);
+                        }
+                        out[(int64_t)cur * ldo + f] = v;
+                    }
+                }
+                if (r < 0) break;
+                cur = r;
+                bv = pval[(int64_t)s * F + f];
+                if constexpr (RED == 3) ba = parg[(int64_t)s * F + f];
+            } else {
+                const float v = pval[(int64_t)s * F + f];
+                if constexpr (RED == 3) {
+                    if (v > bv) { bv = v; ba = parg[(int64_t)s * F + f]; }
+                } else {
+                    bv += v;
+                }
+            }
+        }
+    }
+}
+
 // max: combine the chunk partials of split rows in chunk (= edge) order, strict > (first wins)
 __global__ void k_mlp_max_combine(const int4* __restrict__ splits, int F, const float* __restrict__ pval,
                                   const int* __restrict__ parg, float* __restrict__ Y, int64_t ldy,
@@ -1280,6 +1546,54 @@ hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStr
         return hipGetLastError();
     }
     return hipSuccess;
+}
+
+// the stream forward's grid (one 512-thread block per CU) and its boundary-slot workspace
+static int mlp_stream_blocks() {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    return ncu > 1024 ? 1024 : ncu;
+}
+int64_t mlp_stream_work_bytes(int F) {
+    const int64_t slots = 2 * 1024;
+    return slots * F * 8 + slots * 4;
+}
+
+hipError_t run_mlp_fwd_stream(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st) {
+    if (a.n_rows == 0) return hipSuccess;
+    const int nb = mlp_stream_blocks();
+    const int slots = 2 * nb;
+    float* pval = static_cast<float*>(a.work);
+    int* parg = reinterpret_cast<int*>(pval + (int64_t)2 * 1024 * a.F);
+    int* prow = parg + (int64_t)2 * 1024 * a.F;
+    const int FP = (a.F + 31) / 32 * 32;
+    const h8v* w16 = static_cast<const h8v*>(mlp_p16(a.Wp, a.H, a.F));
+    const float* winv = reinterpret_cast<const float*>(reinterpret_cast<const char*>(w16) + (int64_t)FP * mlp_ng(a.H) * 64);
+    hipLaunchKernelGGL(k_mlp_empty_rows, dim3((unsigned)((a.n_rows + 3) / 4)), dim3(256), 0, st, a.rowptr, a.n_rows,
+                       a.F, a.out, a.ldo, red == 3 ? a.arg : nullptr, a.lda);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess || a.n_edges == 0) return err;
+    err = by_acts(act1, act2, [&](auto A1, auto A2) {
+        constexpr int X1 = decltype(A1)::value, X2 = decltype(A2)::value;
+        auto launch = [&](auto R) {
+            constexpr int RV = decltype(R)::value;
+            hipLaunchKernelGGL((k_mlp_fwd16r<X1, X2, RV>), dim3((unsigned)nb), dim3(512), 0, st, a.col, a.erow, a.rowptr,
+                               a.n_edges, a.Q, a.ldq, a.K, a.ldk, a.norm_row, a.norm_col, a.slope, a.F, w16, winv,
+                               a.bias, a.out, a.ldo, a.arg, a.lda, pval, parg, prow);
+            hipLaunchKernelGGL((k_mlp_stream_combine<RV>), dim3(1), dim3(256), 0, st, pval, parg, prow, slots, a.F,
+                               a.rowptr, a.out, a.ldo, a.arg, a.lda);
+            return hipGetLastError();
+        };
+        switch (red) {
+            case AGG_SUM: return launch(std::integral_constant<int, AGG_SUM>());
+            case AGG_MEAN: return launch(std::integral_constant<int, AGG_MEAN>());
+            case AGG_SYM: return launch(std::integral_constant<int, AGG_SYM>());
+            default: return launch(std::integral_constant<int, 3>());
+        }
+    });
+    return err;
 }
 
 // blocks of the backward grid = rows of the destination pass's dW partials: 2048 waves' worth of

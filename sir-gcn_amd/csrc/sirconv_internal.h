@@ -135,7 +135,14 @@ struct EdgeMlpArgs {
     int* parg;                          // split partials (MAX args)
     float* Gm;                          // backward destination pass, MEAN: g / deg rows [rows, F]
     float* wpart;                       // backward destination pass: per-wave partial [dW | db]
+    // edge-stream forward (run_mlp_fwd_stream): the destination row of every dst-CSR edge, sizes, and
+    // the per-block boundary slots (mlp_stream_work_bytes)
+    const int* erow;
+    int64_t n_rows, n_edges;
+    void* work;
 };
+int64_t mlp_stream_work_bytes(int F);
+hipError_t run_mlp_fwd_stream(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st);
 int64_t mlp_pack_floats(int H, int F);
 hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t st);
 hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st);

@@ -65,6 +65,9 @@ SIGNATURES = {
     "sir_edge_mlp_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _I, _I,
                                         _F, _I, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "sir_edge_mlp_bwd_parts": (ctypes.c_int64, [_I64, _I64, _I64]),
+    "sir_edge_mlp_stream_work_bytes": (ctypes.c_int64, [_I64]),
+    "sir_edge_mlp_fwd_stream": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _I, _I,
+                                               _F, _I, _P, _P, _P, _I64, _P, _I64, _P, _P]),
     "sir_edge_max_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
                                             _P, _I64, _I, _F, _P, _P, _I64, _P, _P, _P]),
     "sir_edge_max_bwd_src": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P,

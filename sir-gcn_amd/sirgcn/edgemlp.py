@@ -74,17 +74,43 @@ def _pack(W):
     return packed
 
 
+# the edge-stream forward (sir_edge_mlp_fwd_stream) for H = 256, F <= 256; False: the per-item kernels
+STREAM = True
+
+
+def _edge_rows(csr):
+    """Destination row of every dst-CSR edge (int32, cached on the plan)."""
+    er = getattr(csr, "_erow", None)
+    if er is None:
+        deg = (csr.rowptr[1:] - csr.rowptr[:-1]).long()
+        er = torch.repeat_interleave(torch.arange(csr.n_rows, device=deg.device, dtype=torch.int32), deg)
+        csr._erow = er
+    return er
+
+
 def _fwd(plan, Q, K, W, b, agg, act1, slope, act2, out, arg=None):
     lib = _native.load()
     csr = plan.dst
     Fo, H = W.shape
     in_norm, out_norm = plan.norms(agg if agg != "max" else "sum")
     packed = _pack(W)
+    P = _native._ptr
+    if STREAM and H == 256 and Fo <= 256:
+        E = csr.col.numel()
+        work = torch.empty((lib.sir_edge_mlp_stream_work_bytes(Fo),), dtype=torch.uint8, device=Q.device)
+        code = AGG_MAX if agg == "max" else _native.AGG[agg]
+        with _native._Timed("sir_edge_mlp_fwd", Q.device, 2 * E * H * Fo):
+            rc = lib.sir_edge_mlp_fwd_stream(P(csr.rowptr), P(csr.col) if E else None, P(_edge_rows(csr)) if E else None,
+                                             csr.n_rows, E, H, Fo, P(Q), Q.stride(0), P(K), K.stride(0), P(in_norm),
+                                             P(out_norm), code, act1, float(slope), act2, P(packed), P(b), P(out),
+                                             out.stride(0), P(arg), arg.stride(0) if arg is not None else Fo, P(work),
+                                             _native._stream(Q.device))
+        _native._check(rc, lib)
+        return packed
     n = csr.n_slots
     pval = torch.empty((max(n, 1) * Fo,), device=Q.device, dtype=torch.float32) if n else None
     parg = torch.empty((max(n, 1) * Fo,), device=Q.device, dtype=torch.int32) if (n and arg is not None) else None
     code = AGG_MAX if agg == "max" else _native.AGG[agg]
-    P = _native._ptr
     with _native._Timed("sir_edge_mlp_fwd", Q.device, 2 * csr.col.numel() * H * Fo):
         rc = lib.sir_edge_mlp_fwd(P(csr.rowptr), P(csr.col), P(csr.items), csr.n_items, P(csr.splits), csr.n_splits,
                                   H, Fo, P(Q), Q.stride(0), P(K), K.stride(0), P(in_norm), P(out_norm), code, act1,

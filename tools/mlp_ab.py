@@ -51,22 +51,36 @@ def main():
     act2 = _native.ACT_IDENTITY if a.agg == "max" else _native.ACT_RELU
     P = _native._ptr
     st = _native._stream(torch.device(dev))
-    libs = []
+    libs, stream = [], {}
     for kv in a.libs:
         name, path = kv.split("=", 1)
+        path, _, mode = path.partition("@")        # name=path@stream: the edge-stream entry point
         libs.append((name, open_lib(path)))
+        stream[name] = mode == "stream"
+    from sirgcn.edgemlp import _edge_rows
+    erow = _edge_rows(csr)
     n = csr.n_slots
     pval = torch.empty((max(n, 1) * a.F,), device=dev)
     parg = torch.empty((max(n, 1) * a.F,), device=dev, dtype=torch.int32)
-    outs, packs = {}, {}
+    outs, packs, works = {}, {}, {}
     for name, lib in libs:
         pk = torch.empty((lib.sir_edge_mlp_pack_bytes(a.H, a.F),), dtype=torch.uint8, device=dev)
         assert lib.sir_edge_mlp_pack(P(W), a.H, a.F, P(pk), st) == 0
         packs[name] = pk
         outs[name] = (torch.empty(V, a.F, device=dev), torch.empty(V, a.F, device=dev, dtype=torch.int32))
+        if stream[name]:
+            works[name] = torch.empty((lib.sir_edge_mlp_stream_work_bytes(a.F),), dtype=torch.uint8, device=dev)
 
     def run(name, lib):
         Y, arg = outs[name]
+        if stream[name]:
+            work = works[name]
+            rc = lib.sir_edge_mlp_fwd_stream(P(csr.rowptr), P(csr.col), P(erow), csr.n_rows, csr.col.numel(), a.H, a.F,
+                                             P(Q), Q.stride(0), P(K), K.stride(0), P(in_norm), P(out_norm), code,
+                                             _native.ACT_LEAKY, 0.2, act2, P(packs[name]), P(b), P(Y), Y.stride(0),
+                                             P(arg) if a.agg == "max" else None, a.F, P(work), st)
+            assert rc == 0, lib.sir_last_error()
+            return
         rc = lib.sir_edge_mlp_fwd(P(csr.rowptr), P(csr.col), P(csr.items), csr.n_items, P(csr.splits), csr.n_splits,
                                   a.H, a.F, P(Q), Q.stride(0), P(K), K.stride(0), P(in_norm), P(out_norm), code,
                                   _native.ACT_LEAKY, 0.2, act2, P(packs[name]), P(b), P(Y), Y.stride(0),
@@ -89,8 +103,9 @@ def main():
     for name, _ in libs:
         t = statistics.median(times[name])
         same = torch.equal(outs[name][0], outs[base][0]) and (a.agg != "max" or torch.equal(outs[name][1], outs[base][1]))
+        rel = ((outs[name][0] - outs[base][0]).norm() / outs[base][0].norm()).item()
         print(f"{a.graph} {a.agg} H{a.H} F{a.F} {name:8s} {t:8.3f} ms (min {min(times[name]):8.3f})  "
-              f"{2 * E * a.H * a.F / t / 1e9:7.1f} TFLOP/s fp32-equiv  bit-identical to {base}: {same}", flush=True)
+              f"{2 * E * a.H * a.F / t / 1e9:7.1f} TFLOP/s fp32-equiv  bit-identical to {base}: {same} (relL2 {rel:.1e})", flush=True)
 
 
 if __name__ == "__main__":
