@@ -969,6 +969,12 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
             mv[4 * q + 0] = v.x; mv[4 * q + 1] = v.y; mv[4 * q + 2] = v.z; mv[4 * q + 3] = v.w;
         }
         const int next_first = (j + 1 < T) ? __builtin_amdgcn_readlane(rowv1, 0) : row_after;
+        // run ends of the tile as one ballot (bit e: edge e is the last of its row's run here): the row
+        // changes after it, or the block ends there
+        const int li = l & 31;
+        const int r_next = __shfl(rowv0, (li + 1) & 31);
+        const bool end_l = li < nv && ((li + 1 < nv ? r_next : next_first) != rowv0 || (li + 1 == nv && t0 + nv == ee));
+        const uint32_t bnd = (uint32_t)__builtin_amdgcn_ballot_w64(l < 32 && end_l);
         // ---- walk the tile's edges in order; a run of equal rows ends where the row changes
 #pragma unroll
         for (int e = 0; e < 32; ++e) {
@@ -981,9 +987,8 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
                 } else {
                     racc += v;
                 }
-                const int re = __builtin_amdgcn_readlane(rowv0, e);
-                const int rn = (e + 1 < nv) ? __builtin_amdgcn_readlane(rowv0, (e + 1) & 31) : next_first;
-                if (rn != re || (e + 1 == nv && t0 + nv == ee)) {
+                if ((bnd >> e) & 1u) {
+                    const int re = __builtin_amdgcn_readlane(rowv0, e);
                     const bool last_in_block = t0 + e + 1 == ee;
                     const bool cut0 = first_run && re == row_before;
                     const bool cut1 = last_in_block && re == row_after;
