@@ -470,6 +470,10 @@ edge_wave(int64_t wave, const int* __restrict__ rowptr, const int* __restrict__ 
           typename Stor<ST>::T* __restrict__ out, int64_t ldo, float* __restrict__ partial,
           typename Stor<ST>::T* __restrict__ Gm, int64_t ldgm, uint64_t* __restrict__ mask, const Drop& drop,
           int accumulate = 0) {
+    // MK bit 2 (forward only): the segmented forward's accumulate form (S[v] += this call's sum), a
+    // separate instantiation so that the plain forward carries no read of the old row
+    constexpr int MKB = MK & 3;
+    constexpr bool ACC = (MK & 4) != 0;
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int sub = lane / LPR;
@@ -495,7 +499,7 @@ edge_wave(int64_t wave, const int* __restrict__ rowptr, const int* __restrict__ 
         const int c = li + LPR * j;
 #pragma unroll
         for (int w = 0; w < VW; ++w) { acc[j][w] = 0.f; rv[j][w] = 0.f; gv[j][w] = 0.f; }
-        if (MK != 2 && c < HC) vload_row<ST, VW>(rv[j], rp + c * VW);     // mask-read passes need no Q / K row
+        if (MKB != 2 && c < HC) vload_row<ST, VW>(rv[j], rp + c * VW);     // mask-read passes need no Q / K row
     }
     if constexpr (MODE == MODE_BWD_DST) {
         const auto* gp = G + (int64_t)row * ldg;
@@ -541,35 +545,35 @@ edge_wave(int64_t wave, const int* __restrict__ rowptr, const int* __restrict__ 
 #pragma unroll
                 for (int i = 0; i < U; ++i) uc[i] = __builtin_amdgcn_readlane(vc, i);
                 vc = load_col(e + U);
-                edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC,
+                edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MKB>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC,
                                                                   rv, gv, acc, mask, lane, uc, perm);
             }
         }
     } else {
         for (; e + U <= e1; e += U)
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv,
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, U, MKB>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv,
                                                               acc, mask, lane, nullptr, perm);
     }
     if constexpr (U > 8) {
         if (e + 8 <= e1) {
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 8, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 8, MKB>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
             e += 8;
         }
     }
     if constexpr (U > 4) {
         if (e + 4 <= e1) {
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 4, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 4, MKB>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
             e += 4;
         }
     }
     if constexpr (U > 2) {
         if (e + 2 <= e1) {
-            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 2, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
+            edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 2, MKB>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
             e += 2;
         }
     }
     if (e < e1)
-        edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 1, MK>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
+        edge_batch<ST, MODE, ACT, AGG, LPR, NV, VW, 1, MKB>(e, col, C, ldc, G, ldg, norm_col, nr, slope, li, HC, rv, gv, acc, mask, lane, nullptr, perm);
 
     if (slot < 0) {
         if constexpr (MODE == MODE_FWD && AGG == AGG_MEAN) {
@@ -587,7 +591,7 @@ edge_wave(int64_t wave, const int* __restrict__ rowptr, const int* __restrict__ 
                 for (int j = 0; j < NV; ++j) drop_vec<ST, VW>(drop, row, (li + LPR * j) * VW, acc[j]);
             }
         } else {
-            if (accumulate) {       // segmented forward (sirgcn.dist): S[v] = S[v] + this segment's sum
+            if constexpr (ACC) {    // segmented forward (sirgcn.dist): S[v] = S[v] + this segment's sum
 #pragma unroll
                 for (int j = 0; j < NV; ++j) {
                     const int c = li + LPR * j;
@@ -1280,11 +1284,15 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
     constexpr bool kMaskable = (MODE == MODE_FWD) && kReluFamily;
     if constexpr (kMaskable) {
         if (a.mask_out != nullptr) {
-            hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, 1>), dim3((unsigned)blocks), dim3(256), 0, st,
-                               a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,
-                               cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
-                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out, a.drop,
-                               a.accumulate);
+#define SIR_EDGE_FWD_MASK(MKV)                                                                                       \
+            hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, MKV>), dim3((unsigned)blocks), dim3(256), 0,   \
+                               st, a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,        \
+                               cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,  \
+                               a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, a.mask_out,      \
+                               a.drop, a.accumulate)
+            if (a.accumulate) SIR_EDGE_FWD_MASK(1 | 4);
+            else SIR_EDGE_FWD_MASK(1);
+#undef SIR_EDGE_FWD_MASK
             return hipGetLastError();
         }
     } else {
@@ -1301,11 +1309,19 @@ static hipError_t launch_edge_t(const EdgeArgs& a, hipStream_t st) {
         }
     }
     if (a.mask_in != nullptr) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, 0>), dim3((unsigned)blocks), dim3(256), 0, st,
-                       a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,
-                       cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,
-                       a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr, a.drop,
-                       a.accumulate);
+#define SIR_EDGE_PLAIN(MKV)                                                                                           \
+    hipLaunchKernelGGL((k_edge<ST, MODE, ACT, AGG, LPR, NV, VW, U, MKV>), dim3((unsigned)blocks), dim3(256), 0, st,   \
+                       a.rowptr, a.col, nullptr, reinterpret_cast<const int4*>(a.items), a.n_items,                   \
+                       cp_<ST>(a.R), a.ldr, cp_<ST>(a.C), a.ldc, cp_<ST>(a.G), a.ldg, a.norm_row, a.norm_col,         \
+                       a.slope, a.H, mp_<ST>(a.out), a.ldo, a.partial, mp_<ST>(a.Gm), a.ldgm, nullptr, a.drop,        \
+                       a.accumulate)
+    if constexpr (MODE == MODE_FWD) {
+        if (a.accumulate) SIR_EDGE_PLAIN(4);
+        else SIR_EDGE_PLAIN(0);
+    } else {
+        SIR_EDGE_PLAIN(0);
+    }
+#undef SIR_EDGE_PLAIN
     return hipGetLastError();
 }
 
