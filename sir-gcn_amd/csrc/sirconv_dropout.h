@@ -36,8 +36,11 @@ __host__ __device__ inline void drop_seed_words(Drop& d, uint64_t seed) {
 }
 
 // device: a Drop whose seed words come from `sptr` when set (one load per thread, at kernel start)
+#ifndef SIR_DROP_DEVSEED
+#define SIR_DROP_DEVSEED 1
+#endif
 __device__ __forceinline__ Drop drop_resolve(Drop d) {
-    if (d.on() && d.sptr != nullptr) drop_seed_words(d, *d.sptr);
+    if (SIR_DROP_DEVSEED && d.on() && d.sptr != nullptr) drop_seed_words(d, *d.sptr);
     return d;
 }
 

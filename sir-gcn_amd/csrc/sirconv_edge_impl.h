@@ -1125,7 +1125,9 @@ k_edge_mask(const int* __restrict__ rowptr, const int* __restrict__ col, const i
 // every CU at once, so the dQ pass's VALU work hides under the dK pass's memory time instead of
 // running as a separate launch.  Each wave still runs exactly the single-pass code, so results are
 // bit-identical to the two launches.
-template <int ST, int ACT, int AGG, int NV, int UD, int US>
+// DR: a dropout seed lives in device memory (drop_resolve at the start); a separate instantiation —
+// the resolve code alone made the SYM one-launch backward 5 % slower (profiles/r04_ab_devseed.txt)
+template <int ST, int ACT, int AGG, int NV, int UD, int US, bool DR>
 __global__ void __launch_bounds__(256)
 k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
                  int64_t n_items, float* __restrict__ partial, typename Stor<ST>::T* __restrict__ dQ, int64_t lddq,
@@ -1135,8 +1137,10 @@ k_edge_mask_dual(const int* __restrict__ rowptr, const int* __restrict__ col, co
                  const typename Stor<ST>::T* __restrict__ G, int64_t ldg, const uint64_t* __restrict__ mask,
                  const float* __restrict__ in_norm, const float* __restrict__ out_norm, float slope, int H,
                  Drop drop_q, Drop drop_k) {
-    drop_q = drop_resolve(drop_q);
-    drop_k = drop_resolve(drop_k);
+    if constexpr (DR) {
+        drop_q = drop_resolve(drop_q);
+        drop_k = drop_resolve(drop_k);
+    }
     const int64_t w = __builtin_amdgcn_readfirstlane((int)((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int64_t nmin = n_items < n_items_s ? n_items : n_items_s;
     bool dst;
@@ -1344,12 +1348,16 @@ static hipError_t launch_dual_t(const EdgeArgs& a, const EdgeArgs& b, hipStream_
     constexpr int US = (NV == 1) ? unroll_of<MODE_BWD_SRC, ST>() : (NV == 2 ? 4 : 2);
     const int64_t blocks = (a.n_items + b.n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_edge_mask_dual<ST, ACT, AGG, NV, UD, US>), dim3((unsigned)blocks), dim3(256), 0, st,
-                       a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items, a.partial,
-                       mp_<ST>(a.out), a.ldo,
-                       b.rowptr, b.col, b.perm, reinterpret_cast<const int4*>(b.items), b.n_items, b.partial,
-                       mp_<ST>(b.out), b.ldo, cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H,
-                       a.drop, b.drop);
+#define SIR_DUAL(DRV)                                                                                               \
+    hipLaunchKernelGGL((k_edge_mask_dual<ST, ACT, AGG, NV, UD, US, DRV>), dim3((unsigned)blocks), dim3(256), 0, st,  \
+                       a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), a.n_items, a.partial,              \
+                       mp_<ST>(a.out), a.ldo,                                                                      \
+                       b.rowptr, b.col, b.perm, reinterpret_cast<const int4*>(b.items), b.n_items, b.partial,      \
+                       mp_<ST>(b.out), b.ldo, cp_<ST>(a.G), a.ldg, a.mask_in, a.norm_row, a.norm_col, a.slope, a.H, \
+                       a.drop, b.drop)
+    if (a.drop.sptr != nullptr || b.drop.sptr != nullptr) SIR_DUAL(true);
+    else SIR_DUAL(false);
+#undef SIR_DUAL
     return hipGetLastError();
 }
 
