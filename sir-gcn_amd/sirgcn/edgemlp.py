@@ -21,6 +21,8 @@ form applies.
 """
 import ctypes
 
+import warnings
+
 import torch
 from torch import nn
 import torch.nn.functional as F
@@ -216,7 +218,14 @@ class EdgeMaxLinear(torch.autograd.Function):
         fused = EdgeMaxLinear.fused_bwd
         if fused is None:
             need = E * (2 * H + O) * 4
-            fused = need > min(EdgeMaxLinear.materialised_budget, int(0.4 * torch.cuda.mem_get_info(dev)[0]))
+            # free device memory as the caching allocator sees it: the driver's free bytes plus the
+            # blocks it has reserved but not handed out (a warm training loop holds most memory there)
+            avail = torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+            fused = need > min(EdgeMaxLinear.materialised_budget, int(0.4 * avail))
+            if fused and not max_bwd_fused(H, O):
+                warnings.warn(f"sirgcn max backward: the edge-materialised buffers ({need / 2**30:.1f} GiB) exceed "
+                              f"the budget and the fused backward needs H, O <= 256 (H={H}, O={O}); "
+                              "running the materialised backward anyway")
         if fused and max_bwd_fused(H, O):
             dQK, dW, db = _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope)
             return dQK, dW, (db if ctx.has_b else None), None, None, None, None
