@@ -227,10 +227,11 @@ int sir_edge_gather_add(const int32_t* rowptr, const int32_t* col, const int32_t
 
 /* A[e] = act(Q[row(e)] + K[col[e]]), act = SIR_ACT_IDENTITY / _RELU / _LEAKY_RELU (slope): the
  * materialised max backward's activations in one pass (conv.py:45-47; for the ReLU family sign(A)
- * = sign(z), so sigma' is taken from A and z is never stored).  ABI 12. */
+ * = sign(z), so sigma' is taken from A and z is never stored).  sign_mask (optional, F = 256):
+ * uint64[E][4], bit l of word x = A[e][4 l + x] > 0 — the gate of sir_gemm_nt_dact.  ABI 12. */
 int sir_edge_gather_act(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
                         int64_t F, const float* Q, int64_t ldq, const float* K, int64_t ldk, int act, float slope,
-                        float* A, int64_t lda, void* stream);
+                        float* A, int64_t lda, uint64_t* sign_mask, void* stream);
 
 /* out[row] = sum_{e in row} c_e * X[idx(e)],  idx(e) = perm ? perm[e] : e,
  * c_e = norm_col[col[e]] * norm_row[row] when norm_row != NULL (the sym norm product, conv.py:45),
@@ -410,9 +411,11 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
  * (the activation's input z or output sigma(z): the same sign for the ReLU family); act =
  * SIR_ACT_RELU (gate > 0 ? x : 0) or SIR_ACT_LEAKY_RELU (gate > 0 ? x : x * slope) — torch's
  * threshold / leaky_relu backward fused into the GEMM's epilogue (the materialised max backward's
- * dZ = sigma'(z) * (dM W_R), conv.py:46-47).  ABI 12. */
+ * dZ = sigma'(z) * (dM W_R), conv.py:46-47).  gate_mask (instead of gate, N = 256): the sign
+ * words of sir_edge_gather_act — 32 B per row read instead of the row's gate values.  ABI 12. */
 int sir_gemm_nt_dact(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
-                     const float* gate, int act, float slope, float* C, int64_t ldc, void* stream);
+                     const float* gate, const uint64_t* gate_mask, int act, float slope, float* C, int64_t ldc,
+                     void* stream);
 
 /* Small batches (config 5's 1.6k-node molecule batches): C[M, N] = A[M, K] B^T + bias with the
  * weight read as fp32 straight from W (B[n][k] = W[n*ldw + k], trans = 0, or W[k*ldw + n], trans =

@@ -284,7 +284,7 @@ int sir_edge_gather_add(const int32_t* rowptr, const int32_t* col, const int32_t
 
 int sir_edge_gather_act(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
                         int64_t F, const float* Q, int64_t ldq, const float* K, int64_t ldk, int act, float slope,
-                        float* A, int64_t lda, void* stream) {
+                        float* A, int64_t lda, uint64_t* sign_mask, void* stream) {
     const char* fn = "sir_edge_gather_act";
     int rc = check_generic(fn, n_items, F, items);
     if (rc) return rc;
@@ -295,7 +295,8 @@ int sir_edge_gather_act(const int32_t* rowptr, const int32_t* col, const int32_t
     sir::GenericArgs a{};
     a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.F = (int)F;
     a.X = Q; a.ldx = ldq; a.X2 = K; a.ldx2 = ldk; a.out = A; a.ldo = lda;
-    return finish(fn, sir::run_gather_add(a, static_cast<hipStream_t>(stream), act, slope),
+    if (sign_mask != nullptr && F != 256) return fail(SIR_EUNSUPPORTED, fn, "sign_mask needs F = 256");
+    return finish(fn, sir::run_gather_add(a, static_cast<hipStream_t>(stream), act, slope, sign_mask),
                   "unsupported F / alignment");
 }
 
@@ -646,7 +647,8 @@ int sir_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t K, const void* p
 }
 
 int sir_gemm_nt_dact(const float* A, int64_t lda, int64_t M, int64_t K, const void* packed, int64_t N,
-                     const float* gate, int act, float slope, float* C, int64_t ldc, void* stream) {
+                     const float* gate, const uint64_t* gate_mask, int act, float slope, float* C, int64_t ldc,
+                     void* stream) {
     const char* fn = "sir_gemm_nt_dact";
     if (M < 0 || N <= 0 || K <= 0 || N > 65536 || K > 65536) return fail(SIR_EINVAL, fn, "bad shape");
     if ((M + 255) / 256 * ((N + 127) / 128) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
@@ -654,13 +656,15 @@ int sir_gemm_nt_dact(const float* A, int64_t lda, int64_t M, int64_t K, const vo
         return fail(SIR_EINVAL, fn, "K, N, lda, ldc must be multiples of 4 (lda >= K, ldc >= N)");
     if (lda > SIR_GEMM_MAX_LD || ldc > SIR_GEMM_MAX_LD) return fail(SIR_EINVAL, fn, "lda / ldc too large");
     if (act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU) return fail(SIR_EINVAL, fn, "act must be ReLU or LeakyReLU");
-    if (M > 0 && (A == nullptr || C == nullptr || packed == nullptr || gate == nullptr))
+    if (M > 0 && (A == nullptr || C == nullptr || packed == nullptr || (gate == nullptr && gate_mask == nullptr)))
         return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (gate_mask != nullptr && N != 256) return fail(SIR_EUNSUPPORTED, fn, "gate_mask needs N = 256");
     if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(gate) |
           reinterpret_cast<uintptr_t>(packed)) & 15u) != 0)
         return fail(SIR_EINVAL, fn, "A, C, gate and packed must be 16-B aligned");
     hipError_t err = sir::run_gemm_nt(A, lda, M, (int)K, packed, (int)N, nullptr, C, ldc, static_cast<hipStream_t>(stream),
-                                      sir::Drop(), gate, act == SIR_ACT_RELU ? 1 : 0, slope);
+                                      sir::Drop(), gate_mask != nullptr ? nullptr : gate, act == SIR_ACT_RELU ? 1 : 0,
+                                      slope, gate_mask);
     return finish(fn, err, nullptr);
 }
 

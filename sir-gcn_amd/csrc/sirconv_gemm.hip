@@ -107,6 +107,16 @@ __device__ inline void drop4(const Drop& d, int64_t row, int n, float4& o) {
 __device__ inline float gate_dact(float g, float x, int relu, float slope) {
     return g > 0.f ? x : (relu ? 0.f : x * slope);
 }
+// in place, the sign-bit gate (N = 256; see k_gemm_nt_p GATE 2)
+__global__ void __launch_bounds__(256)
+k_gate_dact_bits(float* __restrict__ C, int64_t ldc, const uint64_t* __restrict__ mask, int64_t M, int relu, float slope) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= M * 256) return;
+    const int64_t r = i >> 8;
+    const int c = (int)(i & 255);
+    const bool pos = (mask[r * 4 + (c & 3)] >> (c >> 2)) & 1u;
+    C[r * ldc + c] = gate_dact(pos ? 1.f : -1.f, C[r * ldc + c], relu, slope);
+}
 // in place: C = sigma'(gate) * C (the gated GEMM's epilogue for the routes without it)
 __global__ void __launch_bounds__(256)
 k_gate_dact(float* __restrict__ C, int64_t ldc, const float* __restrict__ gate, int64_t M, int N, int relu, float slope) {
@@ -558,7 +568,9 @@ constexpr int NT_P_NMAX = 512;
 // LeakyReLU: gate > 0 ? x : x * slope — torch's threshold / leaky_relu backward with the activation's
 // output or input as `gate`: the same sign): the materialised max backward's dZ = sigma'(z) * (dM W_R)
 // in the GEMM's epilogue instead of an [E, H] elementwise pass
-template <int NCT, bool GATE>
+// GATE 2: the gate as sign bits (sir_edge_gather_act's mask: N = 256, 4 words per row, bit l of word
+// x = gate(4 l + x) > 0): 32 B per output row instead of the row's 1 KiB of gate values
+template <int NCT, int GATE>
 __global__ void __launch_bounds__(512)
 k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
@@ -754,7 +766,8 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
         const uint32_t ldc4 = (uint32_t)ldc * 4u;
         const uint32_t nrec = (uint32_t)p.rows * ldc4;
         const rsrc_t crs = mk_rsrc(C + p.d0 * ldc, (SIR_ABL_NT & 2) ? 0u : nrec);
-        const rsrc_t grs = mk_rsrc(GATE ? gate + p.d0 * ldc : C, GATE ? nrec : 0u);
+        const rsrc_t grs = GATE == 2 ? mk_rsrc(reinterpret_cast<const char*>(gate) + p.d0 * 32, (uint32_t)p.rows * 32u)
+                                     : mk_rsrc(GATE ? gate + p.d0 * ldc : C, GATE ? nrec : 0u);
         const float* sc = fin + slot * BD;
         char* const wrow = img + ((wq / WF) * 32 + rq) * PITCH + (f_wq + 4 * hq) * 4;
 #pragma unroll
@@ -784,7 +797,19 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
                 const int ml = (ir >> 5) * (TDT * 32) + 32 * b + (ir & 31);
                 const int n = p.f0 + 4 * c16;
                 const uint32_t off = (n < N) ? (uint32_t)ml * ldc4 + (uint32_t)c16 * 16u : nrec;
-                if constexpr (GATE) {
+                if constexpr (GATE == 2) {          // N = 256, f0 = 0: lane c16's 4 features 4 c16 + x
+                    const u4v m01 = __builtin_amdgcn_raw_buffer_load_b128(grs, (uint32_t)ml * 32u, 0, 0);
+                    const u4v m23 = __builtin_amdgcn_raw_buffer_load_b128(grs, (uint32_t)ml * 32u + 16u, 0, 0);
+                    const int sh = c16 & 31;
+                    const uint32_t w0 = c16 < 32 ? m01.x : m01.y, w1 = c16 < 32 ? m01.z : m01.w;
+                    const uint32_t w2 = c16 < 32 ? m23.x : m23.y, w3 = c16 < 32 ? m23.z : m23.w;
+                    const float g0 = ((w0 >> sh) & 1u) ? 1.f : -1.f, g1 = ((w1 >> sh) & 1u) ? 1.f : -1.f;
+                    const float g2 = ((w2 >> sh) & 1u) ? 1.f : -1.f, g3 = ((w3 >> sh) & 1u) ? 1.f : -1.f;
+                    v.x = __float_as_uint(gate_dact(g0, __uint_as_float(v.x), gate_relu, gate_slope));
+                    v.y = __float_as_uint(gate_dact(g1, __uint_as_float(v.y), gate_relu, gate_slope));
+                    v.z = __float_as_uint(gate_dact(g2, __uint_as_float(v.z), gate_relu, gate_slope));
+                    v.w = __float_as_uint(gate_dact(g3, __uint_as_float(v.w), gate_relu, gate_slope));
+                } else if constexpr (GATE == 1) {
                     const u4v gv = __builtin_amdgcn_raw_buffer_load_b128(grs, off, p.f0 * 4, 0);
                     v.x = __float_as_uint(gate_dact(__uint_as_float(gv.x), __uint_as_float(v.x), gate_relu, gate_slope));
                     v.y = __float_as_uint(gate_dact(__uint_as_float(gv.y), __uint_as_float(v.y), gate_relu, gate_slope));
@@ -1813,9 +1838,10 @@ hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, v
 
 hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
                        const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop, const float* gate,
-                       int gate_relu, float gate_slope) {
+                       int gate_relu, float gate_slope, const uint64_t* gate_mask) {
     if (M == 0 || N == 0) return hipSuccess;
-    if (gate != nullptr) {     // fused in k_gemm_nt_p's epilogue; any other route applies it afterwards
+    if (gate_mask != nullptr && N != 256) return hipErrorInvalidValue;
+    if (gate != nullptr || gate_mask != nullptr) {   // fused in k_gemm_nt_p's epilogue; other routes: afterwards
         const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
         if (M >= gemm_small_rows() && N > 128 && np <= NT_P_NMAX && K % KC == 0 && (kc == 4 || kc == 8 || kc == 16)) {
             const u4v* wp = static_cast<const u4v*>(packed);
@@ -1830,17 +1856,28 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
             if (ntiles < (int64_t)1 << 30) {
                 const int tpb = (int)((ntiles + ncu - 1) / ncu);
                 const int nblk = (int)((ntiles + tpb - 1) / tpb);
-                auto kern = kc == 4 ? k_gemm_nt_p<4, true> : (kc == 8 ? k_gemm_nt_p<8, true> : k_gemm_nt_p<16, true>);
-                hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, ldc,
-                                   nft, (int)ntiles, tpb, drop, gate, gate_relu, gate_slope);
+                if (gate_mask != nullptr) {
+                    auto kern = kc == 4 ? k_gemm_nt_p<4, 2> : (kc == 8 ? k_gemm_nt_p<8, 2> : k_gemm_nt_p<16, 2>);
+                    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C,
+                                       ldc, nft, (int)ntiles, tpb, drop, reinterpret_cast<const float*>(gate_mask),
+                                       gate_relu, gate_slope);
+                } else {
+                    auto kern = kc == 4 ? k_gemm_nt_p<4, 1> : (kc == 8 ? k_gemm_nt_p<8, 1> : k_gemm_nt_p<16, 1>);
+                    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C,
+                                       ldc, nft, (int)ntiles, tpb, drop, gate, gate_relu, gate_slope);
+                }
                 return hipGetLastError();
             }
         }
-        hipError_t err = run_gemm_nt(A, lda, M, K, packed, N, bias, C, ldc, st, drop, nullptr, 0, 0.f);
+        hipError_t err = run_gemm_nt(A, lda, M, K, packed, N, bias, C, ldc, st, drop, nullptr, 0, 0.f, nullptr);
         if (err != hipSuccess) return err;
         const int64_t cnt = M * N;
-        hipLaunchKernelGGL(k_gate_dact, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, C, ldc, gate, M, N,
-                           gate_relu, gate_slope);
+        if (gate_mask != nullptr)
+            hipLaunchKernelGGL(k_gate_dact_bits, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, C, ldc, gate_mask, M,
+                               gate_relu, gate_slope);
+        else
+            hipLaunchKernelGGL(k_gate_dact, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, C, ldc, gate, M, N,
+                               gate_relu, gate_slope);
         return hipGetLastError();
     }
     const int np = (int)gemm_pack_npad(N), kc = (K + KC - 1) / KC;
@@ -1882,7 +1919,7 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
         if (ntiles < (int64_t)1 << 30) {
             const int tpb = (int)((ntiles + ncu - 1) / ncu);
             const int nblk = (int)((ntiles + tpb - 1) / tpb);
-            auto kern = kc == 4 ? k_gemm_nt_p<4, false> : (kc == 8 ? k_gemm_nt_p<8, false> : k_gemm_nt_p<16, false>);
+            auto kern = kc == 4 ? k_gemm_nt_p<4, 0> : (kc == 8 ? k_gemm_nt_p<8, 0> : k_gemm_nt_p<16, 0>);
             hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, ldc,
                                nft, (int)ntiles, tpb, drop, nullptr, 0, 0.f);
             return hipGetLastError();

@@ -52,11 +52,13 @@ __device__ __forceinline__ int64_t wave_id() {
 
 // ---------------------------------------------------------------------------------------- gather
 // ACT: ACT_IDENTITY (Z = the sum), ACT_RELU / ACT_LEAKY (A = sigma of it: torch's relu / leaky_relu)
-template <int NV, int VW, int ACT>
+// SM: also the sign bits of the 256 features of each edge (F = 256, one float4 per lane): 4 words per
+// edge, bit l of word x = (value of feature 4 l + x) > 0 — one ballot per word (sir_gemm_nt_dact's gate)
+template <int NV, int VW, int ACT, bool SM>
 __global__ void __launch_bounds__(256)
 k_gather_add(const int* __restrict__ col, const int4* __restrict__ items, int64_t n_items, int F,
              const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
-             float* __restrict__ Z, int64_t ldz, float slope) {
+             float* __restrict__ Z, int64_t ldz, float slope, uint64_t* __restrict__ smask) {
     const int64_t w = wave_id();
     if (w >= n_items) return;
     const Item it = load_item(items, w);
@@ -81,6 +83,12 @@ k_gather_add(const int* __restrict__ col, const int4* __restrict__ items, int64_
                     k[x] = q[j][x] + k[x];                                 // eq[v] + ek[u] (conv.py:45)
                     if constexpr (ACT == ACT_RELU) k[x] = k[x] > 0.f ? k[x] : 0.f;
                     else if constexpr (ACT == ACT_LEAKY) k[x] = k[x] > 0.f ? k[x] : k[x] * slope;
+                }
+                if constexpr (SM) {
+                    uint64_t b[VW];
+#pragma unroll
+                    for (int x = 0; x < VW; ++x) b[x] = __builtin_amdgcn_ballot_w64(k[x] > 0.f);
+                    if (lane < VW) smask[(int64_t)e * VW + lane] = lane == 0 ? b[0] : lane == 1 ? b[1 % VW] : lane == 2 ? b[2 % VW] : b[3 % VW];
                 }
                 st<VW>(Z + (int64_t)e * ldz + c * VW, k);
             }
@@ -356,22 +364,31 @@ bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p
 
 }  // namespace
 
-hipError_t run_gather_add(const GenericArgs& a, hipStream_t st, int act, float slope) {
+hipError_t run_gather_add(const GenericArgs& a, hipStream_t st, int act, float slope, uint64_t* smask) {
     GShape s;
     const bool v4 = al16(a.X) && al16(a.X2) && al16(a.out) && a.ldx % 4 == 0 && a.ldx2 % 4 == 0 && a.ldo % 4 == 0;
     if (!gshape(a.F, v4, &s)) return hipErrorInvalidValue;
     if (act != ACT_IDENTITY && act != ACT_RELU && act != ACT_LEAKY) return hipErrorInvalidValue;
+    if (smask != nullptr && !(a.F == 256 && s.nv == 1 && s.vw == 4)) return hipErrorInvalidValue;
     if (a.n_items == 0) return hipSuccess;
     gdispatch(s, [&](auto nv_, auto vw_) {
         constexpr int NV_ = decltype(nv_)::value, VW_ = decltype(vw_)::value;
         const dim3 grid(blocks_for(a.n_items));
-#define SIR_GATHER(ACTV)                                                                                        \
-        hipLaunchKernelGGL((k_gather_add<NV_, VW_, ACTV>), grid, dim3(256), 0, st, a.col,                       \
+#define SIR_GATHER(ACTV, SMV)                                                                                   \
+        hipLaunchKernelGGL((k_gather_add<NV_, VW_, ACTV, SMV>), grid, dim3(256), 0, st, a.col,                  \
                            reinterpret_cast<const int4*>(a.items), a.n_items, a.F, a.X, a.ldx, a.X2, a.ldx2, a.out, \
-                           a.ldo, slope)
-        if (act == ACT_RELU) SIR_GATHER(ACT_RELU);
-        else if (act == ACT_LEAKY) SIR_GATHER(ACT_LEAKY);
-        else SIR_GATHER(ACT_IDENTITY);
+                           a.ldo, slope, smask)
+        if constexpr (NV_ == 1 && VW_ == 4) {
+            if (smask != nullptr) {
+                if (act == ACT_RELU) SIR_GATHER(ACT_RELU, true);
+                else if (act == ACT_LEAKY) SIR_GATHER(ACT_LEAKY, true);
+                else SIR_GATHER(ACT_IDENTITY, true);
+                return;
+            }
+        }
+        if (act == ACT_RELU) SIR_GATHER(ACT_RELU, false);
+        else if (act == ACT_LEAKY) SIR_GATHER(ACT_LEAKY, false);
+        else SIR_GATHER(ACT_IDENTITY, false);
 #undef SIR_GATHER
     });
     return hipGetLastError();

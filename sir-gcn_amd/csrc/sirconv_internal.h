@@ -79,7 +79,8 @@ struct GenericArgs {
     int* parg;
 };
 
-hipError_t run_gather_add(const GenericArgs& a, hipStream_t st, int act = ACT_IDENTITY, float slope = 0.f);
+hipError_t run_gather_add(const GenericArgs& a, hipStream_t st, int act = ACT_IDENTITY, float slope = 0.f,
+                          uint64_t* smask = nullptr);
 hipError_t run_seg_sum(const GenericArgs& a, hipStream_t st);
 hipError_t run_edge_bcast(const GenericArgs& a, hipStream_t st);
 hipError_t run_seg_max(const GenericArgs& a, hipStream_t st);
@@ -154,7 +155,8 @@ int64_t gemm_pack_bytes(int64_t N, int64_t K);
 hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st);
 hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void* packed, int N,
                        const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop = Drop(),
-                       const float* gate = nullptr, int gate_relu = 0, float gate_slope = 0.f);
+                       const float* gate = nullptr, int gate_relu = 0, float gate_slope = 0.f,
+                       const uint64_t* gate_mask = nullptr);
 hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int trans,
                               int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop);
 int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc);

@@ -33,7 +33,7 @@ SIGNATURES = {
     "sir_graph_norm_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I64,
                                           _P, _P, _P, _P]),
     "sir_edge_gather_add": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P]),
-    "sir_edge_gather_act": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _I64, _P]),
+    "sir_edge_gather_act": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _I64, _P, _P]),
     "sir_segment_sum": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64,
                                        _P, _P]),
     "sir_edge_broadcast": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64, _P]),
@@ -45,7 +45,7 @@ SIGNATURES = {
     "sir_gemm_pack_bytes": (ctypes.c_int64, [_I64, _I64]),
     "sir_gemm_pack": (ctypes.c_int, [_P, _I64, _I64, _I64, _I, _P, _P]),
     "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P, _P]),
-    "sir_gemm_nt_dact": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _I, _F, _P, _I64, _P]),
+    "sir_gemm_nt_dact": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I, _F, _P, _I64, _P]),
     "sir_gemm_nt_direct": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, ctypes.c_int, _I64, _P, _P, _I64, _P, _P]),
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
     "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
@@ -327,14 +327,15 @@ def edge_gather_add(csr, Q, K, Z):
     _check(rc, lib)
 
 
-def edge_gather_act(csr, Q, K, act, slope, A):
-    """A[e] = act(Q[row(e)] + K[col[e]]) for act in {identity, ReLU, LeakyReLU} (dst-CSR edge order)."""
+def edge_gather_act(csr, Q, K, act, slope, A, sign_mask=None):
+    """A[e] = act(Q[row(e)] + K[col[e]]) for act in {identity, ReLU, LeakyReLU} (dst-CSR edge order);
+    ``sign_mask`` (int64 [E, 4], F = 256): bit l of word x = A[e][4 l + x] > 0."""
     lib = load()
     F = A.shape[1]
     with _Timed("sir_edge_gather_act", A.device):
         rc = lib.sir_edge_gather_act(_ptr(csr.rowptr), _ptr(csr.col), _ptr(csr.items), csr.n_items, F,
                                      _ptr(Q), _ld(Q, F), _ptr(K), _ld(K, F), int(act), float(slope), _ptr(A),
-                                     _ld(A, F), _stream(A.device))
+                                     _ld(A, F), _ptr(sign_mask), _stream(A.device))
     _check(rc, lib)
 
 
@@ -470,19 +471,23 @@ def gemm_nt(A, packed, bias=None, out=None, drop=None):
     return out
 
 
-def gemm_nt_dact(A, packed, gate, act, slope, out=None):
+def gemm_nt_dact(A, packed, gate, act, slope, out=None, gate_mask=None):
     """C = sigma'(gate) * (A B^T) (``sir_gemm_nt_dact``: the ReLU family's backward in the GEMM epilogue;
-    ``gate`` = the activation's input or output, C's shape and leading dimension)."""
+    ``gate`` = the activation's input or output, C's shape and leading dimension, or ``gate_mask`` =
+    its sign words from ``edge_gather_act``, N = 256)."""
     lib = load()
     pk, N, K = packed
     M = A.shape[0]
     assert A.dim() == 2 and A.shape[1] == K and A.stride(1) == 1
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    assert gate.shape == out.shape and gate.stride() == out.stride()
-    with _Timed(f"sir_gemm_nt_dact K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + 2 * N))):
-        rc = lib.sir_gemm_nt_dact(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(gate), int(act), float(slope),
-                                  _ptr(out), out.stride(0), _stream(A.device))
+    if gate_mask is None:
+        assert gate.shape == out.shape and gate.stride() == out.stride()
+    else:
+        assert N == 256 and gate_mask.numel() == 4 * M
+    with _Timed(f"sir_gemm_nt_dact K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + N))):
+        rc = lib.sir_gemm_nt_dact(_ptr(A), A.stride(0), M, K, _ptr(pk), N, _ptr(gate) if gate_mask is None else None,
+                                  _ptr(gate_mask), int(act), float(slope), _ptr(out), out.stride(0), _stream(A.device))
     _check(rc, lib)
     return out
 

@@ -233,9 +233,12 @@ class EdgeMaxLinear(torch.autograd.Function):
         # forward).  ReLU family: A = sigma(z) straight from the gather (sign(A) = sign(z), so sigma' is
         # read off A below and z is never stored); other sigmas: z, then sigma(z)
         relu_family = act1 in (_native.ACT_RELU, _native.ACT_LEAKY)
+        smask = None
         if relu_family:
             A = torch.empty((E, H), device=dev, dtype=torch.float32)
-            _native.edge_gather_act(plan.dst, QK[:, :H], QK[:, H:], act1, slope, A)
+            if H == 256:            # sign words for the gated GEMM: 32 B per edge instead of A's 1 KiB
+                smask = torch.empty((E, 4), device=dev, dtype=torch.int64)
+            _native.edge_gather_act(plan.dst, QK[:, :H], QK[:, H:], act1, slope, A, sign_mask=smask)
             Z = A
         else:
             Z = torch.empty((E, H), device=dev, dtype=torch.float32)
@@ -245,7 +248,7 @@ class EdgeMaxLinear(torch.autograd.Function):
         _native.segment_max_bwd(plan.dst, arg, dY, dM)                 # dY to the first arg-max edge
         dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
         if relu_family:     # dZ = sigma'(z) * (dM W_R) with sigma' read off A in the GEMM's epilogue
-            dZ = linalg.mm_w_dact(dM, W, A, act1, slope)
+            dZ = linalg.mm_w_dact(dM, W, A, act1, slope, gate_mask=smask)
             del A, Z, dM
         else:
             del A

@@ -77,13 +77,14 @@ def mm_w(A, W):
     return torch.mm(A, W)
 
 
-def mm_w_dact(A, W, gate, act, slope):
+def mm_w_dact(A, W, gate, act, slope, gate_mask=None):
     """sigma'(gate) * (A W) for the ReLU family (W [K, N]; ``gate`` the activation's input or output,
-    same sign): native with the activation backward in the GEMM epilogue when the operands allow,
-    else torch's mm + threshold / leaky_relu backward."""
+    same sign; ``gate_mask``: its sign words, N = 256): native with the activation backward in the
+    GEMM epilogue when the operands allow, else torch's mm + threshold / leaky_relu backward."""
     if (USE_NATIVE and _ok(A) and _w_ok(W, W.shape[1]) and _ok(gate) and gate.shape == (A.shape[0], W.shape[1])
             and gate.stride(0) == W.shape[1]):
-        return _native.gemm_nt_dact(A, _native.gemm_pack(W.contiguous(), trans=True), gate, act, slope)
+        mask = gate_mask if W.shape[1] == 256 else None
+        return _native.gemm_nt_dact(A, _native.gemm_pack(W.contiguous(), trans=True), gate, act, slope, gate_mask=mask)
     g = torch.mm(A, W)
     if act == _native.ACT_RELU:
         return torch.ops.aten.threshold_backward(g, gate, 0.0)

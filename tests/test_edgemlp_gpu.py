@@ -282,9 +282,18 @@ def test_edge_gather_act_bit_exact(act, slope, H):
     QK = torch.randn(V, 2 * H, generator=gen).to(DEV)
     E = plan.dst.col.numel()
     A = torch.empty(E, H, device=DEV)
-    _native.edge_gather_act(plan.dst, QK[:, :H], QK[:, H:], act, slope, A)
+    smask = torch.empty(E, 4, device=DEV, dtype=torch.int64) if H == 256 else None
+    _native.edge_gather_act(plan.dst, QK[:, :H], QK[:, H:], act, slope, A, sign_mask=smask)
     rows = torch.repeat_interleave(torch.arange(V, device=DEV), (plan.dst.rowptr[1:] - plan.dst.rowptr[:-1]).long())
     z = QK[rows, :H] + QK[plan.dst.col.long(), H:]
     ref = {_native.ACT_RELU: torch.relu, _native.ACT_LEAKY: lambda t: torch.nn.functional.leaky_relu(t, slope),
            _native.ACT_IDENTITY: lambda t: t}[act](z)
     assert torch.equal(A, ref)
+    if smask is not None:                   # bit l of word x = A[e][4 l + x] > 0
+        assert torch.equal(smask, sign_words(ref))
+
+
+def sign_words(A):
+    """int64 [E, 4]: bit l of word x = A[:, 4 l + x] > 0 (sir_edge_gather_act's sign mask, H = 256)."""
+    bits = (A > 0).reshape(A.shape[0], 64, 4).permute(0, 2, 1).long()
+    return (bits << torch.arange(64, device=A.device)).sum(-1)

@@ -438,3 +438,8 @@ def test_gemm_nt_dact_equals_gemm_then_activation_backward(M, K, N, act, slope):
     ref = (torch.ops.aten.threshold_backward(ref, gate, 0.0) if act == _native.ACT_RELU
            else torch.ops.aten.leaky_relu_backward(ref, gate, slope, False))
     assert torch.equal(got, ref)
+    if N == 256:                            # the gate as sign words (sir_edge_gather_act's mask)
+        bits = (gate > 0).reshape(M, 64, 4).permute(0, 2, 1).long()
+        words = (bits << torch.arange(64, device="cuda")).sum(-1).contiguous()
+        got_m = linalg.mm_w_dact(A, W, gate, act, slope, gate_mask=words)
+        assert torch.equal(got_m, ref)
