@@ -81,12 +81,20 @@ def all_reduce_sum(t, group=None):
         dist.all_reduce(t, group=group)
 
 
-def partition_rows(in_deg, world):
-    """Row boundaries [0, r_1, ..., V] with ≈E/world in-edges per range (edge-balanced)."""
+# per-row cost of the edge-cut layer in units of one in-edge: the node-row work (the five projection
+# GEMMs, the halo packing, the dK completion: ~4 ns per row at H = 256) against the edge passes'
+# ~0.32 ns per edge (the S2 profile, tools/dist_model.py) — an edge-only cut left the slowest rank
+# of S2 at 8 ranks with 8 % more rows than the mean
+ROW_WEIGHT = 12
+
+
+def partition_rows(in_deg, world, row_weight=ROW_WEIGHT):
+    """Row boundaries [0, r_1, ..., V] with ≈equal cost per range, cost = in-edges + row_weight per row
+    (row_weight 0: edge-balanced)."""
     in_deg = in_deg.cpu()                  # plan time: a few host syncs, any device
     V = in_deg.numel()
-    E = int(in_deg.sum().item())
-    cum = torch.cumsum(in_deg.to(torch.int64), 0)
+    cum = torch.cumsum(in_deg.to(torch.int64) + int(row_weight), 0)
+    E = int(cum[-1].item()) if V else 0
     bounds = [0]
     for p in range(1, world):
         target = (E * p + world - 1) // world
