@@ -120,18 +120,22 @@ def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg, fused, chu
             assert_close(p["grads"][n], ref[k], 1e-5, f"{n}")
 
 
-def test_partition_rows_balances_edges():
+@pytest.mark.parametrize("row_weight", [0, 12])
+def test_partition_rows_balances_cost(row_weight):
+    """Contiguous row ranges with equal cost = in-edges + row_weight per row, to within one row."""
     from sirgcn.dist import partition_rows
     from sirgcn.synth import powerlaw_edges
     V, E = 10_000, 200_000
     _, dst = powerlaw_edges(V, E, 0.8, seed=1)
     deg = torch.bincount(dst, minlength=V)
+    cost = deg + row_weight
+    total = int(cost.sum())
     for world in (1, 2, 4, 8):
-        b = partition_rows(deg, world)
+        b = partition_rows(deg, world, row_weight=row_weight)
         assert b[0] == 0 and b[-1] == V and all(b[i] <= b[i + 1] for i in range(world))
-        loads = [int(deg[b[i]:b[i + 1]].sum()) for i in range(world)]
-        assert sum(loads) == E
-        assert max(loads) <= E / world + int(deg.max())
+        loads = [int(cost[b[i]:b[i + 1]].sum()) for i in range(world)]
+        assert sum(loads) == total
+        assert max(loads) <= total / world + int(cost.max())
 
 
 @pytest.mark.parametrize("world,agg", [(2, "sum"), (3, "sym"), (4, "mean")])
