@@ -1370,170 +1370,6 @@ k_gemm_nt_s(const float* __restrict__ A, int64_t lda, int64_t M, int K, const u4
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// k_gemm_nt_ws: the weight-stationary NT GEMM of the node-row projections (QK, Y, G, dX at
-// K = 128 / 256 / 512).  The packed weight of a SLAB of NB = 32 NTF features (NB x K x hi/lo fp16
-// = 128 KiB) is staged in LDS once per block — the only barrier of the kernel — and stays there
-// while the block's 8 waves stream data rows past it; a wave owns 32 NTD data rows x the slab,
-// loads its rows' fp32 values straight into the MFMA operand registers (k_gemm_nt_s's fragment
-// loads, two 32-k chunks in flight), splits them in registers, and reads the weight fragments from
-// LDS in lane order (conflict-free ds_read_b128).  No A image in LDS, no per-step barrier: the
-// waves run independently, so one wave's loads, split and epilogue overlap the other waves' MFMAs.
-// The N / NB slabs of a row tile are taken by blocks b, b + 8, ... (the same XCD: dispatch is
-// round-robin over the 8 XCDs) walking the same rows in the same order, so the rows a slab block
-// reads after its sibling come from L2 / the Infinity Cache.  Same chunks, running-scale rule, MFMA
-// order per accumulator and epilogue arithmetic as k_gemm_nt_p: bit-identical results.
-#ifndef SIR_NT_WS
-#define SIR_NT_WS 0             // the default route (env SIR_NT_WS_MODE): 0 k_gemm_nt_p, 1 / 2 k_gemm_nt_ws with 32 / 64 rows per wave
-#endif
-constexpr int WS_SLAB_BYTES = 131072;
-#ifndef WS_NS
-#define WS_NS 2
-#endif
-
-template <int NCH, int NTF, int NTD>
-__global__ void __launch_bounds__(512)
-k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
-             const float* __restrict__ inv_t, const float* __restrict__ bias, int N, float* __restrict__ C,
-             int64_t ldc, int n_slabs, int64_t n_wt, int64_t wt_per_group, Drop drop) {
-    drop = drop_resolve(drop);
-    constexpr int NB = 32 * NTF;
-    constexpr int PLANE = NB * 32;                  // bytes of one (chunk, part, k16 step) plane of the slab
-    constexpr int WB = NCH * 4 * PLANE;
-    static_assert(WB <= WS_SLAB_BYTES, "the weight slab fits the LDS");
-    __shared__ __attribute__((aligned(16))) char wl[WB];
-    const int bid = blockIdx.x;
-    const int slab = (bid >> 3) % n_slabs;
-    const int64_t group = (bid & 7) + 8 * (bid / (8 * n_slabs));
-    const int f0 = slab * NB;
-    // plane q = (c * 2 + part) * 2 + ks of the packed weight holds Npad rows in fimg order; the
-    // slab's rows f0 .. f0 + NB - 1 are PLANE contiguous bytes of it (f0 % 32 == 0)
-    for (int i = threadIdx.x; i < WB / 16; i += 512) {
-        const int q = i / (PLANE / 16), o = i % (PLANE / 16);
-        reinterpret_cast<u4v*>(wl)[i] = Wp[(int64_t)q * Npad * 2 + f0 * 2 + o];
-    }
-    __syncthreads();
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, h = l >> 5;
-    const int64_t g0 = group * wt_per_group;
-    const int64_t g1 = (g0 + wt_per_group < n_wt) ? g0 + wt_per_group : n_wt;
-    const char* const wlane = wl + 16 * l;
-    for (int64_t wt = g0 + w; wt < g1; wt += 8) {
-        const int64_t d0 = wt * 32 * NTD;
-        const int rows = (M - d0 < 32 * NTD) ? (int)(M - d0) : 32 * NTD;
-        const rsrc_t ars = mk_rsrc(A + d0 * lda, (uint32_t)((int64_t)rows * lda * 4));
-        float4 av[WS_NS][NTD][4];                   // [set][row tile][ks * 2 + q]: k = 32c + 16ks + 8h + 4q + (0..3)
-        auto load = [&](int set, int c) {
-#pragma unroll
-            for (int b = 0; b < NTD; ++b)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const u4v u = __builtin_amdgcn_raw_buffer_load_b128(
-                        ars, ((32 * b + r) * (int)lda + 8 * h + (i >> 1) * 16 + (i & 1) * 4) * 4, c * KC * 4, 0);
-                    av[set][b][i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
-                                                __uint_as_float(u.w));
-                }
-        };
-        f16v acc[NTF][NTD];
-        int se_run[NTD];
-        auto chunk = [&](int set, int c, bool first) {
-            h8 dh[NTD][2], dl[NTD][2];
-#pragma unroll
-            for (int b = 0; b < NTD; ++b) {
-                float m = 0.f;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) m = fmax4(m, av[set][b][i]);
-                m = fmaxf(m, __shfl_xor(m, 32));
-                const int se_old = first ? SE_INIT : se_run[b], se = next_se(se_old, bexp(m));
-                se_run[b] = se;
-                if (first) {
-#pragma unroll
-                    for (int a = 0; a < NTF; ++a)
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
-                } else {
-                    const float f = pow2(se - se_old);
-                    if (__builtin_amdgcn_ballot_w64(f != 1.f) != 0) {
-#pragma unroll
-                        for (int a = 0; a < NTF; ++a) acc[a][b] *= f;
-                    }
-                }
-                const float s = pow2(se);
-                split8(av[set][b][0], av[set][b][1], s, dh[b][0], dl[b][0]);
-                split8(av[set][b][2], av[set][b][3], s, dh[b][1], dl[b][1]);
-            }
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                h8 whi[NTF], wlo[NTF];
-#pragma unroll
-                for (int a = 0; a < NTF; ++a) {
-                    whi[a] = *reinterpret_cast<const h8*>(wlane + ((c * 2 + 0) * 2 + ks) * PLANE + a * 1024);
-                    wlo[a] = *reinterpret_cast<const h8*>(wlane + ((c * 2 + 1) * 2 + ks) * PLANE + a * 1024);
-                }
-#pragma unroll
-                for (int a = 0; a < NTF; ++a)
-#pragma unroll
-                    for (int b = 0; b < NTD; ++b) {
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(whi[a], dh[b][ks], acc[a][b], 0, 0, 0);
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(whi[a], dl[b][ks], acc[a][b], 0, 0, 0);
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wlo[a], dh[b][ks], acc[a][b], 0, 0, 0);
-                    }
-            }
-        };
-        // chunk pairs with static register sets; the last pair re-issues the last chunk's loads
-        // (same addresses, unused) so the wait counts stay exact (k_gemm_nt_s)
-        // WS_NS register sets: WS_NS - 1 chunks in flight ahead of the one being multiplied
-#pragma unroll
-        for (int j = 0; j + 1 < WS_NS; ++j) load(j, j);
-#pragma unroll 1
-        for (int c = 0; c < NCH; c += WS_NS) {
-#pragma unroll
-            for (int j = 0; j < WS_NS; ++j) {
-                const int cn = c + j + WS_NS - 1;
-                load((j + WS_NS - 1) % WS_NS, cn < NCH ? cn : NCH - 1);
-                chunk(j, c + j, c + j == 0);
-            }
-        }
-        // C[m][n] = acc * 2^-se(m) * inv_t[n] + bias[n]; rows past M / columns past N are dropped by
-        // the store's range (an offset at the end of it)
-        int tq = threadIdx.x;                       // opaque copy: no lane index held across the loop
-        asm volatile("" : "+v"(tq));
-        const int lq = tq & 63, rq = lq & 31, hq = lq >> 5;
-        const uint32_t ldc4 = (uint32_t)ldc * 4u;
-        const uint32_t nrec = (uint32_t)rows * ldc4;
-        const rsrc_t crs = mk_rsrc(C + d0 * ldc, nrec);
-#pragma unroll
-        for (int b = 0; b < NTD; ++b) {
-            const float is = pow2(-se_run[b]);
-            const uint32_t rb = (uint32_t)(32 * b + rq) * ldc4;
-#pragma unroll
-            for (int a = 0; a < NTF; ++a) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int n = f0 + 32 * a + 8 * g + 4 * hq;
-                    const bool in = n < N;
-                    const float4 it = in ? *reinterpret_cast<const float4*>(inv_t + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-                    const float4 bb = (in && bias != nullptr) ? *reinterpret_cast<const float4*>(bias + n)
-                                                              : make_float4(-0.f, -0.f, -0.f, -0.f);
-                    float4 o;
-                    o.x = acc[a][b][4 * g + 0] * is * it.x + bb.x;
-                    o.y = acc[a][b][4 * g + 1] * is * it.y + bb.y;
-                    o.z = acc[a][b][4 * g + 2] * is * it.z + bb.z;
-                    o.w = acc[a][b][4 * g + 3] * is * it.w + bb.w;
-                    if (drop.on()) drop4(drop, d0 + 32 * b + rq, n, o);
-                    u4v ov;
-                    ov.x = __float_as_uint(o.x); ov.y = __float_as_uint(o.y);
-                    ov.z = __float_as_uint(o.z); ov.w = __float_as_uint(o.w);
-                    __builtin_amdgcn_raw_buffer_store_b128(ov, crs, in ? rb + (uint32_t)n * 4u : nrec, 0, 0);
-                    // k_gemm_nt_p: a 16-byte store reads its data VGPRs over several cycles
-                    __builtin_amdgcn_sched_barrier(0);
-                    asm volatile("s_nop 1" ::: "memory");
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        }
-    }
-}
-
 // Small contractions with both operands split in the kernel (no packed weight): a block of 4 waves
 // owns one 32 x 32 output tile, the waves take the 32-k chunks c = q, q + 4, ... of the contraction
 // (up to 4 chunks' operands loaded at once: one memory latency per 4 chunks, not one per chunk), each
@@ -1811,16 +1647,6 @@ hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, con
     return hipGetLastError();
 }
 
-// the block-tiled NT route: 1 = k_gemm_nt_ws (32 rows per wave), 2 = k_gemm_nt_ws (64 rows per wave),
-// 0 = k_gemm_nt_p; env SIR_NT_WS_MODE, read once (A/B runs)
-static int nt_ws_mode() {
-    static const int mode = [] {
-        const char* e = getenv("SIR_NT_WS_MODE");
-        return (e != nullptr && e[0] != 0) ? atoi(e) : SIR_NT_WS;
-    }();
-    return mode;
-}
-
 int64_t gemm_pack_npad(int64_t N) { return (N + 255) / 256 * 256; }
 // the packed weight: the k_gemm_nt / k_gemm_nt_p fragment image, then the per-feature inverse scales
 int64_t gemm_pack_bytes(int64_t N, int64_t K) {
@@ -1885,29 +1711,6 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
     const float* inv = reinterpret_cast<const float*>(static_cast<const char*>(packed) + (int64_t)kc * 4 * np * 32);
     const bool kfull = K % KC == 0;
     if (M < gemm_small_rows()) return run_gemm_nt_s(A, lda, M, K, packed, N, bias, C, ldc, st, drop);
-    if (nt_ws_mode() != 0 && kfull && (K == 256 || K == 512)) {
-        const int NB = 32768 / K;                           // 128 KiB of hi/lo weight per slab
-        const int n_slabs = (N + NB - 1) / NB;
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-        const int n_groups = (ncu / n_slabs) / 8 * 8;
-        const int ntd = (nt_ws_mode() == 2 && K == 512) ? 2 : 1;
-        if (n_groups >= 8 && n_slabs * NB <= np) {
-            const int64_t n_wt = (M + 32 * ntd - 1) / (32 * ntd);
-            const int64_t wpg = ((n_wt + n_groups - 1) / n_groups + 7) / 8 * 8;
-            const dim3 grid((unsigned)(n_groups * n_slabs));
-#define SIR_WS_LAUNCH(NCH_, NTF_, NTD_)                                                                          \
-    hipLaunchKernelGGL((k_gemm_nt_ws<NCH_, NTF_, NTD_>), grid, dim3(512), 0, st, A, lda, M, wp, np, inv, bias, N, C, \
-                       ldc, n_slabs, n_wt, wpg, drop)
-            if (K == 256) SIR_WS_LAUNCH(8, 4, 1);
-            else if (ntd == 2) SIR_WS_LAUNCH(16, 2, 2);
-            else SIR_WS_LAUNCH(16, 2, 1);
-#undef SIR_WS_LAUNCH
-            return hipGetLastError();
-        }
-    }
     if (SIR_NT_PERSIST && N > 128 && np <= NT_P_NMAX && kfull && (kc == 4 || kc == 8 || kc == 16)) {
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;
