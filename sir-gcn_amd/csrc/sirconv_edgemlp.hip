@@ -9,11 +9,11 @@
 //     act1 = ReLU, (W, b) = the sigma Linear, act2 = ReLU, reduce = sum/mean/sym;
 //   * conv.py:46-47 (agg_type='max'): the per-edge linear_relation: act1 = sigma, (W, b) = W_R, b_R,
 //     act2 = identity, reduce = max.
-// The reference materialises a_e and m_e as [E, H] / [E, F] tensors (DGL edge UDF); here one wave
-// owns a work item (a destination row, or a <= chunk-edge piece of a hub row), stages 32 edges'
-// a_e in LDS, runs h = a W^T on fp32 MFMA (v_mfma_f32_32x32x2_f32: full fp32 products, fp32
-// accumulation) with W streamed from L2 in fragment order, and reduces m_e in registers — no
-// [E, *] tensor in HBM.
+// The reference materialises a_e and m_e as [E, H] / [E, F] tensors (DGL edge UDF); here a block
+// owns a work item (a destination row, or a <= chunk-edge piece of a hub row) or, at H = 256, a range
+// of the dst-CSR edge stream (k_mlp_fwd16r), stages 32 edges' a_e in LDS, runs h = a W^T on
+// split-fp16 MFMA (three v_mfma_f32_32x32x16_f16 per 16 k on hi / lo parts: fp32-accurate products,
+// fp32 accumulation) and reduces m_e in registers — no [E, *] tensor in HBM.
 //
 // Backward of the sum family (H, F <= 256): a destination pass (dQ, and per-block partial dW / db of
 // the layer) and a source pass (dK), each recomputing z, a, h for its edges:
@@ -64,145 +64,9 @@ __global__ void k_mlp_pack(const float* __restrict__ W, int H, int F, int HP, in
     out[idx] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-// ------------------------------------------------------------------------------ forward
-// One block per work item: NW waves share the staged a-tile (LDS) of 32 edges; wave w computes the
-// output tiles t = w + NW * j (j < TPW) of 32 features each.
-template <int ACT1, int ACT2, int RED, int NW, int TPW>
-__global__ void __launch_bounds__(64 * NW)
-k_mlp_fwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
-          const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
-          const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope,
-          int H, int HP, int F, const float4* __restrict__ Wp, const float* __restrict__ bias,
-          float* __restrict__ out, int64_t ldo, int* __restrict__ arg, int64_t lda,
-          float* __restrict__ pval, int* __restrict__ parg) {
-    extern __shared__ float smem[];
-    const int pitch = HP + 1;
-    float* sA = smem;                    // [32][pitch] a_e
-    float* sC = smem + 32 * pitch;       // [32] c_e (0 past the tile's last edge)
-    const int l = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int4 it = uniform_item(items, blockIdx.x);
-    const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
-    const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
-    const float* qp = Q + (int64_t)row * ldq;
-    const int nq = HP / 8;
-    const int ntile = (F + 31) / 32;
-
-    float racc[TPW], best[TPW], bb[TPW];
-    int bidx[TPW];
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-        racc[j] = 0.f; best[j] = -INFINITY; bidx[j] = INT_MAX;
-        const int n = 32 * (w + NW * j) + (l & 31);
-        bb[j] = (bias != nullptr && n < F) ? bias[n] : 0.f;
-    }
-
-    for (int t0 = e0; t0 < e1; t0 += 32) {
-        const int nv = (e1 - t0) < 32 ? (e1 - t0) : 32;
-        // ---- stage a = act1(Q[v] + K[u]) (wave w: rows w, w + NW, ...; rows past nv: zeros)
-        for (int c0 = 0; c0 < HP; c0 += 256) {
-            const int k = c0 + 4 * l;
-            float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (k < H) q4 = *reinterpret_cast<const float4*>(qp + k);
-#pragma unroll 8
-            for (int i = w; i < 32; i += NW) {
-                float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (i < nv && k < H) {
-                    const int u = col[t0 + i];
-                    const float4 k4 = *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k);
-                    a4.x = act_f<ACT1>(q4.x + k4.x, slope); a4.y = act_f<ACT1>(q4.y + k4.y, slope);
-                    a4.z = act_f<ACT1>(q4.z + k4.z, slope); a4.w = act_f<ACT1>(q4.w + k4.w, slope);
-                }
-                if (k < HP) {
-                    float* d = sA + i * pitch + k;
-                    d[0] = a4.x; d[1] = a4.y; d[2] = a4.z; d[3] = a4.w;
-                }
-            }
-        }
-        if (w == 0 && l < 32) {
-            float c = 0.f;
-            if (l < nv) c = (RED == AGG_SYM) ? norm_col[col[t0 + l]] * nr : 1.f;   // conv.py:45 operand order
-            sC[l] = c;
-        }
-        __syncthreads();
-        // ---- h = a W^T on MFMA (this wave's output tiles)
-        mf16 acc[TPW];
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-        const float* arow = sA + (l & 31) * pitch + (l >> 5);
-        for (int q = 0; q < nq; ++q) {
-            float av[4];
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) av[jj] = arow[8 * q + 2 * jj];
-#pragma unroll
-            for (int j = 0; j < TPW; ++j) {
-                const int t = w + NW * j;
-                if (t >= ntile) continue;            // wave-uniform: tiles past F have no packed W
-                const float4 b4 = Wp[(int64_t)(t * nq + q) * 64 + l];
-                acc[j] = mfma32(av[0], b4.x, acc[j]);
-                acc[j] = mfma32(av[1], b4.y, acc[j]);
-                acc[j] = mfma32(av[2], b4.z, acc[j]);
-                acc[j] = mfma32(av[3], b4.w, acc[j]);
-            }
-        }
-        // ---- m = act2(h + b), reduced in edge order within the lane
-#pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = drow(r, l);
-                if (i < nv) {
-                    const float m = act_f<ACT2>(acc[j][r] + bb[j], slope);
-                    if constexpr (RED == 3) {
-                        if (m > best[j]) { best[j] = m; bidx[j] = t0 + i; }    // strict >: first wins
-                    } else {
-                        racc[j] += sC[i] * m;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    }
-    // ---- the two half-waves hold interleaved edge groups of the same columns: combine, store
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-        const int n = 32 * (w + NW * j) + (l & 31);
-        if constexpr (RED == 3) {
-            const float ob = __shfl_xor(best[j], 32);
-            const int oi = __shfl_xor(bidx[j], 32);
-            if (ob > best[j] || (ob == best[j] && oi < bidx[j])) { best[j] = ob; bidx[j] = oi; }
-            if (l < 32 && n < F) {
-                const bool any = bidx[j] != INT_MAX;
-                if (slot < 0) {
-                    out[(int64_t)row * ldo + n] = any ? best[j] : 0.f;
-                    arg[(int64_t)row * lda + n] = any ? bidx[j] : -1;
-                } else {
-                    pval[(int64_t)slot * F + n] = best[j];
-                    parg[(int64_t)slot * F + n] = bidx[j];
-                }
-            }
-        } else {
-            const float other = __shfl_xor(racc[j], 32);
-            float v = (l < 32) ? racc[j] + other : other + racc[j];
-            if (l < 32 && n < F) {
-                if (slot < 0) {
-                    if constexpr (RED == AGG_MEAN) {
-                        const int d = e1 - e0;
-                        v = v / (float)(d > 1 ? d : 1);
-                    }
-                    out[(int64_t)row * ldo + n] = v;
-                } else {
-                    pval[(int64_t)slot * F + n] = v;
-                }
-            }
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------ forward, split-fp16 MFMA
-// The same dataflow as k_mlp_fwd with h = a W^T on v_mfma_f32_32x32x16_f16 and the two-term operand
+// One block per work item (a destination row or a chunk of a hub row): its waves stage 32 edges' a_e
+// rows in LDS and compute h = a W^T on v_mfma_f32_32x32x16_f16 with the two-term operand
 // split of the projection GEMMs (sirconv_gemm.hip): a = (a_hi + a_lo) / s_e with one power-of-two
 // scale per edge row (the whole row is staged before it is split), W = (w_hi + w_lo) / s_n per
 // feature (packed once, k_mlp_pack16), h = (a_hi w_hi + a_hi w_lo + a_lo w_hi) / (s_e s_n) with fp32
@@ -1329,9 +1193,6 @@ k_mlp_bwd(const int* __restrict__ rowptr, const int* __restrict__ col, const int
     }
 }
 
-#ifndef SIR_MLP_F16
-#define SIR_MLP_F16 1           // 1: the forward on split-fp16 MFMA (k_mlp_fwd16); 0: fp32 MFMA (k_mlp_fwd)
-#endif
 int mlp_ng(int H) { return (H + 15) / 16; }
 int64_t mlp_pack16_bytes(int H, int F) {
     const int FP = (F + 31) / 32 * 32;
@@ -1354,10 +1215,7 @@ hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a,
     const h8v* w16 = static_cast<const h8v*>(p16);
     const float* winv = reinterpret_cast<const float*>(static_cast<const char*>(p16) + (int64_t)FP * NG * 64);
     if (SIR_MLP_PIPE && a.col != nullptr && a.F <= 256 && NG == 16) {
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
+        const int ncu = device_cu_count();
         // resident blocks only (a persistent block never yields its CU): one 512-thread block per CU
         const int64_t cap = (int64_t)ncu;
         const int64_t nb = a.n_items < cap ? a.n_items : cap;
@@ -1372,10 +1230,7 @@ hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a,
         return hipGetLastError();
     }
     if (SIR_MLP_RESIDENT && a.F <= 256 && (NG == 4 || NG == 8)) {
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
+        const int ncu = device_cu_count();
         // resident blocks only (a persistent block never yields its CU): NG = 16 takes ~208 VGPRs (one
         // 512-thread block per CU), NG <= 8 fits two
         const int64_t cap = (int64_t)ncu * (NG == 16 ? 1 : 2);
@@ -1410,23 +1265,6 @@ hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a,
     return hipGetLastError();
 }
 
-template <int ACT1, int ACT2, int RED>
-hipError_t mlp_fwd_nt(int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeMlpArgs& a) {
-#define SIR_MLP_FWD(NWV, TPWV)                                                                                 \
-    hipLaunchKernelGGL((k_mlp_fwd<ACT1, ACT2, RED, NWV, TPWV>), grid, dim3(64 * NWV), lds, st, a.rowptr, a.col, \
-                       reinterpret_cast<const int4*>(a.items), a.Q, a.ldq, a.K, a.ldk, a.norm_row, a.norm_col,   \
-                       a.slope, a.H, a.HP, a.F, reinterpret_cast<const float4*>(a.Wp), a.bias, a.out, a.ldo,    \
-                       a.arg, a.lda, a.pval, a.parg)
-    // nt output tiles of 32 features over NW waves x TPW tiles (tiles past nt only compute zeros)
-    if (nt <= 1) SIR_MLP_FWD(1, 1);
-    else if (nt <= 2) SIR_MLP_FWD(2, 1);
-    else if (nt <= 4) SIR_MLP_FWD(4, 1);
-    else if (nt <= 8) SIR_MLP_FWD(4, 2);
-    else SIR_MLP_FWD(8, 2);                      // F <= 512 (roman-empire: H = O = 512)
-#undef SIR_MLP_FWD
-    return hipGetLastError();
-}
-
 template <int ACT1, int ACT2>
 hipError_t mlp_fwd16_red(int red, int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
     switch (red) {
@@ -1434,16 +1272,6 @@ hipError_t mlp_fwd16_red(int red, int nt, dim3 grid, hipStream_t st, const EdgeM
         case AGG_MEAN: return mlp_fwd16_nt<ACT1, ACT2, AGG_MEAN>(nt, grid, st, a, p16);
         case AGG_SYM: return mlp_fwd16_nt<ACT1, ACT2, AGG_SYM>(nt, grid, st, a, p16);
         default: return mlp_fwd16_nt<ACT1, ACT2, 3>(nt, grid, st, a, p16);
-    }
-}
-
-template <int ACT1, int ACT2>
-hipError_t mlp_fwd_red(int red, int nt, dim3 grid, size_t lds, hipStream_t st, const EdgeMlpArgs& a) {
-    switch (red) {
-        case AGG_SUM: return mlp_fwd_nt<ACT1, ACT2, AGG_SUM>(nt, grid, lds, st, a);
-        case AGG_MEAN: return mlp_fwd_nt<ACT1, ACT2, AGG_MEAN>(nt, grid, lds, st, a);
-        case AGG_SYM: return mlp_fwd_nt<ACT1, ACT2, AGG_SYM>(nt, grid, lds, st, a);
-        default: return mlp_fwd_nt<ACT1, ACT2, 3>(nt, grid, lds, st, a);
     }
 }
 
@@ -1526,14 +1354,11 @@ hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t 
 
 hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st) {
     if (a.n_items > 0) {
+        if (a.H > 512) return hipErrorInvalidValue;           // the ABI's limit (sirconv.h)
         const int nt = (a.F + 31) / 32;
-        const size_t lds = (size_t)(32 * (a.HP + 1) + 32) * sizeof(float);
         const dim3 grid((unsigned)a.n_items);
-        const bool f16 = SIR_MLP_F16 && a.H <= 512;
         hipError_t err = by_acts(act1, act2, [&](auto A1, auto A2) {
-            return f16 ? mlp_fwd16_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, st, a,
-                                                                               mlp_p16(a.Wp, a.H, a.F))
-                       : mlp_fwd_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, lds, st, a);
+            return mlp_fwd16_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, st, a, mlp_p16(a.Wp, a.H, a.F));
         });
         if (err != hipSuccess) return err;
     }
@@ -1555,10 +1380,7 @@ hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStr
 
 // the stream forward's grid (one 512-thread block per CU) and its boundary-slot workspace
 static int mlp_stream_blocks() {
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-        ncu = 256;
+    const int ncu = device_cu_count();
     return ncu > 1024 ? 1024 : ncu;
 }
 int64_t mlp_stream_work_bytes(int F) {

@@ -1675,10 +1675,7 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
             constexpr int BD = 256, BF = 256;
             const int nft = (N + BF - 1) / BF;
             const int64_t ntiles = (M + BD - 1) / BD * nft;
-            int dev = 0, ncu = 256;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-                ncu = 256;
+            const int ncu = device_cu_count();
             if (ntiles < (int64_t)1 << 30) {
                 const int tpb = (int)((ntiles + ncu - 1) / ncu);
                 const int nblk = (int)((ntiles + tpb - 1) / tpb);
@@ -1715,10 +1712,7 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
         constexpr int BD = 256, BF = 256;
         const int nft = (N + BF - 1) / BF;
         const int64_t ntiles = (M + BD - 1) / BD * nft;
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
+        const int ncu = device_cu_count();
         if (ntiles < (int64_t)1 << 30) {
             const int tpb = (int)((ntiles + ncu - 1) / ncu);
             const int nblk = (int)((ntiles + tpb - 1) / tpb);

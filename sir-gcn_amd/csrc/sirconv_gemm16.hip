@@ -627,10 +627,7 @@ static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, cons
                               void* C, int64_t ldc, unsigned short* Acopy, int64_t ldac, hipStream_t st, const Drop& drop) {
     const int np = (N + 255) / 256 * 256, nft = np / 256;
     const int64_t ntiles = (M + 255) / 256 * nft;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        ncu <= 0)
-        ncu = 256;
+    const int ncu = device_cu_count();
     const int tpb = (int)((ntiles + ncu - 1) / ncu);
     const int nblk = (int)((ntiles + tpb - 1) / tpb);
     const auto* wp = static_cast<const u4v*>(packed);

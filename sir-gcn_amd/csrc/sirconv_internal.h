@@ -179,4 +179,17 @@ hipError_t run_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int
 // is not native): X[m][n] = keep(m, col0 + n) ? X[m][n] * scale : 0, storage dtype SIR_DTYPE_*
 hipError_t run_dropout_apply(void* X, int64_t ldx, int64_t M, int N, int dtype, const Drop& drop, hipStream_t st);
 
+// compute units of the current device (persistent-grid sizing), queried once per device: the
+// attribute query is not free and the launch paths run it on every call otherwise
+inline int device_cu_count() {
+    static int cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+    if (dev < 64 && cached[dev] > 0) return cached[dev];
+    int ncu = 256;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    if (dev < 64) cached[dev] = ncu;
+    return ncu;
+}
+
 }  // namespace sir

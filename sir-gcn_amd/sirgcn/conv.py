@@ -72,9 +72,10 @@ class EdgeAggregate(torch.autograd.Function):
     fp32 S anyway.  The backward reads dS and writes dQ/dK in that dtype as well.
 
     Backward returns dQK written by the dst pass (dQ half) and the src pass (dK half).
-    For sigma in {ReLU, LeakyReLU} (and 128 < H <= 1024) the forward also stores the sign of
-    every z = Q[v] + K[u] (H bits per edge) and the backward runs in sign-mask mode: no Q/K
-    re-gather, QK not kept alive; results are bit-identical to the recompute mode."""
+    For sigma in {ReLU, LeakyReLU} (any H <= 1024; the sub-wave rows of H <= 128 write their record
+    from the wave ballots, ``sir_mask_words``) the forward also stores the sign of every z = Q[v] + K[u] and the
+    backward runs in sign-mask mode: no Q/K re-gather, QK not kept alive; results are bit-identical
+    to the recompute mode."""
 
     use_mask = True
     dual = True          # one-launch backward (sir_edge_agg_bwd) where it applies

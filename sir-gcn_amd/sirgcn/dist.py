@@ -433,14 +433,25 @@ def _complete_dk(dg, big, recvs, works, backend):
     return dK
 
 
-def _drops(drop):
-    """(Q drop, K drop) of a (seeds, p) pair: two independent device seeds (or ints)."""
+_SEED_MIX = 0x2545F4914F6CDD1D        # odd 62-bit multiplier mixing a rank's global row offset into its seeds
+
+
+def _drops(drop, row_begin=0):
+    """(Q drop, K drop) of a (seeds, p) pair: two independent device seeds (or ints).  The kernels
+    hash the LOCAL row index, so each rank's seeds are offset by a function of its first global row
+    (``row_begin``): local row i of two ranks then draws independent bits, as the reference's
+    nn.Dropout does over the whole [V, H] tensor (every rank draws the same seeds from its generator
+    under the usual torch.manual_seed(same))."""
     if drop is None:
         return None, None
     seeds, p = drop
+    off = (int(row_begin) * _SEED_MIX) % (1 << 62)
     if isinstance(seeds, torch.Tensor):
+        if off:
+            seeds = torch.bitwise_xor(seeds, off)
         return (seeds[0:1], p), (seeds[1:2], p)
-    return (int(seeds), p), ((int(seeds) * 0x9E3779B97F4A7C15 + 1) % (1 << 62), p)
+    s0 = int(seeds) ^ off
+    return (s0, p), ((s0 * 0x9E3779B97F4A7C15 + 1) % (1 << 62), p)
 
 
 class DistSIRConvFunction(torch.autograd.Function):
@@ -459,7 +470,7 @@ class DistSIRConvFunction(torch.autograd.Function):
         n = dg.n_rows
         dev = X.device
         X = X.contiguous()
-        dq, dk = _drops(drop)
+        dq, dk = _drops(drop, dg.row_begin)
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
         linalg.mm_wt(X, W_K, out=K_ext[:n], drop=dk)
         works = [dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True) for c in range(dg.chunks)]
@@ -525,7 +536,7 @@ class DistSIRConvFunction16(torch.autograd.Function):
         n = dg.n_rows
         dev = X.device
         X = X.contiguous()
-        dq, dk = _drops(drop)
+        dq, dk = _drops(drop, dg.row_begin)
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=dt)
         if X.dtype == dt:
             Xh = X
@@ -665,8 +676,13 @@ class DistSIRConv(torch.nn.Module):
             raise ValueError(f"feat has {feat.shape[0]} rows, rank owns {dgraph.n_rows}")
         act, slope = activation_code(c.activation)
         H = c.linear_query.out_features
+        # training dropout inside the fused functions needs the native kernels on device tensors (the
+        # hashed masks are applied by sir_dropout_apply / the GEMM epilogues): CPU rehearsals and
+        # injected edge backends with p > 0 take the modular path (nn.Dropout) instead
+        drop_native = feat.is_cuda and self.backend is _native
         fused = (self.use_fused and feat.dtype == torch.float32 and not torch.is_autocast_enabled()
-                 and c.linear_query.weight.dtype == torch.float32)
+                 and c.linear_query.weight.dtype == torch.float32
+                 and (drop_native or not (c.training and c.dropout.p > 0)))
         if fused:
             return DistSIRConvFunction.apply(feat, c.linear_query.weight, c.linear_query.bias, c.linear_key.weight,
                                              c.linear_relation.weight, c.linear_relation.bias, dgraph,

@@ -231,8 +231,9 @@ class EdgeMaxLinear(torch.autograd.Function):
             return dQK, dW, (db if ctx.has_b else None), None, None, None, None
         # the arg edges' activations are needed for dW_R: recompute them once (no copy kept from the
         # forward).  ReLU family: A = sigma(z) straight from the gather (sign(A) = sign(z), so sigma' is
-        # read off A below and z is never stored); other sigmas: z, then sigma(z)
-        relu_family = act1 in (_native.ACT_RELU, _native.ACT_LEAKY)
+        # read off A below and z is never stored); other sigmas: z, then sigma(z).  A LeakyReLU with a
+        # negative slope flips the sign (z < 0 gives A = slope z > 0), so it takes the z route
+        relu_family = act1 == _native.ACT_RELU or (act1 == _native.ACT_LEAKY and slope >= 0)
         smask = None
         if relu_family:
             A = torch.empty((E, H), device=dev, dtype=torch.float32)

@@ -219,3 +219,57 @@ def test_edge_cut_async_exchange_waits_before_use(agg):
     r = oracle.reference_cpu_step(src, dst, V, X, *w, dY, agg, "leaky", 0.2)
     assert_parity(Y, r["Y"], t["Y"], 1e-5, "Y")
     assert_parity(dX, r["dX"], t["dX"], 1e-5, "dX")
+
+
+def _dropout_worker(rank, world, port, outdir):
+    for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from torch import nn
+    import cpu_edge_backend
+    from sirgcn import SIRConv
+    from sirgcn.dist import DistGraph, DistSIRConv
+    from sirgcn.synth import powerlaw_edges
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    V, E, d, H, O = 300, 3000, 8, 16, 8
+    src, dst = powerlaw_edges(V, E, 0.8, seed=5)
+    X = torch.randn(V, d, generator=torch.Generator().manual_seed(1))
+    torch.manual_seed(3)
+    conv = SIRConv(d, H, O, nn.ReLU(), 0.5, agg_type="sum")
+    conv.train()
+    dg = DistGraph.from_global(src, dst, V, rank, world, "cpu", chunk=64)
+    dconv = DistSIRConv(conv, backend=cpu_edge_backend)       # use_fused stays True: CPU + p > 0 must not enter it
+    r0, r1 = dg.row_begin, dg.row_end
+    Xl = X[r0:r1].clone().requires_grad_(True)
+    Y = dconv(dg, Xl)
+    Y.sum().backward()
+    dconv.allreduce_grads()
+    torch.save({"Y": Y.detach(), "dX": Xl.grad, "gq": conv.linear_query.weight.grad}, os.path.join(outdir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_edge_cut_training_dropout_on_cpu_takes_the_modular_path(tmp_path):
+    """CPU rehearsals with dropout > 0 in train mode must not reach the native dropout
+    kernels (host pointers); they run nn.Dropout on the modular path."""
+    mp.spawn(_dropout_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        part = torch.load(tmp_path / f"rank{r}.pt", weights_only=True)
+        assert torch.isfinite(part["Y"]).all() and torch.isfinite(part["dX"]).all()
+        assert part["gq"] is not None and torch.isfinite(part["gq"]).all()
+
+
+def test_dropout_seeds_differ_across_ranks():
+    """the kernels hash the LOCAL row index, so each rank's seeds are offset by its first
+    global row; rank 0 (row_begin 0) keeps the drawn seeds."""
+    sys.path.insert(0, PKG)
+    from sirgcn.dist import _drops
+    seeds = torch.tensor([123456789, 987654321], dtype=torch.int64)
+    q0, k0 = _drops((seeds, 0.2), 0)
+    q1, k1 = _drops((seeds, 0.2), 1000)
+    assert int(q0[0]) == 123456789 and int(k0[0]) == 987654321
+    assert int(q1[0]) != int(q0[0]) and int(k1[0]) != int(k0[0])
+    a, b = _drops((42, 0.2), 0), _drops((42, 0.2), 77)
+    assert a[0][0] == 42 and a[0][0] != b[0][0] and a[1][0] != b[1][0]

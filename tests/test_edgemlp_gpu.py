@@ -297,3 +297,24 @@ def sign_words(A):
     """int64 [E, 4]: bit l of word x = A[:, 4 l + x] > 0 (sir_edge_gather_act's sign mask, H = 256)."""
     bits = (A > 0).reshape(A.shape[0], 64, 4).permute(0, 2, 1).long()
     return (bits << torch.arange(64, device=A.device)).sum(-1)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_max_negative_slope_leaky_both_backwards(fused, monkeypatch):
+    """a LeakyReLU with a negative slope flips the sign (z < 0 gives sigma(z) = slope z > 0),
+    so sigma' must come from z, not from the activation: both max backwards against the oracle."""
+    from sirgcn.edgemlp import EdgeMaxLinear
+    src, dst, V, gen = _graph(101)
+    X, dY = torch.randn(V, 32, generator=gen), torch.randn(V, 96, generator=gen)
+    torch.manual_seed(11)
+    m = SIRConv(32, 128, 96, nn.LeakyReLU(-0.2), 0, agg_type="max").to(DEV)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", fused)
+    got = _run(m, Graph(src, dst, V), X, dY)
+    w = [t.detach().cpu() for t in (m.linear_query.weight, m.linear_query.bias, m.linear_key.weight,
+                                    m.linear_relation.weight, m.linear_relation.bias)]
+    r32 = oracle.reference_cpu_step(src, dst, V, X, *w, dY, "max", "leaky", -0.2)
+    r64 = oracle.reference_cpu_step(src, dst, V, X.double(), *[t.double() for t in w], dY.double(), "max", "leaky",
+                                    -0.2)
+    for k, kr in (("Y", "Y"), ("dX", "dX"), ("linear_query.weight", "dW_Q"), ("linear_key.weight", "dW_K"),
+                  ("linear_relation.weight", "dW_R"), ("linear_relation.bias", "db_R")):
+        assert_parity(got[k], r32[kr], r64[kr], 1e-5, f"max leaky(-0.2) fused={fused} {k}", strict=(k == "Y"))

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-5: k_gemm_nt_w with the split waves loading full 128-B row lines per stage pair; roles alone (SIR_NT_W_ABL)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r05_w6
+mkdir -p $O
+L=sir-gcn_amd/lib/libsirconv.so
+timeout -k 10 300 python -u tools/gemm_ab.py --rounds 5 --only QK,Y,G,dX --libs p=$L w=$L@SIR_GEMM_NT_ROUTE=w > $O/ab0.txt 2>&1 || { cat $O/ab0.txt; exit 1; }
+grep -v amdgpu.ids $O/ab0.txt
+for b in 267 264 536 552 540; do
+  SIR_NT_W_ABL=$b timeout -k 10 200 python -u tools/gemm_ab.py --rounds 3 --only Y --libs w$b=$L@SIR_GEMM_NT_ROUTE=w > $O/ab$b.txt 2>&1 || { cat $O/ab$b.txt; exit 1; }
+  grep -v "^total\|amdgpu.ids" $O/ab$b.txt
+done
