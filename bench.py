@@ -363,7 +363,8 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             import cpu_edge_backend as backend
         dg = DistGraph.from_global(src, dst, V, rank, world, dev, chunk=args.chunk or DEFAULT_CHUNK)
-        dconv = DistSIRConv(conv, backend=backend)
+        # weight gradients all-reduced inside the backward, dW_R / dW_Q under the reverse exchange
+        dconv = DistSIRConv(conv, backend=backend, reduce_in_backward=True)
         r0, r1 = dg.row_begin, dg.row_end
         X = X_full[r0:r1].to(dev).requires_grad_(True)
         dY = dY_full[r0:r1].to(dev)

@@ -82,10 +82,11 @@ def all_reduce_sum(t, group=None):
 
 
 # per-row cost of the edge-cut layer in units of one in-edge: the node-row work (the five projection
-# GEMMs, the halo packing, the dK completion: ~4 ns per row at H = 256) against the edge passes'
-# ~0.32 ns per edge (the S2 profile, tools/dist_model.py) — an edge-only cut left the slowest rank
+# GEMMs ~4 ns, the halo packing, the segments' read-modify-writes of S and the dK completion ~4 ns per
+# row at H = 256) against the edge passes' ~0.31 ns per edge (the S2 profile, tools/dist_model.py: the
+# slowest of 8 ranks 3.53 ms at 12, 3.50 at 20-24, 3.51 at 32); an edge-only cut left the slowest rank
 # of S2 at 8 ranks with 8 % more rows than the mean
-ROW_WEIGHT = 12
+ROW_WEIGHT = 24
 
 
 def partition_rows(in_deg, world, row_weight=ROW_WEIGHT):
@@ -172,6 +173,8 @@ class DistGraph:
         self.group = group
         C = (DEFAULT_EXCHANGE_CHUNKS if chunks is None else int(chunks)) if world > 1 else 0
         self.chunks = C
+        # own rows of exchange chunk c: [part_bounds[c], part_bounds[c + 1]) (local row x is in part (x C) // n)
+        self.part_bounds = [-(-c * n // C) for c in range(C + 1)] if C else [0, n]
         dev = self.device
         src = torch.as_tensor(src, dtype=torch.int64).to(dev)
         dst = torch.as_tensor(dst, dtype=torch.int64).to(dev)
@@ -184,12 +187,14 @@ class DistGraph:
         self.n_ext = n + self.n_halo
         bt = torch.tensor(self.bounds, dtype=torch.int64, device=dev)
         owner = torch.searchsorted(bt, halo, right=True) - 1
-        # ---- chunk-major halo order: chunk c of owner q = positions [c L_q / C, (c+1) L_q / C) ----
+        # ---- chunk-major halo order: chunk c of owner q = the requested rows in the c-th of C equal
+        # parts of q's row RANGE, so that an owner can send chunk c as soon as the K rows of its own
+        # range part c are projected, and complete the dK of that part as soon as chunk c's reverse
+        # exchange lands (the synthetic graphs relabel node ids at random: the parts hold similar
+        # numbers of requested rows) ----
         if self.n_halo:
-            cnt = torch.bincount(owner, minlength=world)
-            start = torch.cumsum(cnt, 0) - cnt
-            pos = torch.arange(self.n_halo, device=dev) - start[owner]
-            hchunk = (pos * C) // cnt[owner]
+            lo_q = bt[owner]
+            hchunk = ((halo - lo_q) * C) // (bt[owner + 1] - lo_q)
             key = hchunk * world + owner
             order = torch.argsort(key, stable=True)
             new_pos = torch.empty_like(order)
@@ -214,14 +219,15 @@ class DistGraph:
             sc = sc_t.cpu().tolist()
             req = torch.empty(sum(sc), dtype=torch.int64, device=dev)
             all_to_all_rows(req, halo.contiguous(), sc, req_cnt.cpu().tolist(), group=group)
-            parts = list(torch.split(req, sc))
+            parts = [t - self.row_begin for t in torch.split(req, sc)]      # ascending local rows per peer
+            qb = torch.tensor(self.part_bounds, dtype=torch.int64, device=dev)
+            cuts = [torch.searchsorted(t, qb).cpu().tolist() for t in parts]
             for c in range(C):
                 idx_c = []
                 for q in range(world):
-                    L = sc[q]
-                    a, b = -(-c * L // C), -(-(c + 1) * L // C)   # positions with (pos * C) // L == c
+                    a, b = cuts[q][c], cuts[q][c + 1]                     # requests inside my part c
                     self.send_splits[c][q] = b - a
-                    idx_c.append(parts[q][a:b] - self.row_begin)
+                    idx_c.append(parts[q][a:b])
                 self.send_idx[c] = torch.cat(idx_c).contiguous()
             allidx = torch.cat(self.send_idx)
             if allidx.numel():
@@ -308,6 +314,16 @@ class DistGraph:
         for idx, part in zip(self._send_parts[c], torch.split(recv, self.send_splits[c])):
             if idx.numel():
                 own.index_add_(0, idx, part)
+
+    def own_range(self, c):
+        """Own rows whose K rows exchange chunk c sends and whose dK it completes."""
+        return self.part_bounds[c], self.part_bounds[c + 1]
+
+    def recv_part(self, c):
+        """``recv_plan`` restricted to the own rows of part c (their received rows all come with chunk c)."""
+        if not hasattr(self, "_recv_parts"):
+            self._recv_parts = [_row_slice(self.recv_plan, *self.own_range(k)) for k in range(self.chunks)]
+        return self._recv_parts[c]
 
     def gather_halo(self, own, ext):
         """ext[n:] ← the owners' rows of ``own``, every chunk (synchronous)."""
@@ -413,6 +429,43 @@ def _backward_buffers(dg, H, dev, dtype):
     return big, big[:dg.n_ext], recvs
 
 
+def _complete_dk_parts(dg, big, recvs, works, backend, out=None):
+    """Yield (dK rows of own part c, a, b) as each reverse chunk lands: the rows of part c receive
+    partials from chunk c only, summed in a fixed order (own partial, then peers ascending) — one
+    native segment sum per part (a gather: no atomics), else per-peer index_add (unique indices per
+    call: deterministic)."""
+    n = dg.n_rows
+    if not dg.chunks:
+        if out is not None:
+            out.copy_(big[:n])
+            yield out, 0, n
+        else:
+            yield big[:n], 0, n
+        return
+    native = backend is _native and big.dtype == torch.float32
+    if native:
+        dK = out if out is not None else torch.empty((n, big.shape[1]), device=big.device, dtype=big.dtype)
+        part = torch.empty((dg.recv_plan.n_slots * big.shape[1],), device=big.device) if dg.recv_plan.n_slots else None
+    for c in range(dg.chunks):
+        if works[c] is not None:
+            works[c].wait()
+        a, b = dg.own_range(c)
+        if b <= a:
+            continue
+        if native:
+            rp = dg.recv_part(c)
+            _native.segment_sum(rp, big, dK, perm=rp.col, partial=part)
+            yield dK[a:b], a, b
+        else:
+            own = big[:n]
+            dg.add_received(c, own, recvs[c])
+            if out is not None:
+                out[a:b] = own[a:b]
+                yield out[a:b], a, b
+            else:
+                yield own[a:b], a, b
+
+
 def _complete_dk(dg, big, recvs, works, backend):
     """dK of the own rows = own partial + every peer's halo partial, in a fixed order (own, then chunk by
     chunk, peers ascending): one native segment sum gathering the rows of ``big`` (fp32), else per chunk
@@ -454,6 +507,54 @@ def _drops(drop, row_begin=0):
     return (s0, p), ((s0 * 0x9E3779B97F4A7C15 + 1) % (1 << 62), p)
 
 
+def _drop_at(drop, row0):
+    """The K dropout of the own-row part starting at local row ``row0``: the K GEMM runs per part
+    (its epilogue hashes the row index inside the part), so each part's seed is offset by ``row0``
+    (part 0 keeps the rank's seed); the backward applies the same per-part masks to dK."""
+    if drop is None or row0 == 0:
+        return drop
+    seed, p = drop
+    off = (int(row0) * _SEED_MIX * 3) % (1 << 62)
+    if isinstance(seed, torch.Tensor):
+        return torch.bitwise_xor(seed, off), p
+    return int(seed) ^ off, p
+
+
+class _GradReducer:
+    """Weight gradients all-reduced INSIDE the backward (``DistSIRConv(reduce_in_backward=True)``):
+    dW_R / db_R and dW_Q / db_Q are queued on RCCL right after they are computed, under the reverse
+    exchange; dW_K, the last one, at the end.  ``group=None`` with no process group: nothing."""
+
+    def __init__(self, group):
+        self.group = group
+        self.pending = []
+
+    def add(self, tensors):
+        ts = [t for t in tensors if t is not None]
+        if not ts:
+            return
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        if hasattr(self.group, "all_to_all_rows"):
+            raise NotImplementedError("reduce_in_backward needs a torch.distributed process group")
+        if flat.is_cuda and not _host_staged(self.group, flat):
+            work = dist.all_reduce(flat, group=self.group, async_op=True)     # RCCL, under the exchange
+        else:
+            all_reduce_sum(flat, group=self.group)                            # gloo rehearsals
+            work = None
+        self.pending.append((work, flat, ts))
+
+    def finish(self):
+        for work, flat, ts in self.pending:
+            if work is not None:
+                work.wait()
+            off = 0
+            for t in ts:
+                k = t.numel()
+                t.copy_(flat[off:off + k].view_as(t))
+                off += k
+        self.pending = []
+
+
 class DistSIRConvFunction(torch.autograd.Function):
     """One rank's share of the whole layer, hand-scheduled around the two pipelined exchanges.
 
@@ -465,15 +566,23 @@ class DistSIRConvFunction(torch.autograd.Function):
     ``drop``: (two device seeds, p) of the Q / K feature dropout (conv.py:60-61), or None."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on=True, drop=None):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on=True, drop=None,
+                reduce=False):
         H = W_Q.shape[0]
         n = dg.n_rows
+        ctx.reduce = reduce
         dev = X.device
         X = X.contiguous()
         dq, dk = _drops(drop, dg.row_begin)
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=torch.float32)
-        linalg.mm_wt(X, W_K, out=K_ext[:n], drop=dk)
-        works = [dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True) for c in range(dg.chunks)]
+        # K part by part: exchange chunk c carries only rows of part c, so it leaves as soon as they exist
+        works = []
+        for c in range(max(dg.chunks, 1)):
+            a, b = dg.own_range(c)
+            if b > a:
+                linalg.mm_wt(X[a:b], W_K, out=K_ext[a:b], drop=_drop_at(dk, a))
+            if c < dg.chunks:
+                works.append(dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True))
         Q = linalg.mm_wt(X, W_Q, b_Q, drop=dq)
         S = torch.empty((n, H), device=dev, dtype=torch.float32)
         training = grad_on and any(ctx.needs_input_grad[:6])     # grad mode passed in (see conv.py)
@@ -504,22 +613,38 @@ class DistSIRConvFunction(torch.autograd.Function):
         n = dg.n_rows
         dev = X.device
         dY = dY.contiguous()
+        red = _GradReducer(dg.group) if ctx.reduce else None
         G = linalg.mm_w(dY, W_R)
-        dQ = torch.empty((n, H), device=dev, dtype=torch.float32)
+        # dQ and the completed own-row dK side by side ([dQ | dK], as on one GPU): dX of each part is then
+        # ONE K = 2H GEMM against [W_Q; W_K], written once (no dX read-modify-write per part)
+        dQK = torch.empty((n, 2 * H), device=dev, dtype=torch.float32)
+        dQ = dQK[:, :H]
         big, dK_ext, recvs = _backward_buffers(dg, H, dev, torch.float32)
         works = _chunked_backward(backend, dg, H, agg, act, slope, G, Q, K_ext, mask, dQ, dK_ext, recvs)
         if dq is not None:
             _native.dropout_apply(dQ, dq)
         dW_R, db_R = _weight_and_bias_grad(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
-        dX = linalg.mm_w(dQ, W_Q) if ctx.needs_input_grad[0] else None
+        if red is not None:
+            red.add([dW_R, db_R])
         dW_Q, db_Q = _weight_and_bias_grad(dQ, X, ctx.needs_input_grad[1], ctx.has_bq and ctx.needs_input_grad[2])
-        dK = _complete_dk(dg, big, recvs, works, backend)
-        if dk is not None:
-            _native.dropout_apply(dK, dk)
-        if dX is not None:
-            dX += linalg.mm_w(dK, W_K)
-        dW_K = _tn(dK, X) if ctx.needs_input_grad[3] else None
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None
+        if red is not None:
+            red.add([dW_Q, db_Q])
+        dX = torch.empty((n, X.shape[1]), device=dev, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        W_cat = torch.cat([W_Q, W_K], 0) if dX is not None else None
+        # dK part by part as each reverse chunk lands: complete, mask, dX = [dQ | dK] [W_Q; W_K], dW_K += dK^T X
+        dW_K = None
+        for c, (dK, a, b) in enumerate(_complete_dk_parts(dg, big, recvs, works, backend, out=dQK[:, H:])):
+            if dk is not None:
+                _native.dropout_apply(dK, _drop_at(dk, a))
+            if dX is not None:
+                linalg.mm_w(dQK[a:b], W_cat, out=dX[a:b])
+            if ctx.needs_input_grad[3]:
+                part = _tn(dK, X[a:b])
+                dW_K = part if dW_K is None else dW_K.add_(part)       # parts in order: deterministic
+        if red is not None:
+            red.add([dW_K])
+            red.finish()
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None, None
 
 
 class DistSIRConvFunction16(torch.autograd.Function):
@@ -531,20 +656,26 @@ class DistSIRConvFunction16(torch.autograd.Function):
     per peer than the single-GPU sum; within the AMP tolerance)."""
 
     @staticmethod
-    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on, dt, drop=None):
+    def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on, dt, drop=None,
+                reduce=False):
         H = W_Q.shape[0]
         n = dg.n_rows
+        ctx.reduce = reduce
         dev = X.device
         X = X.contiguous()
         dq, dk = _drops(drop, dg.row_begin)
         K_ext = torch.empty((dg.n_ext, H), device=dev, dtype=dt)
-        if X.dtype == dt:
-            Xh = X
-            linalg.mm16_wt(X, W_K, None, dt, out=K_ext[:n], drop=dk)
-        else:       # X.to(dt) fused into the K GEMM's loads; the rounded X (for dW) written by it
-            Xh = torch.empty(X.shape, dtype=dt, device=dev)
-            linalg.mm16_wt(X, W_K, None, dt, acopy=Xh, out=K_ext[:n], drop=dk)
-        works = [dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True) for c in range(dg.chunks)]
+        Xh = X if X.dtype == dt else torch.empty(X.shape, dtype=dt, device=dev)
+        works = []
+        for c in range(max(dg.chunks, 1)):           # K part by part; chunk c leaves after part c
+            a, b = dg.own_range(c)
+            if b > a:
+                if X.dtype == dt:
+                    linalg.mm16_wt(X[a:b], W_K, None, dt, out=K_ext[a:b], drop=_drop_at(dk, a))
+                else:       # X.to(dt) fused into the K GEMM's loads; the rounded X (for dW) written by it
+                    linalg.mm16_wt(X[a:b], W_K, None, dt, acopy=Xh[a:b], out=K_ext[a:b], drop=_drop_at(dk, a))
+            if c < dg.chunks:
+                works.append(dg.gather_chunk(c, K_ext[:n], K_ext, async_op=True))
         Q = linalg.mm16_wt(Xh, W_Q, b_Q, dt, drop=dq)
         S = torch.empty((n, H), device=dev, dtype=dt)
         training = grad_on and any(ctx.needs_input_grad[:6])
@@ -576,6 +707,7 @@ class DistSIRConvFunction16(torch.autograd.Function):
         n = dg.n_rows
         dev = Xh.device
         dY = dY.contiguous().to(dt)
+        red = _GradReducer(dg.group) if ctx.reduce else None
         G = linalg.mm16_w(dY, W_R, dt)
         dQ = torch.empty((n, H), device=dev, dtype=dt)
         big, dK_ext, recvs = _backward_buffers(dg, H, dev, dt)
@@ -585,18 +717,29 @@ class DistSIRConvFunction16(torch.autograd.Function):
         dW_R = db_R = None
         if ctx.needs_input_grad[4] or ctx.needs_input_grad[5]:
             dW_R, db_R = _weight_and_bias_grad16(dY, S, ctx.needs_input_grad[4], ctx.has_br and ctx.needs_input_grad[5])
+        if red is not None:
+            red.add([dW_R, db_R])
         dX = linalg.mm16_w(dQ, W_Q, dt, out_dtype=torch.float32) if ctx.needs_input_grad[0] else None
         dW_Q = db_Q = None
         if ctx.needs_input_grad[1] or (ctx.has_bq and ctx.needs_input_grad[2]):
             dW_Q, db_Q = _weight_and_bias_grad16(dQ, Xh, True, ctx.has_bq and ctx.needs_input_grad[2])
-        dK = _complete_dk(dg, big, recvs, works, backend)
-        if dk is not None:
-            _native.dropout_apply(dK, dk)
+        if red is not None:
+            red.add([dW_Q, db_Q])
+        dW_K = None
+        for c, (dK, a, b) in enumerate(_complete_dk_parts(dg, big, recvs, works, backend)):
+            if dk is not None:
+                _native.dropout_apply(dK, _drop_at(dk, a))
+            if dX is not None:
+                dX[a:b] += linalg.mm16_w(dK, W_K, dt, out_dtype=torch.float32)
+            if ctx.needs_input_grad[3]:
+                part = _weight_and_bias_grad16(dK, Xh[a:b], True, False)[0]
+                dW_K = part if dW_K is None else dW_K.add_(part)
         if dX is not None:
-            dX += linalg.mm16_w(dK, W_K, dt, out_dtype=torch.float32)
             dX = dX.to(ctx.x_dtype)
-        dW_K = _weight_and_bias_grad16(dK, Xh, True, False)[0] if ctx.needs_input_grad[3] else None
-        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None, None
+        if red is not None:
+            red.add([dW_K])
+            red.finish()
+        return dX, dW_Q, db_Q, dW_K, dW_R, db_R, None, None, None, None, None, None, None, None, None, None
 
 
 class DistEdgeAggregate(torch.autograd.Function):
@@ -644,6 +787,33 @@ class DistEdgeAggregate(torch.autograd.Function):
         return dQ, dK, None, None, None, None, None, None, None, None
 
 
+class HaloGather(torch.autograd.Function):
+    """K_ext = [K own rows | halo rows of the peers] (forward: the chunked alltoallv); backward: the
+    halo rows' gradients go back to their owners (reverse alltoallv) and are added to the own rows per
+    chunk and peer in a fixed order (deterministic).  The modular edge-cut route (``agg_type='max'``)."""
+
+    @staticmethod
+    def forward(ctx, K, dg):
+        n = dg.n_rows
+        K_ext = torch.empty((dg.n_ext, K.shape[1]), device=K.device, dtype=K.dtype)
+        K_ext[:n] = K
+        dg.gather_halo(K_ext[:n], K_ext)
+        ctx.dg = dg
+        return K_ext
+
+    @staticmethod
+    def backward(ctx, dK_ext):
+        dg = ctx.dg
+        n = dg.n_rows
+        dK_ext = dK_ext.contiguous()
+        dK = dK_ext[:n].clone()
+        for c in range(dg.chunks):
+            recv = torch.empty((dg.send_idx[c].numel(), dK.shape[1]), device=dK.device, dtype=dK.dtype)
+            dg.scatter_chunk(c, dK_ext, recv)
+            dg.add_received(c, dK, recv)
+        return dK, None
+
+
 class DistSIRConv(torch.nn.Module):
     """Wraps a :class:`sirgcn.SIRConv` (same parameters / state_dict) for the edge-cut layout.
 
@@ -652,11 +822,16 @@ class DistSIRConv(torch.nn.Module):
 
     use_fused = True
 
-    def __init__(self, conv, backend=None, use_mask=True):
+    def __init__(self, conv, backend=None, use_mask=True, reduce_in_backward=False):
+        """``reduce_in_backward``: the fused functions all-reduce the weight gradients themselves, dW_R /
+        dW_Q under the reverse exchange and dW_K at the end (RCCL, async); :meth:`allreduce_grads`
+        then skips what they reduced."""
         super().__init__()
         self.conv = conv
         self.backend = backend if backend is not None else _native
         self.use_mask = use_mask
+        self.reduce_in_backward = reduce_in_backward
+        self._reduced = False
 
     def _drop(self, device):
         """(two seeds, p) of this forward's Q / K dropout (conv.py:35,60-61), or None: drawn on the
@@ -670,12 +845,23 @@ class DistSIRConv(torch.nn.Module):
 
     def forward(self, dgraph, feat):
         c = self.conv
-        if c._agg_type not in ("sum", "mean", "sym"):
+        if c._agg_type not in ("sum", "mean", "sym", "max"):
             raise NotImplementedError(f"DistSIRConv: agg_type={c._agg_type!r}")
         if feat.shape[0] != dgraph.n_rows:
             raise ValueError(f"feat has {feat.shape[0]} rows, rank owns {dgraph.n_rows}")
         act, slope = activation_code(c.activation)
         H = c.linear_query.out_features
+        self._reduced = False
+        if c._agg_type == "max":
+            # conv.py:46-47 + fn.max on the edge-cut: Q, K of the own rows, K's halo rows gathered, then
+            # the fused per-edge W_R with the running max (sirgcn.edgemlp) on [own | halo] K rows
+            from .edgemlp import EdgeMaxLinearQK, max_supported
+            if not (feat.is_cuda and self.backend is _native and max_supported(H, c.linear_relation.out_features)):
+                raise NotImplementedError("DistSIRConv max: native GPU path only (H, O <= 512, H % 4 == 0)")
+            Q = c.dropout(c._linear(feat, c.linear_query.weight, c.linear_query.bias))
+            K = c.dropout(c._linear(feat, c.linear_key.weight, None))
+            K_ext = HaloGather.apply(K, dgraph)
+            return EdgeMaxLinearQK.apply(Q, K_ext, c.linear_relation.weight, c.linear_relation.bias, dgraph, act, slope)
         # training dropout inside the fused functions needs the native kernels on device tensors (the
         # hashed masks are applied by sir_dropout_apply / the GEMM epilogues): CPU rehearsals and
         # injected edge backends with p > 0 take the modular path (nn.Dropout) instead
@@ -684,21 +870,23 @@ class DistSIRConv(torch.nn.Module):
                  and c.linear_query.weight.dtype == torch.float32
                  and (drop_native or not (c.training and c.dropout.p > 0)))
         if fused:
+            self._reduced = self.reduce_in_backward
             return DistSIRConvFunction.apply(feat, c.linear_query.weight, c.linear_query.bias, c.linear_key.weight,
                                              c.linear_relation.weight, c.linear_relation.bias, dgraph,
                                              c._agg_type, act, slope, self.backend, self.use_mask,
-                                             torch.is_grad_enabled(), self._drop(feat.device))
+                                             torch.is_grad_enabled(), self._drop(feat.device), self.reduce_in_backward)
         if (self.use_fused and feat.is_cuda and torch.is_autocast_enabled() and H % 4 == 0
                 and c.linear_query.weight.dtype == torch.float32
                 and feat.dtype in (torch.float32, torch.bfloat16, torch.float16)):
             dt = torch.get_autocast_dtype("cuda")
             if dt in (torch.bfloat16, torch.float16):
                 with torch.autocast("cuda", enabled=False):
+                    self._reduced = self.reduce_in_backward
                     return DistSIRConvFunction16.apply(feat, c.linear_query.weight, c.linear_query.bias,
                                                        c.linear_key.weight, c.linear_relation.weight,
                                                        c.linear_relation.bias, dgraph, c._agg_type, act, slope,
                                                        self.backend, self.use_mask, torch.is_grad_enabled(), dt,
-                                                       self._drop(feat.device))
+                                                       self._drop(feat.device), self.reduce_in_backward)
         Q = c.dropout(c.linear_query(feat))
         K = c.dropout(c.linear_key(feat))
         S = DistEdgeAggregate.apply(Q, K, dgraph, H, c._agg_type, act, slope, self.backend, self.use_mask,
@@ -706,6 +894,9 @@ class DistSIRConv(torch.nn.Module):
         return c.linear_relation(S)
 
     def allreduce_grads(self, group=None):
+        if self._reduced:          # the fused backward reduced every weight gradient already
+            self._reduced = False
+            return
         params = [p for p in self.conv.parameters() if p.grad is not None]
         if not params or not dist.is_initialized() or dist.get_world_size(group) == 1:
             return

@@ -210,59 +210,96 @@ class EdgeMaxLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dY):
         QK, W, arg = ctx.saved_tensors
-        plan, H, act1, slope = ctx.plan, ctx.H, ctx.act1, ctx.slope
-        dY = dY.contiguous().float()
-        O = W.shape[0]
-        E = plan.dst.col.numel()
-        dev = dY.device
-        fused = EdgeMaxLinear.fused_bwd
-        if fused is None:
-            need = E * (2 * H + O) * 4
-            # free device memory as the caching allocator sees it: the driver's free bytes plus the
-            # blocks it has reserved but not handed out (a warm training loop holds most memory there)
-            avail = torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-            fused = need > min(EdgeMaxLinear.materialised_budget, int(0.4 * avail))
-            if fused and not max_bwd_fused(H, O):
-                warnings.warn(f"sirgcn max backward: the edge-materialised buffers ({need / 2**30:.1f} GiB) exceed "
-                              f"the budget and the fused backward needs H, O <= 256 (H={H}, O={O}); "
-                              "running the materialised backward anyway")
-        if fused and max_bwd_fused(H, O):
-            dQK, dW, db = _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope)
-            return dQK, dW, (db if ctx.has_b else None), None, None, None, None
-        # the arg edges' activations are needed for dW_R: recompute them once (no copy kept from the
-        # forward).  ReLU family: A = sigma(z) straight from the gather (sign(A) = sign(z), so sigma' is
-        # read off A below and z is never stored); other sigmas: z, then sigma(z).  A LeakyReLU with a
-        # negative slope flips the sign (z < 0 gives A = slope z > 0), so it takes the z route
-        relu_family = act1 == _native.ACT_RELU or (act1 == _native.ACT_LEAKY and slope >= 0)
-        smask = None
-        if relu_family:
-            A = torch.empty((E, H), device=dev, dtype=torch.float32)
-            if H == 256:            # sign words for the gated GEMM: 32 B per edge instead of A's 1 KiB
-                smask = torch.empty((E, 4), device=dev, dtype=torch.int64)
-            _native.edge_gather_act(plan.dst, QK[:, :H], QK[:, H:], act1, slope, A, sign_mask=smask)
-            Z = A
-        else:
-            Z = torch.empty((E, H), device=dev, dtype=torch.float32)
-            _native.edge_gather_add(plan.dst, QK[:, :H], QK[:, H:], Z)
-            A = _act(Z, act1, slope)
-        dM = torch.empty((E, O), device=dev, dtype=torch.float32)
-        _native.segment_max_bwd(plan.dst, arg, dY, dM)                 # dY to the first arg-max edge
-        dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
-        if relu_family:     # dZ = sigma'(z) * (dM W_R) with sigma' read off A in the GEMM's epilogue
-            dZ = linalg.mm_w_dact(dM, W, A, act1, slope, gate_mask=smask)
-            del A, Z, dM
-        else:
-            del A
-            dA = linalg.mm_w(dM, W)                                    # [E, H]
-            del dM
-            dZ = _act_bwd(Z, dA, act1, slope)
-            del Z, dA
+        H = ctx.H
         dQK = torch.empty_like(QK)
-        n_slots = max(plan.dst.n_slots, plan.src.n_slots)
-        part = torch.empty((max(n_slots, 1) * H,), device=dev, dtype=torch.float32) if n_slots else None
-        _native.segment_sum(plan.dst, dZ, dQK[:, :H], partial=part)                     # dQ
-        _native.segment_sum(plan.src, dZ, dQK[:, H:], perm=plan.src.perm, partial=part)  # dK
+        dW, db = max_linear_backward(ctx.plan, QK[:, :H], QK[:, H:], W, arg, dY, ctx.act1, ctx.slope,
+                                     dQK[:, :H], dQK[:, H:])
         return dQK, dW, (db if ctx.has_b else None), None, None, None, None
+
+
+class EdgeMaxLinearQK(torch.autograd.Function):
+    """:class:`EdgeMaxLinear` on separate Q [dst rows, H] and K [src rows, H] (the edge-cut's own-row Q
+    and K_ext = own + halo rows, sirgcn.dist): the plan's dst CSR columns index K, its src CSR rows
+    are K's rows.  Same kernels, same backward routes."""
+
+    @staticmethod
+    def forward(ctx, Q, K, W, b, plan, act1, slope):
+        if Q.device.type != "cuda":
+            raise RuntimeError("sirgcn fused max path needs a ROCm GPU tensor (no CPU fallback)")
+        Q, K = Q.contiguous().float(), K.contiguous().float()
+        W = W.contiguous().float()
+        b = b.contiguous().float() if b is not None else None
+        O = W.shape[0]
+        V = plan.dst.n_rows
+        Y = torch.empty((V, O), device=Q.device, dtype=torch.float32)
+        arg = torch.empty((V, O), device=Q.device, dtype=torch.int32)
+        _fwd(plan, Q, K, W, b, "max", act1, slope, _native.ACT_IDENTITY, Y, arg)
+        ctx.save_for_backward(Q, K, W, arg)
+        ctx.plan, ctx.act1, ctx.slope, ctx.has_b = plan, act1, slope, b is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        Q, K, W, arg = ctx.saved_tensors
+        dQ, dK = torch.empty_like(Q), torch.empty_like(K)
+        dW, db = max_linear_backward(ctx.plan, Q, K, W, arg, dY, ctx.act1, ctx.slope, dQ, dK)
+        return dQ, dK, dW, (db if ctx.has_b else None), None, None, None
+
+
+def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
+    """Backward of Y[v] = max_e (W act1(Q[v] + K[u]) + b): dQ / dK written into the given views,
+    returns (dW, db).  Route by ``EdgeMaxLinear.fused_bwd`` (see there)."""
+    H = Q.shape[1]
+    dY = dY.contiguous().float()
+    O = W.shape[0]
+    E = plan.dst.col.numel()
+    dev = dY.device
+    fused = EdgeMaxLinear.fused_bwd
+    if fused is None:
+        need = E * (2 * H + O) * 4
+        # free device memory as the caching allocator sees it: the driver's free bytes plus the
+        # blocks it has reserved but not handed out (a warm training loop holds most memory there)
+        avail = torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        fused = need > min(EdgeMaxLinear.materialised_budget, int(0.4 * avail))
+        if fused and not max_bwd_fused(H, O):
+            warnings.warn(f"sirgcn max backward: the edge-materialised buffers ({need / 2**30:.1f} GiB) exceed "
+                          f"the budget and the fused backward needs H, O <= 256 (H={H}, O={O}); "
+                          "running the materialised backward anyway")
+    if fused and max_bwd_fused(H, O):
+        return _max_bwd_fused(plan, Q, K, W, arg, dY, H, act1, slope, dQ, dK)
+    # the arg edges' activations are needed for dW_R: recompute them once (no copy kept from the
+    # forward).  ReLU family: A = sigma(z) straight from the gather (sign(A) = sign(z), so sigma' is
+    # read off A below and z is never stored); other sigmas: z, then sigma(z).  A LeakyReLU with a
+    # negative slope flips the sign (z < 0 gives A = slope z > 0), so it takes the z route
+    relu_family = act1 == _native.ACT_RELU or (act1 == _native.ACT_LEAKY and slope >= 0)
+    smask = None
+    if relu_family:
+        A = torch.empty((E, H), device=dev, dtype=torch.float32)
+        if H == 256:            # sign words for the gated GEMM: 32 B per edge instead of A's 1 KiB
+            smask = torch.empty((E, 4), device=dev, dtype=torch.int64)
+        _native.edge_gather_act(plan.dst, Q, K, act1, slope, A, sign_mask=smask)
+        Z = A
+    else:
+        Z = torch.empty((E, H), device=dev, dtype=torch.float32)
+        _native.edge_gather_add(plan.dst, Q, K, Z)
+        A = _act(Z, act1, slope)
+    dM = torch.empty((E, O), device=dev, dtype=torch.float32)
+    _native.segment_max_bwd(plan.dst, arg, dY, dM)                 # dY to the first arg-max edge
+    dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
+    if relu_family:     # dZ = sigma'(z) * (dM W_R) with sigma' read off A in the GEMM's epilogue
+        dZ = linalg.mm_w_dact(dM, W, A, act1, slope, gate_mask=smask)
+        del A, Z, dM
+    else:
+        del A
+        dA = linalg.mm_w(dM, W)                                    # [E, H]
+        del dM
+        dZ = _act_bwd(Z, dA, act1, slope)
+        del Z, dA
+    n_slots = max(plan.dst.n_slots, plan.src.n_slots)
+    part = torch.empty((max(n_slots, 1) * H,), device=dev, dtype=torch.float32) if n_slots else None
+    _native.segment_sum(plan.dst, dZ, dQ, partial=part)                     # dQ
+    _native.segment_sum(plan.src, dZ, dK, perm=plan.src.perm, partial=part)  # dK
+    return dW, db
 
 
 def max_bwd_fused(H, O):
@@ -270,7 +307,7 @@ def max_bwd_fused(H, O):
     return H % 4 == 0 and H <= 256 and O <= 256
 
 
-def _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope):
+def _max_bwd_fused(plan, Q, K, W, arg, dY, H, act1, slope, dQ, dK):
     """``sir_edge_max_bwd_dst`` (dQ, per-block dW_R / db_R partials) + ``sir_edge_max_bwd_src`` (dK):
     dY reaches each (v, o)'s first arg-max edge only; z, a recomputed per edge."""
     lib = _native.load()
@@ -278,8 +315,6 @@ def _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope):
     O = W.shape[0]
     dev = dY.device
     d, s = plan.dst, plan.src
-    dQK = torch.empty_like(QK)
-    Q, K = QK[:, :H], QK[:, H:]
     parts = lib.sir_edge_mlp_bwd_parts(d.n_items, H, O)
     OP, HP = (O + 31) // 32 * 32, (H + 7) // 8 * 8
     wpart = torch.empty((parts, OP * HP + OP), device=dev, dtype=torch.float32)
@@ -288,19 +323,19 @@ def _max_bwd_fused(plan, QK, W, arg, dY, H, act1, slope):
     with _native._Timed("sir_edge_max_bwd_dst", dev):
         rc = lib.sir_edge_max_bwd_dst(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits, H, O,
                                       P(Q), Q.stride(0), P(K), K.stride(0), P(dY), dY.stride(0), P(arg),
-                                      arg.stride(0), act1, float(slope), P(W), P(dQK), dQK.stride(0), P(part),
+                                      arg.stride(0), act1, float(slope), P(W), P(dQ), dQ.stride(0), P(part),
                                       P(wpart), st)
     _native._check(rc, lib)
     with _native._Timed("sir_edge_max_bwd_src", dev):
         rc = lib.sir_edge_max_bwd_src(P(s.rowptr), P(s.col), P(s.perm), P(s.items), s.n_items, P(s.splits),
                                       s.n_splits, H, O, P(K), K.stride(0), P(Q), Q.stride(0), P(dY), dY.stride(0),
-                                      P(arg), arg.stride(0), act1, float(slope), P(W), P(dQK[:, H:]), dQK.stride(0),
+                                      P(arg), arg.stride(0), act1, float(slope), P(W), P(dK), dK.stride(0),
                                       P(part), st)
     _native._check(rc, lib)
     tot = _native.col_sum(wpart)                    # per-block partials summed in block order
     dW = tot[:OP * HP].view(OP, HP)[:O, :H].contiguous()
     db = tot[OP * HP:OP * HP + O].contiguous()
-    return dQK, dW, db
+    return dW, db
 
 
 def _act(z, code, slope):

@@ -68,13 +68,15 @@ def mm_wt(A, W, bias=None, out=None, drop=None):
     return out
 
 
-def mm_w(A, W):
-    """A W; W [K, N]."""
-    if USE_NATIVE and _ok(A) and _w_ok(W, W.shape[1]):
+def mm_w(A, W, out=None):
+    """A W; W [K, N] (into ``out`` when given)."""
+    if USE_NATIVE and _ok(A) and _w_ok(W, W.shape[1]) and (out is None or _ok(out)):
         if _direct_ok(A, W):
-            return _native.gemm_nt_direct(A, W, True)
-        return _native.gemm_nt(A, _native.gemm_pack(W.contiguous(), trans=True))
-    return torch.mm(A, W)
+            return _native.gemm_nt_direct(A, W, True, out=out)
+        return _native.gemm_nt(A, _native.gemm_pack(W.contiguous(), trans=True), out=out)
+    if out is None:
+        return torch.mm(A, W)
+    return torch.mm(A, W, out=out)
 
 
 def mm_w_dact(A, W, gate, act, slope, gate_mask=None):

@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, agg, outdir, fused=True, chunks=None):
+def _worker(rank, world, port, agg, outdir, fused=True, chunks=None, reduce=False):
     for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -41,7 +41,7 @@ def _worker(rank, world, port, agg, outdir, fused=True, chunks=None):
     torch.manual_seed(3)
     conv = SIRConv(d, H, O, nn.LeakyReLU(0.2), 0, agg_type=agg)
     dg = DistGraph.from_global(src, dst, V, rank, world, "cpu", chunk=64, chunks=chunks)
-    dconv = DistSIRConv(conv, backend=cpu_edge_backend)
+    dconv = DistSIRConv(conv, backend=cpu_edge_backend, reduce_in_backward=reduce)
     dconv.use_fused = fused
     r0, r1 = dg.row_begin, dg.row_end
     Xl = X[r0:r1].clone().requires_grad_(True)
@@ -57,15 +57,18 @@ def _worker(rank, world, port, agg, outdir, fused=True, chunks=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,agg,fused,chunks", [(2, "sum", True, None), (2, "sym", True, 1), (3, "mean", True, 3),
-                                                    (4, "sym", True, None), (3, "sum", False, 2),
-                                                    (2, "mean", False, 7)])
-def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg, fused, chunks):
+@pytest.mark.parametrize("world,agg,fused,chunks,reduce", [(2, "sum", True, None, False), (2, "sym", True, 1, False),
+                                                           (3, "mean", True, 3, False), (4, "sym", True, None, False),
+                                                           (3, "sum", False, 2, False), (2, "mean", False, 7, False),
+                                                           (3, "sum", True, 4, True), (2, "sym", True, 2, True)])
+def test_edge_cut_matches_single_process_oracle(tmp_path, world, agg, fused, chunks, reduce):
+    """``reduce``: the weight gradients are all-reduced inside the fused backward (dW_R / dW_Q under the
+    reverse exchange, dW_K last); allreduce_grads() must then leave them alone."""
     import oracle
     from sirgcn.synth import powerlaw_edges
     from torch import nn
     from sirgcn import SIRConv
-    mp.spawn(_worker, args=(world, _free_port(), agg, str(tmp_path), fused, chunks), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), agg, str(tmp_path), fused, chunks, reduce), nprocs=world, join=True)
     parts = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     V, E, d, H, O = 500, 6000, 16, 40, 12
     src, dst = powerlaw_edges(V, E, 0.8, seed=7)

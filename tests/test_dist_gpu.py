@@ -18,7 +18,8 @@ from conftest import rel_err
 
 from sirgcn import _native
 from sirgcn.conv import EdgeAggregate, SIRConv
-from sirgcn.dist import DistGraph, DistSIRConv, DistSIRConvFunction, DistSIRConvFunction16, partition_rows
+from sirgcn.dist import (DistGraph, DistSIRConv, DistSIRConvFunction, DistSIRConvFunction16, _drop_at, _drops,
+                         partition_rows)
 from sirgcn.graph import Graph
 from sirgcn.synth import powerlaw_edges
 from thread_comm import FakeCtx, ThreadComm, run_ranks
@@ -191,13 +192,22 @@ def test_edge_cut_training_dropout_vs_explicit_mask(world, agg):
             g = DistSIRConvFunction.backward(ctx, dY[sl])
         torch.cuda.synchronize()
         n = dg.n_rows
-        mq = _native.dropout_apply(torch.ones(n, H, device=DEV), (seeds[r][0:1], p))
-        mk = _native.dropout_apply(torch.ones(n, H, device=DEV), (seeds[r][1:2], p))
+        # the masks the layer drew: seeds offset by the rank's first row (Q, K) and, for K (projected part
+        # by part), by the part's first row
+        dq, dk = _drops((seeds[r], p), dg.row_begin)
+        mq = _native.dropout_apply(torch.ones(n, H, device=DEV), dq)
+        mk = torch.ones(n, H, device=DEV)
+        for c in range(dg.chunks):
+            a, b = dg.own_range(c)
+            if b > a:
+                _native.dropout_apply(mk[a:b], _drop_at(dk, a))
         return Y, g, mq, mk
 
     outs = run_ranks(world, fn)
     Mk = torch.cat([torch.cat([o[2], o[3]], 1) for o in outs]).cpu()
     assert 0.15 < float((Mk == 0).float().mean()) < 0.25
+    # equal local rows of two ranks draw different bits
+    assert not torch.equal(outs[0][2][:64].cpu(), outs[1][2][:64].cpu())
     got = {"Y": torch.cat([o[0] for o in outs]).cpu(), "dX": torch.cat([o[1][0] for o in outs]).cpu()}
     for i, k in enumerate(("dW_Q", "db_Q", "dW_K", "dW_R", "db_R"), start=1):
         got[k] = sum(o[1][i].double() for o in outs).cpu()
@@ -216,3 +226,56 @@ def test_edge_cut_training_dropout_vs_explicit_mask(world, agg):
     r32, r64 = ref(torch.float32), ref(torch.float64)
     for k, v in got.items():
         assert_parity(v, r32[k], r64[k], 1e-5, f"edge-cut dropout x{world} {agg} {k}", strict=(k == "Y"))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_edge_cut_max_vs_single_gpu(world):
+    """agg_type='max' on the edge-cut (conv.py:46-47 + fn.max): own-row Q, K_ext = [own | halo] K rows
+    gathered by the chunked alltoallv (HaloGather), the fused per-edge W_R with the running max on them
+    (EdgeMaxLinearQK), the halo rows' dK sent back to their owners — against the single-GPU layer with
+    the same weights.  The GEMMs are row-wise, so every Q / K row is the single-GPU value: Y is held to
+    1e-6.  The ranks are threads on the one GPU; their backward runs through the Functions' own
+    backward (the autograd engine has one worker per device: concurrent Tensor.backward calls of
+    threads that exchange rows would deadlock on it)."""
+    from sirgcn.dist import HaloGather
+    from sirgcn.edgemlp import EdgeMaxLinearQK
+    V, E, H, O = 3000, 60000, 128, 64
+    src, dst = powerlaw_edges(V, E, 0.8, seed=21)
+    X = torch.randn(V, 48, generator=torch.Generator().manual_seed(1)).to(DEV)
+    dY = torch.randn(V, O, generator=torch.Generator().manual_seed(2)).to(DEV)
+    torch.manual_seed(4)
+    conv = SIRConv(48, H, O, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
+    xs = X.clone().requires_grad_(True)
+    Ys = conv(Graph(src, dst, V), xs)
+    Ys.backward(dY)
+    ref = {"Y": Ys.detach(), "dX": xs.grad, "dW_Q": conv.linear_query.weight.grad, "db_Q": conv.linear_query.bias.grad,
+           "dW_K": conv.linear_key.weight.grad, "dW_R": conv.linear_relation.weight.grad,
+           "db_R": conv.linear_relation.bias.grad}
+    WQ, bQ, WK = conv.linear_query.weight.detach(), conv.linear_query.bias.detach(), conv.linear_key.weight.detach()
+    WR, bR = conv.linear_relation.weight.detach(), conv.linear_relation.bias.detach()
+    comms = ThreadComm.make(world)
+    bounds = partition_rows(torch.bincount(dst.to(DEV), minlength=V), world)
+
+    def fn(r):
+        dg = DistGraph(src, dst, V, bounds, r, world, DEV, group=comms[r])
+        sl = slice(dg.row_begin, dg.row_end)
+        x = X[sl]
+        with torch.no_grad():
+            Q = x @ WQ.t() + bQ
+            K = x @ WK.t()
+            c1, c2 = FakeCtx((True, False)), FakeCtx((True, True, True, True, False, False, False))
+            K_ext = HaloGather.forward(c1, K, dg)
+            Y = EdgeMaxLinearQK.forward(c2, Q, K_ext, WR, bR, dg, _native.ACT_LEAKY, 0.2)
+            dQ, dK_ext, dWR, dbR = EdgeMaxLinearQK.backward(c2, dY[sl])[:4]
+            dK = HaloGather.backward(c1, dK_ext)[0]
+        torch.cuda.synchronize()
+        return {"Y": Y, "dX": dQ @ WQ + dK @ WK, "dW_Q": dQ.t() @ x, "db_Q": dQ.sum(0), "dW_K": dK.t() @ x,
+                "dW_R": dWR, "db_R": dbR}
+
+    outs = run_ranks(world, fn)
+    got = {k: torch.cat([o[k] for o in outs]) for k in ("Y", "dX")}
+    for k in ("dW_Q", "db_Q", "dW_K", "dW_R", "db_R"):
+        got[k] = sum(o[k].double() for o in outs).float()
+    for k, v in got.items():
+        e = float((v.double() - ref[k].double()).norm() / ref[k].double().norm().clamp_min(1e-30))
+        assert e < (1e-6 if k == "Y" else 1e-5), (k, e)
