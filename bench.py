@@ -511,7 +511,9 @@ def roofline_fwd(args, kernels, V, E, V_src, H, s, world):
     out = {"bound": "hbm", "kernel": "sir_edge_agg_fwd (k_edge<FWD> + k_combine)",
            "achieved": round(phys if phys else ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round((phys if phys else ach) / HBM_PEAK_GBS, 4),
-           "frac_basis": "counter (HBM-side bytes from PMC)" if phys else "algorithmic (no PMC file for this config)",
+           "frac_basis": ("counter: L2-miss bytes from PMC (FETCH_SIZE x2 + WRITE_SIZE); FETCH_SIZE also counts "
+                          "Infinity-Cache (MALL) hits, so this is an upper bound on physical HBM bytes")
+                         if phys else "algorithmic (no PMC file for this config)",
            "traffic": traffic, "traffic_source": traffic_source, "algorithmic_bytes": alg, "ms_per_launch": k["ms"],
            "achieved_algorithmic": round(ach, 1), "frac_algorithmic": round(frac_alg, 4),
            "bytes_formula": "SURVEY 8(d): E*(s_i + H*s) + V*(2*H*s + s_i)",

@@ -182,12 +182,13 @@ class EdgeMLPSum(torch.autograd.Function):
 class EdgeMaxLinear(torch.autograd.Function):
     """Y[v] = max_e (W_R act1(Q[v] + K[u]) + b_R), first arg-max edge (DGL fn.max), empty rows 0.
 
-    Backward route (``fused_bwd``): ``None`` (default) picks by memory — the edge-materialised
-    backward (z recomputed once into [E, H], dM [E, O]; its GEMMs on the split-fp16 MFMA kernels) when
-    its buffers, E (2H + O) 4 bytes, stay within ``materialised_budget`` (48 GiB, and 40 % of the free
-    device memory), else the fused backward (no [E, *] buffer; its three edge-contracted products
-    run on fp32 MFMA, ~4x slower on MI355X at S1: the route of the S2 shape, whose buffers would take
-    123 GB); ``True`` / ``False`` force one (tests)."""
+    Backward route (``fused_bwd``): ``None`` (default) — the edge-materialised backward (z recomputed
+    once into [E, H], dM [E, O]; its GEMMs on the split-fp16 MFMA kernels), over the whole graph when its
+    buffers, E (2H + O) 4 bytes, stay within ``materialised_budget`` (48 GiB, and 40 % of the free device
+    memory), else over destination-row ranges that each fit it (the S2 shape, 123 GB of buffers: 4
+    ranges; r05: 710 -> see DESIGN §8 ms per S2 step against the fused route); ``True`` — the fused
+    backward (no [E, *] buffer; its three edge-contracted products on fp32 MFMA, 14x slower at S2);
+    ``False`` — the materialised one (tests)."""
     fused_bwd = None
     materialised_budget = 48 << 30
 
@@ -255,18 +256,78 @@ def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
     E = plan.dst.col.numel()
     dev = dY.device
     fused = EdgeMaxLinear.fused_bwd
-    if fused is None:
-        need = E * (2 * H + O) * 4
-        # free device memory as the caching allocator sees it: the driver's free bytes plus the
-        # blocks it has reserved but not handed out (a warm training loop holds most memory there)
-        avail = torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-        fused = need > min(EdgeMaxLinear.materialised_budget, int(0.4 * avail))
-        if fused and not max_bwd_fused(H, O):
-            warnings.warn(f"sirgcn max backward: the edge-materialised buffers ({need / 2**30:.1f} GiB) exceed "
-                          f"the budget and the fused backward needs H, O <= 256 (H={H}, O={O}); "
-                          "running the materialised backward anyway")
     if fused and max_bwd_fused(H, O):
         return _max_bwd_fused(plan, Q, K, W, arg, dY, H, act1, slope, dQ, dK)
+    per_edge = (2 * H + O) * 4
+    # free device memory as the caching allocator sees it: the driver's free bytes plus the blocks it
+    # has reserved but not handed out (a warm training loop holds most memory there)
+    avail = torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    budget = min(EdgeMaxLinear.materialised_budget, int(0.4 * avail))
+    if E * per_edge > budget and E > 0:
+        # the [E, *] buffers exceed the budget: the same dataflow over destination-row ranges of
+        # <= budget / per_edge edges each (the S2 shape: 123 GB of buffers -> 3 ranges of <= 48 GiB)
+        # range size quantised to 4 Mi edges (a stable cache key while the free memory moves)
+        e_max = max((budget // per_edge) >> 22 << 22, 1 << 20)
+        return _max_bwd_ranges(plan, Q, K, W, arg, dY, act1, slope, dQ, dK, e_max)
+    return _max_bwd_materialised(plan.dst, plan.src, Q, K, W, arg, dY, act1, slope, dQ, dK)
+
+
+def _max_bwd_ranges(plan, Q, K, W, arg, dY, act1, slope, dQ, dK, e_max):
+    """The edge-materialised max backward over destination-row ranges of <= e_max edges: each range is
+    its own sub-graph (rows rebased to 0, its edges in dst-CSR order, a source-side CSR over all K rows;
+    built once per plan and cached), dW_R / db_R summed over the ranges in order, dK accumulated
+    over the ranges in order (deterministic)."""
+    key = ("max_ranges", int(e_max))
+    cache = getattr(plan, "_sub_plans", None)
+    if cache is None:
+        cache = plan._sub_plans = {}
+    if key not in cache:
+        cache[key] = _row_ranges(plan.dst, K.shape[0], int(e_max))
+    dW = db = None
+    first = True
+    for r0, r1, e0, d_c, s_c in cache[key]:
+        dK_c = dK if first else torch.empty_like(dK)
+        a_c = arg[r0:r1] - e0 if e0 else arg[r0:r1]                # arg edges as positions inside the range
+        w, b = _max_bwd_materialised(d_c, s_c, Q[r0:r1], K, W, a_c, dY[r0:r1], act1, slope, dQ[r0:r1], dK_c)
+        if first:
+            dW, db = w, b
+        else:
+            dW += w
+            db += b
+            dK += dK_c
+        first = False
+    return dW, db
+
+
+def _row_ranges(dst, n_src, e_max):
+    """[(r0, r1, e0, dst sub-CSR, src sub-CSR)] of consecutive destination rows holding <= e_max edges
+    (a row longer than e_max gets a range of its own)."""
+    from .graph import build_plans_native
+    rp = dst.rowptr.to(torch.int64).cpu()
+    n = rp.numel() - 1
+    out, r0 = [], 0
+    while r0 < n:
+        e0 = int(rp[r0])
+        r1 = int(torch.searchsorted(rp, torch.tensor(e0 + e_max), right=True)) - 1
+        r1 = min(max(r1, r0 + 1), n)
+        e1 = int(rp[r1])
+        deg = (dst.rowptr[r0 + 1:r1 + 1] - dst.rowptr[r0:r1]).to(torch.int64)
+        rows = torch.repeat_interleave(torch.arange(r1 - r0, device=deg.device), deg)
+        d_c, s_c = build_plans_native(dst.col[e0:e1].to(torch.int64), rows, r1 - r0, n_src)
+        out.append((r0, r1, e0, d_c, s_c))
+        r0 = r1
+    return out
+
+
+def _max_bwd_materialised(dcsr, scsr, Q, K, W, arg, dY, act1, slope, dQ, dK):
+    """The edge-materialised max backward over one (sub-)graph: z recomputed once into [E, H], dM = dY
+    routed to the first arg-max edges [E, O], dW_R = dM^T A and dZ = sigma'(z) (dM W_R) on the split-fp16
+    GEMMs, dQ / dK by native segment sums.  Returns (dW, db)."""
+    H = Q.shape[1]
+    O = W.shape[0]
+    E = dcsr.col.numel()
+    dev = dY.device
+    dY = dY.contiguous()
     # the arg edges' activations are needed for dW_R: recompute them once (no copy kept from the
     # forward).  ReLU family: A = sigma(z) straight from the gather (sign(A) = sign(z), so sigma' is
     # read off A below and z is never stored); other sigmas: z, then sigma(z).  A LeakyReLU with a
@@ -277,14 +338,14 @@ def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
         A = torch.empty((E, H), device=dev, dtype=torch.float32)
         if H == 256:            # sign words for the gated GEMM: 32 B per edge instead of A's 1 KiB
             smask = torch.empty((E, 4), device=dev, dtype=torch.int64)
-        _native.edge_gather_act(plan.dst, Q, K, act1, slope, A, sign_mask=smask)
+        _native.edge_gather_act(dcsr, Q, K, act1, slope, A, sign_mask=smask)
         Z = A
     else:
         Z = torch.empty((E, H), device=dev, dtype=torch.float32)
-        _native.edge_gather_add(plan.dst, Q, K, Z)
+        _native.edge_gather_add(dcsr, Q, K, Z)
         A = _act(Z, act1, slope)
     dM = torch.empty((E, O), device=dev, dtype=torch.float32)
-    _native.segment_max_bwd(plan.dst, arg, dY, dM)                 # dY to the first arg-max edge
+    _native.segment_max_bwd(dcsr, arg, dY, dM)                     # dY to the first arg-max edge
     dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
     if relu_family:     # dZ = sigma'(z) * (dM W_R) with sigma' read off A in the GEMM's epilogue
         dZ = linalg.mm_w_dact(dM, W, A, act1, slope, gate_mask=smask)
@@ -295,10 +356,10 @@ def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
         del dM
         dZ = _act_bwd(Z, dA, act1, slope)
         del Z, dA
-    n_slots = max(plan.dst.n_slots, plan.src.n_slots)
+    n_slots = max(dcsr.n_slots, scsr.n_slots)
     part = torch.empty((max(n_slots, 1) * H,), device=dev, dtype=torch.float32) if n_slots else None
-    _native.segment_sum(plan.dst, dZ, dQ, partial=part)                     # dQ
-    _native.segment_sum(plan.src, dZ, dK, perm=plan.src.perm, partial=part)  # dK
+    _native.segment_sum(dcsr, dZ, dQ, partial=part)                     # dQ
+    _native.segment_sum(scsr, dZ, dK, perm=scsr.perm, partial=part)     # dK
     return dW, db
 
 

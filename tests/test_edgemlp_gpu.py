@@ -318,3 +318,28 @@ def test_max_negative_slope_leaky_both_backwards(fused, monkeypatch):
     for k, kr in (("Y", "Y"), ("dX", "dX"), ("linear_query.weight", "dW_Q"), ("linear_key.weight", "dW_K"),
                   ("linear_relation.weight", "dW_R"), ("linear_relation.bias", "db_R")):
         assert_parity(got[k], r32[kr], r64[kr], 1e-5, f"max leaky(-0.2) fused={fused} {k}", strict=(k == "Y"))
+
+
+def test_max_backward_row_ranges_match_whole_graph(monkeypatch):
+    """Over budget, the edge-materialised max backward runs over destination-row ranges (the S2 shape):
+    each range a rebased sub-graph, dW_R / db_R / dK summed over the ranges in order.  dQ rows are
+    summed inside one range in the whole graph's order (bit-identical); the rest within fp32 rounding."""
+    from sirgcn import edgemlp
+    from sirgcn.edgemlp import EdgeMaxLinear
+    src, dst, V, gen = _graph(131)
+    X, dY = torch.randn(V, 32, generator=gen), torch.randn(V, 256, generator=gen)
+    torch.manual_seed(13)
+    m = SIRConv(32, 256, 256, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
+    g = Graph(src, dst, V)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", None)
+    whole = _run(m, g, X, dY)
+    calls = []
+    orig = edgemlp._max_bwd_ranges
+    monkeypatch.setattr(edgemlp, "_max_bwd_ranges", lambda *a: calls.append(a[-1]) or orig(*a[:-1], 3000))
+    monkeypatch.setattr(EdgeMaxLinear, "materialised_budget", 1 << 20)     # 1 MiB: forces the ranges
+    ranged = _run(m, g, X, dY)
+    assert calls, "the row-range route was not taken"
+    assert torch.equal(ranged["Y"], whole["Y"])
+    for k in whole:
+        e = float((ranged[k].double() - whole[k].double()).norm() / whole[k].double().norm().clamp_min(1e-30))
+        assert e < 1e-6, (k, e)
