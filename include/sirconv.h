@@ -420,7 +420,8 @@ int sir_gemm_nt_dact(const float* A, int64_t lda, int64_t M, int64_t K, const vo
 /* Small batches (config 5's 1.6k-node molecule batches): C[M, N] = A[M, K] B^T + bias with the
  * weight read as fp32 straight from W (B[n][k] = W[n*ldw + k], trans = 0, or W[k*ldw + n], trans =
  * 1) — no packing pass per weight update; both operands split in the kernel, each with running
- * scales.  Same accuracy bar as sir_gemm_nt (fp32-equivalent); any M, but the 32 x 32 tiles and the
+ * scales.  Same accuracy bar as sir_gemm_nt (fp32-equivalent); any M, but the small tiles (64 weight
+ * lines x 32 rows, LDS-DMA staged; a 4-byte-aligned W takes a register-load kernel) and the
  * in-kernel weight split make it the route for M below ~16k rows only.  K, N, lda, ldc multiples of
  * 4; A, C, bias 16-B aligned; ldw <= SIR_GEMM_MAX_LD.  Replaces addmm(b, X, W^T) / mm(X, W). */
 int sir_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int64_t K, const float* W, int64_t ldw, int trans,

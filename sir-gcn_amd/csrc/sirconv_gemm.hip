@@ -29,6 +29,7 @@
 // LDS stage image (both kernels): [part hi/lo][k-step 0/1][rows in fimg order] — one k-step of
 // 32 rows is 1 KiB contiguous, exactly one ds_read_b128 per lane, in lane order (conflict-free).
 #include <type_traits>
+#include <algorithm>
 
 #include "sirconv_internal.h"
 #include "sirconv_gemm_util.h"
@@ -1423,23 +1424,72 @@ struct SOp {
     }
 };
 
-// The contraction of one wave: chunks q, q + 4, ... < nc; returns the partial tile in true scale
-// (acc * 2^-se0(row i) * 2^-se1(lane column)) in p, and (if CS) the sums of the lane's src0 values.
-template <bool C0, bool C1, bool CS>
-__device__ __forceinline__ void small_contract(const SOp<C0>& o0, const SOp<C1>& o1, int nc, int q, int h,
-                                               float (&p)[16], float& cs) {
-    float csc = 0.f;            // Kahan compensation of the column sum
+// One wave's 32 x 32 split-fp16 tile, fed one 32-k chunk at a time: x0 = the lane's 16 values of
+// its src0 line (MFMA row), x1 of its src1 line (MFMA column), each line with its running scale
+// (k_gemm_tn's rule); with CS also the Kahan sum of the lane's src0 values.
+struct SplitTile {
     f16v acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     int se0 = SE_INIT, se1 = SE_INIT;
     bool first = true;
-    auto colmax = [&](const float (&x)[16]) {
+    float cs = 0.f, csc = 0.f;
+    __device__ __forceinline__ SplitTile() {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    }
+    static __device__ __forceinline__ float colmax(const float (&x)[16]) {
         float mm = 0.f;
 #pragma unroll
         for (int i = 0; i < 16; i += 4) mm = fmax4(mm, make_float4(x[i], x[i + 1], x[i + 2], x[i + 3]));
-        return fmaxf(mm, __shfl_xor(mm, 32));
-    };
+        // with the partner half (lane ^ 32): v_permlane32_swap, no LDS round trip
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mm), __float_as_uint(mm), false, false);
+        return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    template <bool CS>
+    __device__ __forceinline__ void step(const float (&x0)[16], const float (&x1)[16], int h) {
+        const int s0 = first ? SE_INIT : se0, s1 = first ? SE_INIT : se1;
+        se0 = next_se(s0, bexp(colmax(x0)));
+        se1 = next_se(s1, bexp(colmax(x1)));
+        if (!first) {
+            const float f0 = pow2(se0 - s0), f1 = pow2(se1 - s1);
+            if (__builtin_amdgcn_ballot_w64(f0 != 1.f || f1 != 1.f) != 0) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] *= __shfl(f0, (i & 3) + 8 * (i >> 2) + 4 * h) * f1;
+            }
+        }
+        first = false;
+        if constexpr (CS) {
+            float t = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) t += x0[i];
+            kahan_add(cs, csc, t);
+        }
+        h8 ah[2], al[2], bh[2], bl[2];
+        const float sa = pow2(se0), sb = pow2(se1);
+        split8(make_float4(x0[0], x0[1], x0[2], x0[3]), make_float4(x0[4], x0[5], x0[6], x0[7]), sa, ah[0], al[0]);
+        split8(make_float4(x0[8], x0[9], x0[10], x0[11]), make_float4(x0[12], x0[13], x0[14], x0[15]), sa, ah[1], al[1]);
+        split8(make_float4(x1[0], x1[1], x1[2], x1[3]), make_float4(x1[4], x1[5], x1[6], x1[7]), sb, bh[0], bl[0]);
+        split8(make_float4(x1[8], x1[9], x1[10], x1[11]), make_float4(x1[12], x1[13], x1[14], x1[15]), sb, bh[1], bl[1]);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh[ks], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl[ks], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh[ks], acc, 0, 0, 0);
+        }
+    }
+    // the tile in true scale: acc * 2^-se0(row i) * 2^-se1(lane column)
+    __device__ __forceinline__ void result(float (&p)[16], int h) const {
+        const float i0 = pow2(-se0), i1 = pow2(-se1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) p[i] = acc[i] * __shfl(i0, (i & 3) + 8 * (i >> 2) + 4 * h) * i1;
+    }
+};
+
+// The contraction of one wave: chunks q, q + 4, ... < nc; returns the partial tile in true scale
+// in p, and (if CS) the sums of the lane's src0 values.
+template <bool C0, bool C1, bool CS>
+__device__ __forceinline__ void small_contract(const SOp<C0>& o0, const SOp<C1>& o1, int nc, int q, int h,
+                                               float (&p)[16], float& cs) {
+    SplitTile t;
     for (int cb = q; cb < nc; cb += 16) {
         float x0[4][16], x1[4][16];
 #pragma unroll
@@ -1454,40 +1504,11 @@ __device__ __forceinline__ void small_contract(const SOp<C0>& o0, const SOp<C1>&
             if (c >= nc) break;
             o0.mask_tail(x0[g], c, h);
             o1.mask_tail(x1[g], c, h);
-            const int s0 = first ? SE_INIT : se0, s1 = first ? SE_INIT : se1;
-            se0 = next_se(s0, bexp(colmax(x0[g])));
-            se1 = next_se(s1, bexp(colmax(x1[g])));
-            if (!first) {
-                const float f0 = pow2(se0 - s0), f1 = pow2(se1 - s1);
-                if (__builtin_amdgcn_ballot_w64(f0 != 1.f || f1 != 1.f) != 0) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) acc[i] *= __shfl(f0, (i & 3) + 8 * (i >> 2) + 4 * h) * f1;
-                }
-            }
-            first = false;
-            if constexpr (CS) {
-                float t = 0.f;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) t += x0[g][i];
-                kahan_add(cs, csc, t);
-            }
-            h8 ah[2], al[2], bh[2], bl[2];
-            const float sa = pow2(se0), sb = pow2(se1);
-            split8(make_float4(x0[g][0], x0[g][1], x0[g][2], x0[g][3]), make_float4(x0[g][4], x0[g][5], x0[g][6], x0[g][7]), sa, ah[0], al[0]);
-            split8(make_float4(x0[g][8], x0[g][9], x0[g][10], x0[g][11]), make_float4(x0[g][12], x0[g][13], x0[g][14], x0[g][15]), sa, ah[1], al[1]);
-            split8(make_float4(x1[g][0], x1[g][1], x1[g][2], x1[g][3]), make_float4(x1[g][4], x1[g][5], x1[g][6], x1[g][7]), sb, bh[0], bl[0]);
-            split8(make_float4(x1[g][8], x1[g][9], x1[g][10], x1[g][11]), make_float4(x1[g][12], x1[g][13], x1[g][14], x1[g][15]), sb, bh[1], bl[1]);
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bh[ks], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[ks], bl[ks], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[ks], bh[ks], acc, 0, 0, 0);
-            }
+            t.step<CS>(x0[g], x1[g], h);
         }
     }
-    const float i0 = pow2(-se0), i1 = pow2(-se1);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) p[i] = acc[i] * __shfl(i0, (i & 3) + 8 * (i >> 2) + 4 * h) * i1;
+    t.result(p, h);
+    cs = t.cs;
 }
 
 // C[d0 + r][n0 + n] = sum_k A[d0 + r][k] W(n0 + n, k) + bias: src0 = W lines (features), src1 = A rows
@@ -1595,6 +1616,244 @@ k_gemm_reduce2(const float* __restrict__ part, int P, int64_t count, int Nc, flo
     else C[(i / Nc) * ldc + i % Nc] = s;
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS-tiled small GEMMs (the small-batch route: config 5's 1.6k-node batches).  A block of 4 waves
+// owns a (32 W0) x (32 W1) output tile: W0 x W1 waves of 32 x 32, times WK waves that take the
+// 32-k chunks of each step in turn (partials added in LDS, in wave order).  The operands' k-slices
+// of a step (32 WK k) go global -> LDS by LDS-DMA (global_load_lds_dwordx4: no registers, whole
+// 128-byte lines per 8 lanes) into a ring of NS stage buffers, NS - 1 steps in flight ahead of the
+// one being read (counted vmcnt + a raw barrier; the 4-wave k_gemm_nt_sw / k_gemm_tn_s load 16
+// scattered bytes per line and lane, every wave its own copy, one memory latency per 4 chunks);
+// each wave then reads its lines in the MFMA operand layout and runs SplitTile on them.
+// Operand 0 feeds the MFMA rows, operand 1 the columns.  CONTIG operands are line-major in memory
+// (x[line * ld + k]: A rows, an nn.Linear weight), imaged [line][32 WK k] with the 16-byte slots of
+// each line XOR-swizzled (the DMA writes lane-linear; the swizzle goes on the source address, the
+// reads undo it: conflict-free ds_read_b128); strided ones are k-major (x[k * ld + line]: the
+// node-row contraction of the weight gradients, a transposed weight), imaged [k][line].
+//   EPI 0 (NT): C[op1 line][op0 line] = sum_k + bias, dropout  (op0 = W lines, op1 = A rows)
+//   EPI 1 (TN): part[p][op0 line][op1 line] (+ column sums of op0)  (op0 = A cols, op1 = B cols)
+template <bool C0, bool C1, int W0, int W1, int WK, int NS>
+struct Lt {
+    static constexpr int L0 = 32 * W0, L1 = 32 * W1, KS = 32 * WK;
+    static constexpr int F0 = L0 * KS, F1 = L1 * KS;                          // floats per stage image
+    static constexpr int BUF = F0 + F1;
+    static constexpr int N0 = L0 * KS / 1024, N1 = L1 * KS / 1024;            // DMAs per thread per step
+    static constexpr int D = N0 + N1;
+    static constexpr int RED = (WK - 1) * W0 * W1 * 16 * 64;                  // partial-tile floats
+    static constexpr int CRED = 2 * W0 * 32 * WK;                             // column-sum halves
+    static constexpr int LDS = (NS * BUF > RED + CRED ? NS * BUF : RED + CRED);
+    static_assert(W0 * W1 * WK == 4, "4 waves");
+    static_assert(N0 >= 1 && N1 >= 1, "a DMA per thread");
+    static_assert(NS >= 2 && (NS - 2) * D <= 63, "vmcnt range");
+};
+
+__device__ __attribute__((aligned(16))) float g_lt_zero[4];    // source of the DMAs past the operand
+
+// one operand of the block: element (line, k) of the block's tile at x[line * ld + k] (CONTIG) or
+// x[k * ld + line]; lines >= `lines` and k >= `klen` read as zeros (k in 4-aligned groups: klen % 4 == 0
+// for CONTIG operands, checked by the launchers).  Thread t fills the 16-byte slots u = t + 256 i
+// (i < N) of every step's image (wave-instruction i of wave w: slots 256 i + 64 w + lane); the
+// slot's source at step 0 and its k offset are set up once, a step adds s * KS (CONTIG) or
+// s * KS * ld (strided) elements.
+template <bool CONTIG, int L, int KS>
+struct LtOp {
+    static constexpr int NC = KS / 4;                                 // 16-byte slots per image line
+    static constexpr int N = L * KS / 1024;
+    const float* src[N];
+    int kof[N];                                                       // slot k at step 0 (INT_MAX: dead line)
+    int64_t step;                                                     // elements per step
+    int klen;
+    __device__ __forceinline__ static int swz(int line) { return KS == 32 ? (line >> 1) & 7 : line & (NC - 1); }
+    __device__ __forceinline__ LtOp(const float* x, int64_t ld, int lines, int klen_, int t) : klen(klen_) {
+        step = CONTIG ? (int64_t)KS : (int64_t)KS * ld;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int u = t + 256 * i;
+            int line, k;
+            if constexpr (CONTIG) { line = u / NC; k = 4 * ((u % NC) ^ swz(u / NC)); }
+            else { k = u / (L / 4); line = 4 * (u % (L / 4)); }
+            src[i] = CONTIG ? x + (int64_t)line * ld + k : x + (int64_t)k * ld + line;
+            kof[i] = line < lines ? k : 0x7fffffff - KS * 4096;
+        }
+    }
+    __device__ __forceinline__ const float* at(int i, int s) const {
+        return s * KS + kof[i] < klen ? src[i] + s * step : g_lt_zero;
+    }
+    // the lane's 16 values of its line j, chunk kc of the step (k = 32 kc + 16 (i >> 3) + 8 h + (i & 7))
+    __device__ __forceinline__ static void read(const float* img, int j, int kc, int h, float (&x)[16]) {
+        if constexpr (CONTIG) {
+            const int sw = swz(j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = 8 * kc + 4 * (i >> 1) + 2 * h + (i & 1);
+                const float4 v = *reinterpret_cast<const float4*>(img + j * KS + 4 * (c ^ sw));
+                x[4 * i + 0] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = img[(32 * kc + (i >> 3) * 16 + 8 * h + (i & 7)) * L + j];
+        }
+    }
+};
+
+// One LDS-DMA wave-instruction: lane l's 16 bytes at g go to LDS lds_wave_base + 16 l.  Inline asm,
+// not the builtin: hipcc makes every ds_read wait vmcnt(0) behind a visible LDS-DMA (the ring's
+// later steps would drain at each read); the waits are ours (wait_vm), M0 saved around the
+// statement (the compiler does not preserve it for us).
+__device__ __forceinline__ void dma16(const float* g, float* lds_wave_base) {
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_wave_base);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+}
+// LDS barrier without the vector-memory drain of __syncthreads (the DMAs of later steps stay in flight)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+
+// tools/dbg/lt_trace.hip: per-block phase clocks (s_memtime) of k_gemm_lt, wave 0 lane 0
+#ifdef SIR_LT_TRACE
+__device__ uint64_t* g_lt_trace;
+#define SIR_LT_TRACE_AT(i, v) do { if (threadIdx.x == 0) g_lt_trace[blockIdx.x * 24 + (i)] = (v); } while (0)
+#else
+#define SIR_LT_TRACE_AT(i, v) do { } while (0)
+#endif
+template <bool C0, bool C1, int W0, int W1, int WK, int NS, int EPI>
+__global__ void __launch_bounds__(256)
+k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X1, int64_t ld1, int64_t n0lines,
+          int64_t n1lines, int64_t klen_all, int nt0, int nt1, int64_t rps, const float* __restrict__ bias,
+          float* __restrict__ C, int64_t ldc, float* __restrict__ csum_part, Drop drop) {
+    using G = Lt<C0, C1, W0, W1, WK, NS>;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS];
+    const int t = threadIdx.x, l = t & 63, j = l & 31, h = l >> 5, w = t >> 6;
+    const int w0 = w % W0, w1 = (w / W0) % W1, wk = w / (W0 * W1);
+    const int tiles = nt0 * nt1;
+    // XCD-aware: consecutive ids on one XCD, so an XCD's blocks share their op1 rows (NT: A row
+    // tiles, each read by the XCD that owns it; TN: row splits) and only the small op0 is read by
+    // all eight L2s
+    const int bid = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int64_t p = bid / tiles;                              // TN: the row split
+    const int t0 = (bid % tiles) % nt0, t1 = (bid % tiles) / nt0;
+    const int64_t a0 = (int64_t)t0 * G::L0, a1 = (int64_t)t1 * G::L1;    // first line of each operand
+    const int lines0 = (int)(n0lines - a0 < G::L0 ? n0lines - a0 : G::L0);
+    const int lines1 = (int)(n1lines - a1 < G::L1 ? n1lines - a1 : G::L1);
+    const int64_t v0 = p * rps;
+    const int klen = (int)(klen_all - v0 < rps ? klen_all - v0 : rps);
+    const LtOp<C0, G::L0, G::KS> o0(C0 ? X0 + a0 * ld0 + v0 : X0 + v0 * ld0 + a0, ld0, lines0, klen, t);
+    const LtOp<C1, G::L1, G::KS> o1(C1 ? X1 + a1 * ld1 + v0 : X1 + v0 * ld1 + a1, ld1, lines1, klen, t);
+    const int nsteps = klen > 0 ? (klen + G::KS - 1) / G::KS : 0;
+    constexpr bool CS = EPI == 1;
+    const bool do_cs = CS && csum_part != nullptr && t1 == 0 && w1 == 0;
+
+    // step s's DMAs into stage buffer s % NS (steps past the last read zeros into a free buffer, so
+    // every step issues the same count and the waits stay compile-time)
+    auto issue = [&](int s) {
+        float* img = lds + (s % NS) * G::BUF;
+#pragma unroll
+        for (int i = 0; i < G::N0; ++i) dma16(o0.at(i, s), img + (256 * i + 64 * w) * 4);
+#pragma unroll
+        for (int i = 0; i < G::N1; ++i) dma16(o1.at(i, s), img + G::F0 + (256 * i + 64 * w) * 4);
+    };
+    // the epilogue's bias and dropout seed, loaded ahead of the loop (their latency off the tail)
+    float4 bb[4];
+    if constexpr (EPI == 0) {
+        drop = drop_resolve(drop);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int64_t n = a0 + 32 * w0 + 8 * g + 4 * h;
+            bb[g] = (bias != nullptr && n < n0lines) ? *reinterpret_cast<const float4*>(bias + n)
+                                                     : make_float4(-0.f, -0.f, -0.f, -0.f);
+        }
+    }
+    SplitTile tile;
+    SIR_LT_TRACE_AT(0, __builtin_amdgcn_s_memrealtime());
+    SIR_LT_TRACE_AT(1, __builtin_amdgcn_s_memtime());
+    if (nsteps > 0) {
+#pragma unroll
+        for (int q = 0; q < NS - 1; ++q) issue(q);
+    }
+    SIR_LT_TRACE_AT(2, __builtin_amdgcn_s_memtime());
+    for (int s = 0; s < nsteps; ++s) {
+        wait_vm<(NS - 2) * G::D>();                             // this thread's DMAs of step s landed
+        lds_barrier();                                          // everyone's; step s - 1's reads done
+        SIR_LT_TRACE_AT(4 + 2 * (s & 7), __builtin_amdgcn_s_memtime());
+        issue(s + NS - 1);                                      // into the buffer step s - 1 used
+        if (s == 1) SIR_LT_TRACE_AT(22, __builtin_amdgcn_s_memtime());
+        const float* img = lds + (s % NS) * G::BUF;
+        if ((s * WK + wk) * 32 < klen) {
+            float x0[16], x1[16];
+            LtOp<C0, G::L0, G::KS>::read(img, w0 * 32 + j, wk, h, x0);
+            LtOp<C1, G::L1, G::KS>::read(img + G::F0, w1 * 32 + j, wk, h, x1);
+#ifdef SIR_LT_TRACE
+            if (s == 1) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("" :: "v"(x0[0]), "v"(x1[0]), "v"(x0[15]), "v"(x1[15]));
+                SIR_LT_TRACE_AT(23, __builtin_amdgcn_s_memtime());
+            }
+#endif
+            if (do_cs) tile.step<true>(x0, x1, h);
+            else tile.step<false>(x0, x1, h);
+        }
+        SIR_LT_TRACE_AT(5 + 2 * (s & 7), __builtin_amdgcn_s_memtime());
+    }
+    SIR_LT_TRACE_AT(3, __builtin_amdgcn_s_memtime());
+    float pv[16];
+    tile.result(pv, h);
+    wait_vm<0>();                                               // the trailing DMAs too
+    __syncthreads();                                            // the images are free: partials go there
+    float* red = lds;
+    float* cred = lds + G::RED;                                 // [WK][32 W0][2] column-sum halves
+    const int tile_id = w0 + W0 * w1;
+    if (wk > 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(((wk - 1) * W0 * W1 + tile_id) * 16 + i) * 64 + l] = pv[i];
+    }
+    if (do_cs) cred[(wk * G::L0 + w0 * 32 + j) * 2 + h] = tile.cs;
+    __syncthreads();
+    if (wk == 0) {
+#pragma unroll
+        for (int q = 1; q < WK; ++q) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pv[i] += red[(((q - 1) * W0 * W1 + tile_id) * 16 + i) * 64 + l];
+        }
+        // acc element i of lane (j, h): op0 line 32 w0 + (i & 3) + 8 (i >> 2) + 4 h, op1 line 32 w1 + j
+        const int64_t r1 = a1 + 32 * w1 + j;
+        if constexpr (EPI == 0) {
+            if (r1 < n1lines) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int64_t n = a0 + 32 * w0 + 8 * g + 4 * h;
+                    if (n < n0lines) {
+                        float4 o = make_float4(pv[4 * g] + bb[g].x, pv[4 * g + 1] + bb[g].y, pv[4 * g + 2] + bb[g].z,
+                                               pv[4 * g + 3] + bb[g].w);
+                        if (drop.on()) drop4(drop, r1, (int)n, o);
+                        *reinterpret_cast<float4*>(C + r1 * ldc + n) = o;
+                    }
+                }
+            }
+        } else {
+            float* out = C + p * n0lines * n1lines;
+            if (r1 < n1lines) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t m = a0 + 32 * w0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (m < n0lines) out[m * n1lines + r1] = pv[i];
+                }
+            }
+        }
+    }
+    SIR_LT_TRACE_AT(20, __builtin_amdgcn_s_memtime());
+    SIR_LT_TRACE_AT(21, __builtin_amdgcn_s_memrealtime());
+    if (do_cs && t < G::L0 && a0 + t < n0lines) {
+        float sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < WK; ++q) sum += cred[(q * G::L0 + t) * 2] + cred[(q * G::L0 + t) * 2 + 1];
+        csum_part[p * n0lines + a0 + t] = sum;
+    }
+}
+
 }  // namespace
 
 #ifndef SIR_SMALL_ROWS
@@ -1609,6 +1868,39 @@ static int64_t gemm_small_rows() {
 #ifndef SIR_TN_S_ROWS
 #define SIR_TN_S_ROWS 512       // k_gemm_tn_s: node rows per split (<= 16 splits)
 #endif
+// LDS-tiled small GEMMs (k_gemm_lt) and their wave arrangement (W0 x W1 tiles of 32 x 32, WK
+// k-ways).  NT: 1 = 2x2x1, 2 = 1x2x2, 3 = 2x1x2 (default: 64 weight lines x 32 rows), 4 = 1x1x4,
+// 5 = 1x4x1; TN: 1 = 2x2x1, 2 = 1x2x2 (default), 3 = 1x1x4; 0 = the 4-wave k_gemm_nt_sw /
+// k_gemm_tn_s.  env SIR_LT_NT / SIR_LT_TN override per call (A/B runs, the arrangement tests);
+// measured in profiles/r05_small_gemm.txt.
+#ifndef SIR_LT_NT
+#define SIR_LT_NT 3
+#endif
+#ifndef SIR_LT_TN
+#define SIR_LT_TN 2
+#endif
+static int lt_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e != nullptr && e[0] != 0) ? atoi(e) : dflt;
+}
+#ifndef SIR_LT_BLOCKS
+#define SIR_LT_BLOCKS 512       // k_gemm_lt TN: row splits until about this many blocks
+#endif
+static bool aligned16(const void* p, int64_t ld) { return ((uintptr_t)p & 15u) == 0 && ld % 4 == 0; }
+// TN row splits of k_gemm_lt: each split a multiple of KS rows, at most 32 splits
+static int gemm_tn_splits_lt(int64_t R, int64_t tiles, int KS, int64_t* rps) {
+    int64_t P = (SIR_LT_BLOCKS + tiles - 1) / tiles;
+    const int64_t pmax = (R + KS - 1) / KS;
+    if (P > pmax) P = pmax;
+    if (P > 32) P = 32;
+    if (P < 1) P = 1;
+    int64_t r = (R + P - 1) / P;
+    r = (r + KS - 1) / KS * KS;
+    *rps = r > 0 ? r : KS;
+    P = (R + *rps - 1) / *rps;
+    return (int)(P < 1 ? 1 : P);
+}
+
 static int gemm_tn_splits_s(int64_t R, int64_t, int64_t) {
     int64_t P = (R + SIR_TN_S_ROWS - 1) / SIR_TN_S_ROWS;
     if (P > 16) P = 16;
@@ -1633,9 +1925,42 @@ static hipError_t run_gemm_nt_s(const float* A, int64_t lda, int64_t M, int K, c
     return hipGetLastError();
 }
 
+#ifndef SIR_LT_NS
+#define SIR_LT_NS 3             // k_gemm_lt stage buffers (NS - 1 steps in flight)
+#endif
+template <bool TRANS, int W0, int W1, int WK>
+static void launch_nt_lt(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int N,
+                         const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
+    using G = Lt<!TRANS, true, W0, W1, WK, SIR_LT_NS>;
+    const int nt0 = (N + G::L0 - 1) / G::L0;
+    const int64_t nt1 = (M + G::L1 - 1) / G::L1;
+    hipLaunchKernelGGL((k_gemm_lt<!TRANS, true, W0, W1, WK, SIR_LT_NS, 0>), dim3((unsigned)(nt0 * nt1)), dim3(256), 0, st,
+                       W, ldw, A, lda, (int64_t)N, M, (int64_t)K, nt0, (int)nt1, (int64_t)K, bias, C, ldc, nullptr, drop);
+}
+
 hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int trans,
                               int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
     if (M == 0 || N == 0) return hipSuccess;
+    const int lt = lt_env("SIR_LT_NT", SIR_LT_NT);
+    // k_gemm_lt: 16-byte loads of both operands, every byte offset of a tile's resource in 31 bits
+    if (lt > 0 && K % 4 == 0 && N % 4 == 0 && aligned16(A, lda) && aligned16(W, ldw) && ((uintptr_t)bias & 15u) == 0
+        && 128 * lda < ((int64_t)1 << 29) && (trans ? (int64_t)K * ldw : 128 * ldw) < ((int64_t)1 << 29)
+        && (M + 31) / 32 * ((N + 31) / 32) < ((int64_t)1 << 31)) {
+        switch (lt * 2 + (trans ? 1 : 0)) {
+        case 2: launch_nt_lt<false, 2, 2, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 3: launch_nt_lt<true, 2, 2, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 4: launch_nt_lt<false, 1, 2, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 5: launch_nt_lt<true, 1, 2, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 6: launch_nt_lt<false, 2, 1, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 7: launch_nt_lt<true, 2, 1, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 8: launch_nt_lt<false, 1, 1, 4>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 9: launch_nt_lt<true, 1, 1, 4>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 10: launch_nt_lt<false, 1, 4, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 11: launch_nt_lt<true, 1, 4, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     const int nft = (N + 31) / 32;
     const int64_t blocks = (M + 31) / 32 * nft;
     if (trans)
@@ -1770,6 +2095,7 @@ int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc) {
     if (R < gemm_small_rows()) {
         const int64_t ps = gemm_tn_splits_s(R, Mc, Nc);    // k_gemm_tn_s
         if (ps > P) P = ps;
+        if (P < 32) P = 32;                                // k_gemm_lt: at most 32 splits
     }
     return P * (Mc * Nc + Mc) * 4;                         // partial products + column sums
 }
@@ -1783,6 +2109,32 @@ hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb,
     const int nmt = (Mc + 255) / 256, nnt = (Nc + 255) / 256;
     float* part = static_cast<float*>(workspace);
     float* cpart = colsum != nullptr ? part + (int64_t)P * Mc * Nc : nullptr;
+    const int lt = lt_env("SIR_LT_TN", SIR_LT_TN);
+    if (small && lt > 0 && aligned16(A, lda) && aligned16(B, ldb) && (Mc + 31) / 32 * ((Nc + 31) / 32) < (1 << 24)) {
+        const int W0 = lt == 1 ? 2 : 1, W1 = lt == 1 ? 2 : (lt == 2 ? 2 : 1), WK = 4 / (W0 * W1);
+        const int64_t tiles = (int64_t)((Mc + 32 * W0 - 1) / (32 * W0)) * ((Nc + 32 * W1 - 1) / (32 * W1));
+        int64_t rl = 0;
+        const int Pl = gemm_tn_splits_lt(R, tiles, 32 * WK, &rl);
+        if (rl * std::max(lda, ldb) < ((int64_t)1 << 29)) {
+            float* cp = colsum != nullptr ? part + (int64_t)Pl * Mc * Nc : nullptr;
+            const int nt0 = (Mc + 32 * W0 - 1) / (32 * W0), nt1 = (Nc + 32 * W1 - 1) / (32 * W1);
+            const dim3 grid((unsigned)((int64_t)Pl * tiles));
+            if (lt == 1)
+                hipLaunchKernelGGL((k_gemm_lt<false, false, 2, 2, 1, SIR_LT_NS, 1>), grid, dim3(256), 0, st, A, lda, B, ldb,
+                                   (int64_t)Mc, (int64_t)Nc, R, nt0, nt1, rl, nullptr, part, (int64_t)0, cp, Drop{});
+            else if (lt == 2)
+                hipLaunchKernelGGL((k_gemm_lt<false, false, 1, 2, 2, SIR_LT_NS, 1>), grid, dim3(256), 0, st, A, lda, B, ldb,
+                                   (int64_t)Mc, (int64_t)Nc, R, nt0, nt1, rl, nullptr, part, (int64_t)0, cp, Drop{});
+            else
+                hipLaunchKernelGGL((k_gemm_lt<false, false, 1, 1, 4, SIR_LT_NS, 1>), grid, dim3(256), 0, st, A, lda, B, ldb,
+                                   (int64_t)Mc, (int64_t)Nc, R, nt0, nt1, rl, nullptr, part, (int64_t)0, cp, Drop{});
+            const int64_t count = (int64_t)Mc * Nc;
+            const int64_t nbm = (count + 255) / 256, nbc = colsum != nullptr ? (Mc + 255) / 256 : 0;
+            hipLaunchKernelGGL(k_gemm_reduce2, dim3((unsigned)(nbm + nbc)), dim3(256), 0, st, part, Pl, count, Nc, C, ldc,
+                               cp, Mc, colsum, nbm);
+            return hipGetLastError();
+        }
+    }
     if (small) {
         const int smt = (Mc + 31) / 32, snt = (Nc + 31) / 32;
         hipLaunchKernelGGL(k_gemm_tn_s, dim3((unsigned)((int64_t)P * smt * snt)), dim3(256), 0, st, A, lda, B, ldb, R,

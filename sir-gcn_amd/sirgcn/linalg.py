@@ -37,9 +37,10 @@ def _w_ok(W, n_out):
     return W.is_cuda and W.dtype == torch.float32 and n_out % 4 == 0 and n_out <= MAX_DIM
 
 
-# Below this many rows the weight is read as fp32 by the GEMM itself (sir_gemm_nt_direct, 4-wave
-# split-k tiles of 32 x 32) instead of being packed first: at config 5's 1.6k rows the packing pass
-# cost as much as the product (profiles/r03_ab_gemm_small.txt).
+# Below this many rows the weight is read as fp32 by the GEMM itself (sir_gemm_nt_direct: the
+# LDS-tiled k_gemm_lt, 64 x 32 tiles, both operands split in the kernel) instead of being packed
+# first: at config 5's 1.6k rows the packing pass cost as much as the product
+# (profiles/r03_ab_gemm_small.txt, profiles/r05_small_gemm.txt).
 DIRECT_ROWS = int(os.environ.get("SIRGCN_GEMM_DIRECT_ROWS", 8192))
 
 

@@ -383,7 +383,7 @@ def test_gemm_tn_small_and_block_routes_vs_fp64(R, M, N, route, monkeypatch):
 @pytest.mark.parametrize("trans,with_bias", [(False, True), (True, False), (False, False)])
 def test_gemm_nt_direct_vs_fp64(M, K, N, trans, with_bias):
     """sir_gemm_nt_direct (the small-batch route of nn.Linear: the fp32 weight split in the kernel,
-    running scales on both operands, 4 waves splitting K per 32 x 32 tile) vs fp64, on rows and
+    running scales on both operands; the LDS-tiled k_gemm_lt by default) vs fp64, on rows and
     weight rows spanning 2^60, rows whose maximum grows along K, a zero row; strided A (lda > K)."""
     g = torch.Generator(device=DEV).manual_seed(M + 7 * K + N)
     A0 = torch.randn(M, K + 8, device=DEV, generator=g)
@@ -400,6 +400,57 @@ def test_gemm_nt_direct_vs_fp64(M, K, N, trans, with_bias):
     ref = torch.addmm(b, A, Wt) if with_bias else A @ Wt
     _check(C, A.double(), Wt.double(), ref, b, f"nt direct M={M} K={K} N={N} trans={trans}")
     assert torch.equal(C, _native.gemm_nt_direct(A, W, trans, b)), "deterministic"
+
+
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("M,K,N", [(1582, 300, 600), (1582, 600, 300), (33, 36, 12), (97, 68, 132), (1, 32, 4)])
+@pytest.mark.parametrize("trans", [False, True])
+def test_gemm_nt_direct_lt_arrangements(cfg, M, K, N, trans, monkeypatch):
+    """Every wave arrangement of the LDS-tiled small kernel (SIR_LT_NT: 1 = 2x2 tiles, 2 = 1x2 tiles x
+    2 k-ways, 3 = 2x1 x 2, 4 = 1 tile x 4 k-ways, 5 = 1x4; 0 = the 4-wave k_gemm_nt_sw) vs fp64 with
+    bias and dropout, ragged tiles, a row whose scale grows along K; a weight view not 16-byte aligned
+    takes k_gemm_nt_sw whatever the setting."""
+    monkeypatch.setenv("SIR_LT_NT", cfg)
+    g = torch.Generator(device=DEV).manual_seed(M + K + N + int(cfg))
+    A = torch.randn(M, K, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-20, 20, (M, 1), device=DEV, generator=g).float())
+    A[M // 2] *= torch.exp2(torch.linspace(-20, 20, K, device=DEV))
+    W = (torch.randn(K, N, device=DEV, generator=g) if trans else torch.randn(N, K, device=DEV, generator=g)) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g)
+    Wt = W if trans else W.t()
+    C = _native.gemm_nt_direct(A, W, trans, b)
+    _check(C, A.double(), Wt.double(), torch.addmm(b, A, Wt), b, f"nt lt{cfg} M={M} K={K} N={N} trans={trans}")
+    if not trans:
+        Cd = _native.gemm_nt_direct(A, W, False, b, drop=(5, 0.25))
+        keep = Cd != 0
+        assert torch.equal(Cd[keep], C[keep] * (1.0 / 0.75))
+    # 4-byte-aligned weight view (k_gemm_nt_sw)
+    Wb = torch.empty(W.numel() + 1, device=DEV)[1:].view_as(W).copy_(W)
+    C2 = _native.gemm_nt_direct(A, Wb, trans, b)
+    _check(C2, A.double(), Wt.double(), torch.addmm(b, A, Wt), b, f"nt unaligned lt{cfg}")
+
+
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("R,M,N", [(1582, 600, 300), (1582, 300, 300), (37, 64, 128), (70, 36, 100), (3000, 4, 8)])
+def test_gemm_tn_small_lt_arrangements(cfg, R, M, N, monkeypatch):
+    """The small TN route per LDS arrangement (SIR_LT_TN: 1 = 2x2 tiles, 2 = 1x2 x 2 k-ways, 3 = 1 x 4
+    k-ways; 0 = k_gemm_tn_s): product and column sums vs fp64, deterministic, ragged rows and tiles."""
+    monkeypatch.setenv("SIR_LT_TN", cfg)
+    monkeypatch.setenv("SIR_GEMM_SMALL_ROWS", ROUTES["small"])
+    g = torch.Generator(device=DEV).manual_seed(R + M + N + int(cfg))
+    A = torch.randn(R, M, device=DEV, generator=g)
+    A *= torch.exp2(torch.randint(-30, 30, (1, M), device=DEV, generator=g).float())
+    B = torch.randn(R, N, device=DEV, generator=g)
+    B[R // 2:R // 2 + 20] *= 2.0 ** 20
+    C, cs = _native.gemm_tn(A, B, colsum=True)
+    assert torch.equal(C, _native.gemm_tn(A, B)), "deterministic / independent of colsum"
+    _check(C, A.double().t(), B.double(), A.t() @ B, None, f"tn lt{cfg} R={R} M={M} N={N}")
+    # column sums per column against sum |a| (a relative L2 over a few columns is decided by the one
+    # whose sum cancels most): the fp32 chain of 16 plain adds + compensated adds stays <= 2e-7
+    ref64, absum = A.double().sum(0), A.double().abs().sum(0)
+    e_ours = ((cs.double() - ref64).abs() / absum).max().item()
+    e_torch = ((A.sum(0).double() - ref64).abs() / absum).max().item()
+    assert e_ours <= max(2 * e_torch, 2e-7), (e_ours, e_torch)
 
 
 def test_gemm_nt_direct_dropout_epilogue_and_errors():
