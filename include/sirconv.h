@@ -16,7 +16,8 @@
  *    bias gradients sir_col_sum, the Q/K feature dropout sir_dropout_t (conv.py:35,60-61);
  *  - agg='max' and the per-edge Linear sigma (conv.py:46-47): sir_edge_mlp_* / sir_edge_max_*;
  *    the edge-materialised helpers (sir_edge_gather_add / _act, sir_segment_*);
- *  - GraphNorm (models/norm.py:7-29): sir_graph_norm_fwd / _bwd;
+ *  - GraphNorm (models/norm.py:7-29): sir_graph_norm_fwd / _bwd, with the stack's activation and
+ *    residual fused: sir_graph_norm_act_fwd / _bwd;
  *  - the graph input (DGL's CSC build for batched graphs): sir_csr_build / sir_csr_perm.
  *
  * Conventions
@@ -45,7 +46,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 12
+#define SIR_ABI_VERSION 13
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57).  SIR_AGG_ACCUMULATE,
  * OR'd into the forward's `agg` (SUM / SYM): S[v] = S[v] + the sum over the given items' edges, rows
@@ -356,6 +357,23 @@ int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X,
                        const float* mean, const float* std_, float* dX, int64_t lddx,
                        float* dw_part, float* dms_part, float* db_part, void* stream);
 
+/* GraphNorm with the stack's activation and residual after it, one kernel per direction — the
+ * layer loop of ogbn-arxiv/model.py:65-73 / ogbg-molhiv/model.py:76-84 (h = act(norm(h)) + resid)
+ * and, with R = NULL, zinc/model.py:54-55 (h = act(norm(h))).  Forward: Y = act(y) + R with y the
+ * sir_graph_norm_fwd output and act = SIR_ACT_IDENTITY / _RELU / _LEAKY_RELU (slope): torch's
+ * relu / leaky_relu and add, the same ops (bit-identical to the three separate calls).  Backward:
+ * dY is the gradient of Y; the kernel takes act'(y) dY (y recomputed by the forward's own ops, so
+ * on the same side of 0; leaky_relu_backward's y > 0 ? g : g * slope) into the GraphNorm backward;
+ * R's gradient is dY itself (the caller's).  bias as in the forward (NULL: none).  ABI 13. */
+int sir_graph_norm_act_fwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                           const float* weight, const float* bias, const float* mean_scale, float eps, int act,
+                           float slope, const float* R, int64_t ldr, float* Y, int64_t ldy, float* mean, float* std_,
+                           void* stream);
+int sir_graph_norm_act_bwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                           const float* dY, int64_t ldg, const float* weight, const float* bias,
+                           const float* mean_scale, const float* mean, const float* std_, int act, float slope,
+                           float* dX, int64_t lddx, float* dw_part, float* dms_part, float* db_part, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Device-side graph plan build.  Replaces DGL's lazily built in-edge CSC
  * (the COO -> CSR counting sort DGL runs on the first update_all, conv.py:63) and this repo's
@@ -426,6 +444,16 @@ int sir_gemm_nt_dact(const float* A, int64_t lda, int64_t M, int64_t K, const vo
  * 4; A, C, bias 16-B aligned; ldw <= SIR_GEMM_MAX_LD.  Replaces addmm(b, X, W^T) / mm(X, W). */
 int sir_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int64_t K, const float* W, int64_t ldw, int trans,
                        int64_t N, const float* bias, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream);
+
+/* sir_gemm_nt_direct with the weight in two parts and a partial bias: weight rows r < split come
+ * from W, rows r >= split from W2 (row r - split; the rows are output features for trans = 0 and k
+ * for trans = 1), and the bias covers the first bias_cols output columns (+ 0 on the rest) — the
+ * layer's QK = X [W_Q; W_K]^T + [b_Q; 0] and dX = [dQ dK] [W_Q; W_K] (conv.py:60-61) without the
+ * per-step torch.cat of the weights and the pad of the bias.  W, W2, bias 16-B aligned, ldw, ldw2
+ * multiples of 4; 0 < split <= weight rows (split = rows: W alone); bias_cols % 4 == 0.  ABI 13. */
+int sir_gemm_nt_direct2(const float* A, int64_t lda, int64_t M, int64_t K, const float* W, int64_t ldw,
+                        const float* W2, int64_t ldw2, int64_t split, int trans, int64_t N, const float* bias,
+                        int64_t bias_cols, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream);
 
 /* C[M, N] = A^T B with A [R, M] (lda), B [R, N] (ldb): the weight gradients (contraction over the
  * R node rows, split over row ranges; the partial products are added in a fixed order, so the

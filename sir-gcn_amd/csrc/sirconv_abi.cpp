@@ -560,8 +560,25 @@ int sir_graph_norm_fwd(const int64_t* off, int64_t B, int64_t F, const float* X,
     if (B > 0 && (off == nullptr || X == nullptr || weight == nullptr || Y == nullptr || mean == nullptr ||
                   std_ == nullptr))
         return fail(SIR_EINVAL, fn, "NULL buffer");
-    return finish(fn, sir::run_graph_norm_fwd(off, B, (int)F, X, ldx, weight, bias, mean_scale, eps, Y, ldy,
-                                              mean, std_, static_cast<hipStream_t>(stream)), nullptr);
+    return finish(fn, sir::run_graph_norm_fwd(off, B, (int)F, X, ldx, weight, bias, mean_scale, eps, SIR_ACT_IDENTITY,
+                                              0.f, nullptr, 0, Y, ldy, mean, std_, static_cast<hipStream_t>(stream)),
+                  nullptr);
+}
+
+int sir_graph_norm_act_fwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                           const float* weight, const float* bias, const float* mean_scale, float eps, int act,
+                           float slope, const float* R, int64_t ldr, float* Y, int64_t ldy, float* mean, float* std_,
+                           void* stream) {
+    const char* fn = "sir_graph_norm_act_fwd";
+    if (B < 0 || F <= 0 || F > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if (ldx < F || ldy < F || (R != nullptr && ldr < F)) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if (act != SIR_ACT_IDENTITY && act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU)
+        return fail(SIR_EINVAL, fn, "act must be identity, relu or leaky_relu");
+    if (B > 0 && (off == nullptr || X == nullptr || weight == nullptr || Y == nullptr || mean == nullptr ||
+                  std_ == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    return finish(fn, sir::run_graph_norm_fwd(off, B, (int)F, X, ldx, weight, bias, mean_scale, eps, act, slope, R, ldr,
+                                              Y, ldy, mean, std_, static_cast<hipStream_t>(stream)), nullptr);
 }
 
 int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
@@ -575,8 +592,26 @@ int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X,
                   std_ == nullptr || dX == nullptr || dw_part == nullptr || db_part == nullptr))
         return fail(SIR_EINVAL, fn, "NULL buffer");
     if (mean_scale != nullptr && dms_part == nullptr && B > 0) return fail(SIR_EINVAL, fn, "dms_part needed");
-    return finish(fn, sir::run_graph_norm_bwd(off, B, (int)F, X, ldx, dY, ldg, weight, mean_scale, mean, std_,
-                                              dX, lddx, dw_part, dms_part, db_part,
+    return finish(fn, sir::run_graph_norm_bwd(off, B, (int)F, X, ldx, dY, ldg, weight, nullptr, mean_scale, mean, std_,
+                                              SIR_ACT_IDENTITY, 0.f, dX, lddx, dw_part, dms_part, db_part,
+                                              static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_graph_norm_act_bwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
+                           const float* dY, int64_t ldg, const float* weight, const float* bias,
+                           const float* mean_scale, const float* mean, const float* std_, int act, float slope,
+                           float* dX, int64_t lddx, float* dw_part, float* dms_part, float* db_part, void* stream) {
+    const char* fn = "sir_graph_norm_act_bwd";
+    if (B < 0 || F <= 0 || F > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if (ldx < F || ldg < F || lddx < F) return fail(SIR_EINVAL, fn, "leading dimensions must be >= F");
+    if (act != SIR_ACT_IDENTITY && act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU)
+        return fail(SIR_EINVAL, fn, "act must be identity, relu or leaky_relu");
+    if (B > 0 && (off == nullptr || X == nullptr || dY == nullptr || weight == nullptr || mean == nullptr ||
+                  std_ == nullptr || dX == nullptr || dw_part == nullptr || db_part == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (mean_scale != nullptr && dms_part == nullptr && B > 0) return fail(SIR_EINVAL, fn, "dms_part needed");
+    return finish(fn, sir::run_graph_norm_bwd(off, B, (int)F, X, ldx, dY, ldg, weight, bias, mean_scale, mean, std_,
+                                              act, slope, dX, lddx, dw_part, dms_part, db_part,
                                               static_cast<hipStream_t>(stream)), nullptr);
 }
 
@@ -684,6 +719,32 @@ int sir_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int64_t K, const 
     if ((reinterpret_cast<uintptr_t>(W) & 3u) != 0) return fail(SIR_EINVAL, fn, "W must be 4-B aligned");
     hipError_t err = sir::run_gemm_nt_direct(A, lda, M, (int)K, W, ldw, trans, (int)N, bias, C, ldc,
                                              static_cast<hipStream_t>(stream), to_drop(drop, 0));
+    return finish(fn, err, nullptr);
+}
+
+int sir_gemm_nt_direct2(const float* A, int64_t lda, int64_t M, int64_t K, const float* W, int64_t ldw,
+                        const float* W2, int64_t ldw2, int64_t split, int trans, int64_t N, const float* bias,
+                        int64_t bias_cols, float* C, int64_t ldc, const sir_dropout_t* drop, void* stream) {
+    const char* fn = "sir_gemm_nt_direct2";
+    if (M < 0 || N <= 0 || K <= 0 || N > 65536 || K > 65536) return fail(SIR_EINVAL, fn, "bad shape");
+    if ((M + 31) / 32 * ((N + 31) / 32) > (int64_t)INT_MAX) return fail(SIR_EINVAL, fn, "M too large");
+    if (K % 4 != 0 || N % 4 != 0 || lda % 4 != 0 || ldc % 4 != 0 || lda < K || ldc < N)
+        return fail(SIR_EINVAL, fn, "K, N, lda, ldc must be multiples of 4 (lda >= K, ldc >= N)");
+    if (trans != 0 && trans != 1) return fail(SIR_EINVAL, fn, "trans must be 0 or 1");
+    const int64_t rows = trans ? K : N;           // weight rows: k (trans) or output features
+    if (split <= 0 || split > rows) return fail(SIR_EINVAL, fn, "split must be in (0, weight rows]");
+    if (bias_cols < 0 || bias_cols % 4 != 0) return fail(SIR_EINVAL, fn, "bias_cols must be a multiple of 4");
+    if (ldw < (trans ? N : K) || ldw2 < (trans ? N : K)) return fail(SIR_EINVAL, fn, "ldw / ldw2 too small");
+    if (lda > SIR_GEMM_MAX_LD || ldw > SIR_GEMM_MAX_LD || ldw2 > SIR_GEMM_MAX_LD)
+        return fail(SIR_EINVAL, fn, "lda/ldw too large");
+    if (M > 0 && (A == nullptr || C == nullptr || W == nullptr || (split < rows && W2 == nullptr)))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(C) | reinterpret_cast<uintptr_t>(bias) |
+          reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(W2)) & 15u) != 0 || ldw % 4 != 0 || ldw2 % 4 != 0)
+        return fail(SIR_EINVAL, fn, "A, C, bias, W, W2 must be 16-B aligned, ldw / ldw2 multiples of 4");
+    hipError_t err = sir::run_gemm_nt_direct(A, lda, M, (int)K, W, ldw, trans, (int)N, bias, C, ldc,
+                                             static_cast<hipStream_t>(stream), to_drop(drop, 0),
+                                             split < rows ? W2 : nullptr, ldw2, split, bias_cols);
     return finish(fn, err, nullptr);
 }
 

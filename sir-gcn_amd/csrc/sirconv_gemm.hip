@@ -1654,30 +1654,52 @@ __device__ __attribute__((aligned(16))) float g_lt_zero[4];    // source of the 
 // for CONTIG operands, checked by the launchers).  Thread t fills the 16-byte slots u = t + 256 i
 // (i < N) of every step's image (wave-instruction i of wave w: slots 256 i + 64 w + lane); the
 // slot's source at step 0 and its k offset are set up once, a step adds s * KS (CONTIG) or
-// s * KS * ld (strided) elements.
-template <bool CONTIG, int L, int KS>
+// s * KS * ld (strided) elements.  TWO: the operand's weight-row index (the line for CONTIG, k for
+// strided) continues from `split` on in a second array x2 (row r >= split at x2 + (r - split) ld2):
+// the layer's [W_Q; W_K] read as it lies, no concatenated copy.  `row0`: the weight row of the
+// tile's line / k 0; x2 is offset to the tile along the other index (k for CONTIG, line otherwise).
+template <bool CONTIG, int L, int KS, bool TWO = false>
 struct LtOp {
     static constexpr int NC = KS / 4;                                 // 16-byte slots per image line
     static constexpr int N = L * KS / 1024;
+    static constexpr bool SPLIT_K = TWO && !CONTIG;                  // the part is chosen per step
     const float* src[N];
+    const float* src2[SPLIT_K ? N : 1];
     int kof[N];                                                       // slot k at step 0 (INT_MAX: dead line)
-    int64_t step;                                                     // elements per step
-    int klen;
+    int64_t step, step2;                                              // elements per step
+    int klen, ksplit;
     __device__ __forceinline__ static int swz(int line) { return KS == 32 ? (line >> 1) & 7 : line & (NC - 1); }
-    __device__ __forceinline__ LtOp(const float* x, int64_t ld, int lines, int klen_, int t) : klen(klen_) {
+    __device__ __forceinline__ LtOp(const float* x, int64_t ld, int lines, int klen_, int t, const float* x2 = nullptr,
+                                    int64_t ld2 = 0, int64_t split = 0, int64_t row0 = 0)
+        : klen(klen_), ksplit(0x7fffffff) {
         step = CONTIG ? (int64_t)KS : (int64_t)KS * ld;
+        step2 = (int64_t)KS * ld2;
+        if constexpr (SPLIT_K) {
+            const int64_t ks = split - row0;
+            ksplit = ks < 0 ? 0 : (ks > 0x7fffffff ? 0x7fffffff : (int)ks);
+        }
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             const int u = t + 256 * i;
             int line, k;
             if constexpr (CONTIG) { line = u / NC; k = 4 * ((u % NC) ^ swz(u / NC)); }
             else { k = u / (L / 4); line = 4 * (u % (L / 4)); }
-            src[i] = CONTIG ? x + (int64_t)line * ld + k : x + (int64_t)k * ld + line;
+            if constexpr (CONTIG) {
+                src[i] = (TWO && row0 + line >= split) ? x2 + (row0 + line - split) * ld2 + k : x + (int64_t)line * ld + k;
+            } else {
+                src[i] = x + (int64_t)k * ld + line;
+                if constexpr (SPLIT_K) src2[i] = x2 + (row0 + k - split) * ld2 + line;
+            }
             kof[i] = line < lines ? k : 0x7fffffff - KS * 4096;
         }
     }
     __device__ __forceinline__ const float* at(int i, int s) const {
-        return s * KS + kof[i] < klen ? src[i] + s * step : g_lt_zero;
+        const int k = s * KS + kof[i];
+        if (k >= klen) return g_lt_zero;
+        if constexpr (SPLIT_K) {
+            if (k >= ksplit) return src2[i] + s * step2;
+        }
+        return src[i] + s * step;
     }
     // the lane's 16 values of its line j, chunk kc of the step (k = 32 kc + 16 (i >> 3) + 8 h + (i & 7))
     __device__ __forceinline__ static void read(const float* img, int j, int kc, int h, float (&x)[16]) {
@@ -1723,7 +1745,9 @@ template <bool C0, bool C1, int W0, int W1, int WK, int NS, int EPI>
 __global__ void __launch_bounds__(256)
 k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X1, int64_t ld1, int64_t n0lines,
           int64_t n1lines, int64_t klen_all, int nt0, int nt1, int64_t rps, const float* __restrict__ bias,
-          float* __restrict__ C, int64_t ldc, float* __restrict__ csum_part, Drop drop) {
+          float* __restrict__ C, int64_t ldc, float* __restrict__ csum_part, Drop drop,
+          const float* __restrict__ X0b = nullptr, int64_t ld0b = 0, int64_t split0 = INT64_MAX,
+          int64_t bias_cols = INT64_MAX) {
     using G = Lt<C0, C1, W0, W1, WK, NS>;
     __shared__ __attribute__((aligned(16))) float lds[G::LDS];
     const int t = threadIdx.x, l = t & 63, j = l & 31, h = l >> 5, w = t >> 6;
@@ -1740,7 +1764,10 @@ k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X
     const int lines1 = (int)(n1lines - a1 < G::L1 ? n1lines - a1 : G::L1);
     const int64_t v0 = p * rps;
     const int klen = (int)(klen_all - v0 < rps ? klen_all - v0 : rps);
-    const LtOp<C0, G::L0, G::KS> o0(C0 ? X0 + a0 * ld0 + v0 : X0 + v0 * ld0 + a0, ld0, lines0, klen, t);
+    // NT (EPI 0): op0 is the weight, possibly in two parts (X0 rows < split0, X0b the rest)
+    const LtOp<C0, G::L0, G::KS, EPI == 0> o0(C0 ? X0 + a0 * ld0 + v0 : X0 + v0 * ld0 + a0, ld0, lines0, klen, t,
+                                              X0b == nullptr ? nullptr : (C0 ? X0b + v0 : X0b + a0), ld0b, split0,
+                                              C0 ? a0 : v0);
     const LtOp<C1, G::L1, G::KS> o1(C1 ? X1 + a1 * ld1 + v0 : X1 + v0 * ld1 + a1, ld1, lines1, klen, t);
     const int nsteps = klen > 0 ? (klen + G::KS - 1) / G::KS : 0;
     constexpr bool CS = EPI == 1;
@@ -1762,8 +1789,9 @@ k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int64_t n = a0 + 32 * w0 + 8 * g + 4 * h;
-            bb[g] = (bias != nullptr && n < n0lines) ? *reinterpret_cast<const float4*>(bias + n)
-                                                     : make_float4(-0.f, -0.f, -0.f, -0.f);
+            // past bias_cols: + 0 (the zeros of a padded bias); no bias: - 0 (x + -0 = x)
+            bb[g] = (bias != nullptr && n < n0lines && n < bias_cols) ? *reinterpret_cast<const float4*>(bias + n)
+                    : (bias != nullptr ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(-0.f, -0.f, -0.f, -0.f));
         }
     }
     SplitTile tile;
@@ -1783,7 +1811,7 @@ k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X
         const float* img = lds + (s % NS) * G::BUF;
         if ((s * WK + wk) * 32 < klen) {
             float x0[16], x1[16];
-            LtOp<C0, G::L0, G::KS>::read(img, w0 * 32 + j, wk, h, x0);
+            LtOp<C0, G::L0, G::KS, EPI == 0>::read(img, w0 * 32 + j, wk, h, x0);
             LtOp<C1, G::L1, G::KS>::read(img + G::F0, w1 * 32 + j, wk, h, x1);
 #ifdef SIR_LT_TRACE
             if (s == 1) {
@@ -1928,39 +1956,51 @@ static hipError_t run_gemm_nt_s(const float* A, int64_t lda, int64_t M, int K, c
 #ifndef SIR_LT_NS
 #define SIR_LT_NS 3             // k_gemm_lt stage buffers (NS - 1 steps in flight)
 #endif
+struct NtW {            // the weight of an NT product: rows < split from W, the rest from W2
+    const float* W;
+    int64_t ldw;
+    const float* W2;
+    int64_t ldw2, split, bias_cols;
+};
 template <bool TRANS, int W0, int W1, int WK>
-static void launch_nt_lt(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int N,
-                         const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
+static void launch_nt_lt(const float* A, int64_t lda, int64_t M, int K, const NtW& w, int N, const float* bias,
+                         float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
     using G = Lt<!TRANS, true, W0, W1, WK, SIR_LT_NS>;
     const int nt0 = (N + G::L0 - 1) / G::L0;
     const int64_t nt1 = (M + G::L1 - 1) / G::L1;
     hipLaunchKernelGGL((k_gemm_lt<!TRANS, true, W0, W1, WK, SIR_LT_NS, 0>), dim3((unsigned)(nt0 * nt1)), dim3(256), 0, st,
-                       W, ldw, A, lda, (int64_t)N, M, (int64_t)K, nt0, (int)nt1, (int64_t)K, bias, C, ldc, nullptr, drop);
+                       w.W, w.ldw, A, lda, (int64_t)N, M, (int64_t)K, nt0, (int)nt1, (int64_t)K, bias, C, ldc, nullptr,
+                       drop, w.W2, w.ldw2, w.split, w.bias_cols);
 }
 
 hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int trans,
-                              int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop) {
+                              int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop,
+                              const float* W2, int64_t ldw2, int64_t split, int64_t bias_cols) {
     if (M == 0 || N == 0) return hipSuccess;
     const int lt = lt_env("SIR_LT_NT", SIR_LT_NT);
-    // k_gemm_lt: 16-byte loads of both operands, every byte offset of a tile's resource in 31 bits
+    const NtW w{W, ldw, W2, ldw2, W2 != nullptr ? split : INT64_MAX, bias_cols};
+    // k_gemm_lt: 16-byte loads of both operands (and of W2), every byte offset of a tile's resource in 31 bits
     if (lt > 0 && K % 4 == 0 && N % 4 == 0 && aligned16(A, lda) && aligned16(W, ldw) && ((uintptr_t)bias & 15u) == 0
-        && 128 * lda < ((int64_t)1 << 29) && (trans ? (int64_t)K * ldw : 128 * ldw) < ((int64_t)1 << 29)
+        && (W2 == nullptr || aligned16(W2, ldw2)) && 128 * lda < ((int64_t)1 << 29)
+        && (trans ? (int64_t)K * ldw : 128 * ldw) < ((int64_t)1 << 29)
         && (M + 31) / 32 * ((N + 31) / 32) < ((int64_t)1 << 31)) {
         switch (lt * 2 + (trans ? 1 : 0)) {
-        case 2: launch_nt_lt<false, 2, 2, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 3: launch_nt_lt<true, 2, 2, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 4: launch_nt_lt<false, 1, 2, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 5: launch_nt_lt<true, 1, 2, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 6: launch_nt_lt<false, 2, 1, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 7: launch_nt_lt<true, 2, 1, 2>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 8: launch_nt_lt<false, 1, 1, 4>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 9: launch_nt_lt<true, 1, 1, 4>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 10: launch_nt_lt<false, 1, 4, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
-        case 11: launch_nt_lt<true, 1, 4, 1>(A, lda, M, K, W, ldw, N, bias, C, ldc, st, drop); break;
+        case 2: launch_nt_lt<false, 2, 2, 1>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 3: launch_nt_lt<true, 2, 2, 1>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 4: launch_nt_lt<false, 1, 2, 2>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 5: launch_nt_lt<true, 1, 2, 2>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 6: launch_nt_lt<false, 2, 1, 2>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 7: launch_nt_lt<true, 2, 1, 2>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 8: launch_nt_lt<false, 1, 1, 4>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 9: launch_nt_lt<true, 1, 1, 4>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 10: launch_nt_lt<false, 1, 4, 1>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 11: launch_nt_lt<true, 1, 4, 1>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
     }
+    // the two-part weight and the partial bias are the LDS-tiled kernel's only
+    if (W2 != nullptr || bias_cols < N) return hipErrorInvalidValue;
     const int nft = (N + 31) / 32;
     const int64_t blocks = (M + 31) / 32 * nft;
     if (trans)

@@ -87,11 +87,12 @@ hipError_t run_seg_max(const GenericArgs& a, hipStream_t st);
 hipError_t run_seg_max_bwd(const GenericArgs& a, hipStream_t st);
 
 hipError_t run_graph_norm_fwd(const int64_t* off, int64_t B, int F, const float* X, int64_t ldx,
-                              const float* w, const float* bias, const float* ms, float eps,
-                              float* Y, int64_t ldy, float* mean, float* sd, hipStream_t st);
+                              const float* w, const float* bias, const float* ms, float eps, int act, float slope,
+                              const float* R, int64_t ldr, float* Y, int64_t ldy, float* mean, float* sd,
+                              hipStream_t st);
 hipError_t run_graph_norm_bwd(const int64_t* off, int64_t B, int F, const float* X, int64_t ldx,
-                              const float* dY, int64_t ldg, const float* w, const float* ms,
-                              const float* mean, const float* sd, float* dX, int64_t lddx,
+                              const float* dY, int64_t ldg, const float* w, const float* bias, const float* ms,
+                              const float* mean, const float* sd, int act, float slope, float* dX, int64_t lddx,
                               float* dw_part, float* dms_part, float* db_part, hipStream_t st);
 
 hipError_t run_degree_norms(const int* rowptr_a, float* norm_a, const int* rowptr_b, float* norm_b,
@@ -158,7 +159,9 @@ hipError_t run_gemm_nt(const float* A, int64_t lda, int64_t M, int K, const void
                        const float* gate = nullptr, int gate_relu = 0, float gate_slope = 0.f,
                        const uint64_t* gate_mask = nullptr);
 hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int trans,
-                              int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop);
+                              int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop,
+                              const float* W2 = nullptr, int64_t ldw2 = 0, int64_t split = 0,
+                              int64_t bias_cols = INT64_MAX);
 int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc);
 hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
                        float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st);

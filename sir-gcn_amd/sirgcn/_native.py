@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("SIRGCN_LIB") or os.path.join(os.path.dirname(os.path.
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 12
+ABI_VERSION = 13
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -32,6 +32,10 @@ SIGNATURES = {
     "sir_graph_norm_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _F, _P, _I64, _P, _P, _P]),
     "sir_graph_norm_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I64,
                                           _P, _P, _P, _P]),
+    "sir_graph_norm_act_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _F, _I, _F, _P, _I64, _P, _I64,
+                                              _P, _P, _P]),
+    "sir_graph_norm_act_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I, _F, _P,
+                                              _I64, _P, _P, _P, _P]),
     "sir_edge_gather_add": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P]),
     "sir_edge_gather_act": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _I64, _P, _P]),
     "sir_segment_sum": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _I, _P, _I64,
@@ -47,6 +51,8 @@ SIGNATURES = {
     "sir_gemm_nt": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P, _P]),
     "sir_gemm_nt_dact": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _P, _I, _F, _P, _I64, _P]),
     "sir_gemm_nt_direct": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, ctypes.c_int, _I64, _P, _P, _I64, _P, _P]),
+    "sir_gemm_nt_direct2": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I64, ctypes.c_int, _I64, _P,
+                                           _I64, _P, _I64, _P, _P]),
     "sir_gemm_tn_workspace": (ctypes.c_int64, [_I64, _I64, _I64]),
     "sir_gemm_tn": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P, _I64, _P]),
     "sir_gemm_tn16": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _I64, _I, _P, _I64, _P, _P, _I64, _P]),
@@ -428,6 +434,30 @@ def graph_norm_fwd(off, X, weight, bias, mean_scale, eps, Y, mean, std):
     _check(rc, lib)
 
 
+def graph_norm_act_fwd(off, X, weight, bias, mean_scale, eps, act, slope, R, Y, mean, std):
+    """GraphNorm -> act -> + R in one kernel (``sir_graph_norm_act_fwd``; R may be None)."""
+    lib = load()
+    B, F = mean.shape
+    with _Timed("sir_graph_norm_fwd", Y.device):
+        rc = lib.sir_graph_norm_act_fwd(_ptr(off), B, F, _ptr(X), _ld(X, F), _ptr(weight), _ptr(bias),
+                                        _ptr(mean_scale), float(eps), int(act), float(slope), _ptr(R),
+                                        _ld(R, F) if R is not None else 0, _ptr(Y), _ld(Y, F), _ptr(mean), _ptr(std),
+                                        _stream(Y.device))
+    _check(rc, lib)
+
+
+def graph_norm_act_bwd(off, X, dY, weight, bias, mean_scale, mean, std, act, slope, dX, dw_part, dms_part, db_part):
+    """Backward of :func:`graph_norm_act_fwd` (dY: the gradient of its output)."""
+    lib = load()
+    B, F = mean.shape
+    with _Timed("sir_graph_norm_bwd", dX.device):
+        rc = lib.sir_graph_norm_act_bwd(_ptr(off), B, F, _ptr(X), _ld(X, F), _ptr(dY), _ld(dY, F), _ptr(weight),
+                                        _ptr(bias), _ptr(mean_scale), _ptr(mean), _ptr(std), int(act), float(slope),
+                                        _ptr(dX), _ld(dX, F), _ptr(dw_part), _ptr(dms_part), _ptr(db_part),
+                                        _stream(dX.device))
+    _check(rc, lib)
+
+
 def graph_norm_bwd(off, X, dY, weight, mean_scale, mean, std, dX, dw_part, dms_part, db_part):
     lib = load()
     B, F = mean.shape
@@ -504,6 +534,30 @@ def gemm_nt_direct(A, W, trans=False, bias=None, out=None, drop=None):
     with _Timed(f"sir_gemm_nt_direct K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + N))):
         rc = lib.sir_gemm_nt_direct(_ptr(A), A.stride(0), M, K, _ptr(W), W.stride(0), int(trans), N, _ptr(bias),
                                     _ptr(out), out.stride(0), _drop(drop), _stream(A.device))
+    _check(rc, lib)
+    return out
+
+
+def gemm_nt_direct2(A, W, W2, trans=False, bias=None, bias_cols=None, out=None, drop=None):
+    """:func:`gemm_nt_direct` on the weight [W; W2] stacked along its row index (trans=False: W
+    [N1, K], W2 [N2, K] -> N = N1 + N2 outputs; trans=True: W [K1, N], W2 [K2, N] -> K = K1 + K2),
+    read in place (``sir_gemm_nt_direct2``), the bias on the first ``bias_cols`` outputs."""
+    lib = load()
+    M, K = A.shape
+    if trans:
+        N = W.shape[1]
+        assert W2.shape[1] == N and W.shape[0] + W2.shape[0] == K
+    else:
+        N = W.shape[0] + W2.shape[0]
+        assert W.shape[1] == K and W2.shape[1] == K
+    assert A.stride(1) == 1 and W.stride(1) == 1 and W2.stride(1) == 1
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    bc = (bias.numel() if bias is not None else 0) if bias_cols is None else bias_cols
+    with _Timed(f"sir_gemm_nt_direct K={K} N={N}", A.device, (2 * M * N * K, 4 * M * (K + N))):
+        rc = lib.sir_gemm_nt_direct2(_ptr(A), A.stride(0), M, K, _ptr(W), W.stride(0), _ptr(W2), W2.stride(0),
+                                     W.shape[0], int(trans), N, _ptr(bias), bc, _ptr(out), out.stride(0), _drop(drop),
+                                     _stream(A.device))
     _check(rc, lib)
     return out
 

@@ -200,9 +200,9 @@ class SIRConvFunction(torch.autograd.Function):
     def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, plan, agg, act, slope, grad_on=True, drop=None):
         H = W_Q.shape[0]
         X = X.contiguous()
-        W_cat = torch.cat([W_Q, W_K], 0)
-        # [b_Q; 0] by one pad kernel (a zeros fill + a cat were two launches: small batches are launch-bound)
-        QK = linalg.mm_wt(X, W_cat, F.pad(b_Q, (0, H)) if b_Q is not None else None, drop=drop)
+        # X [W_Q; W_K]^T + [b_Q; 0]: the small-batch kernel reads W_Q / W_K in place and biases the
+        # Q half only (no cat / pad launches per step: small batches are launch-bound)
+        QK = linalg.mm_wt_pair(X, W_Q, W_K, b_Q, drop=drop)
         _trace_qk(QK)
         V = QK.shape[0]
         in_norm, out_norm = plan.norms(agg)
@@ -215,7 +215,7 @@ class SIRConvFunction(torch.autograd.Function):
         mask = torch.empty((max(plan.dst.col.numel(), 1) * nw,), device=X.device, dtype=torch.int64) if nw else None
         _native.edge_agg_fwd(plan.dst, QK[:, :H], QK[:, H:], in_norm, out_norm, agg, act, slope, S, partial, mask)
         Y = linalg.mm_wt(S, W_R, b_R)
-        ctx.save_for_backward(X, W_cat, W_R, S, mask if mask is not None else QK)
+        ctx.save_for_backward(X, W_Q, W_K, W_R, S, mask if mask is not None else QK)
         ctx.masked = mask is not None
         ctx.plan, ctx.agg, ctx.act, ctx.slope, ctx.drop = plan, agg, act, slope, drop
         ctx.has_bq, ctx.has_br = b_Q is not None, b_R is not None
@@ -223,7 +223,7 @@ class SIRConvFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dY):
-        X, W_cat, W_R, S, saved = ctx.saved_tensors
+        X, W_Q, W_K, W_R, S, saved = ctx.saved_tensors
         plan, agg, act, slope = ctx.plan, ctx.agg, ctx.act, ctx.slope
         H = W_R.shape[1]
         V = X.shape[0]
@@ -238,7 +238,7 @@ class SIRConvFunction(torch.autograd.Function):
             mask = None
         dQK = torch.empty((V, 2 * H), device=X.device, dtype=torch.float32)
         edge_backward(plan, H, agg, act, slope, G, Q, K, mask, dQK, ctx.drop)
-        dX = linalg.mm_w(dQK, W_cat) if ctx.needs_input_grad[0] else None
+        dX = linalg.mm_w_pair(dQK, W_Q, W_K) if ctx.needs_input_grad[0] else None
         dW_Q = dW_K = db_Q = None
         need_bq = ctx.has_bq and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:

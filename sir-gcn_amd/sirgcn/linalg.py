@@ -80,6 +80,34 @@ def mm_w(A, W, out=None):
     return torch.mm(A, W, out=out)
 
 
+def _pair_ok(A, W, W2):
+    return (USE_NATIVE and _ok(A) and A.shape[0] < DIRECT_ROWS
+            and all(w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.stride(1) == 1
+                    and w.stride(0) % 4 == 0 and w.stride(0) <= MAX_LD and w.data_ptr() % 16 == 0 for w in (W, W2)))
+
+
+def mm_wt_pair(A, W, W2, bias=None, drop=None):
+    """A [W; W2]^T + [bias; 0] (the layer's QK = X [W_Q; W_K]^T + [b_Q; 0], conv.py:60-61): on the
+    small-batch route the kernel reads W and W2 where they lie and adds the bias to the first
+    W.shape[0] outputs only (``sir_gemm_nt_direct2``) — no concatenated weight, no padded bias per
+    step; elsewhere the cat + pad + :func:`mm_wt`."""
+    n1 = W.shape[0]
+    if (_pair_ok(A, W, W2) and n1 % 4 == 0 and W2.shape[0] % 4 == 0
+            and (bias is None or (bias.is_cuda and bias.dtype == torch.float32 and bias.is_contiguous()
+                                  and bias.data_ptr() % 16 == 0))):
+        return _native.gemm_nt_direct2(A, W, W2, False, bias, n1 if bias is not None else 0, drop=drop)
+    Wc = torch.cat([W, W2], 0)
+    return mm_wt(A, Wc, torch.nn.functional.pad(bias, (0, W2.shape[0])) if bias is not None else None, drop=drop)
+
+
+def mm_w_pair(A, W, W2):
+    """A [W; W2] (the layer's dX = [dQ dK] [W_Q; W_K]): in place on the small-batch route, else the
+    cat + :func:`mm_w`."""
+    if _pair_ok(A, W, W2) and W.shape[1] % 4 == 0:
+        return _native.gemm_nt_direct2(A, W, W2, True)
+    return mm_w(A, torch.cat([W, W2], 0))
+
+
 def mm_w_dact(A, W, gate, act, slope, gate_mask=None):
     """sigma'(gate) * (A W) for the ReLU family (W [K, N]; ``gate`` the activation's input or output,
     same sign; ``gate_mask``: its sign words, N = 256): native with the activation backward in the

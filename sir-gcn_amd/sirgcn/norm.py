@@ -52,6 +52,56 @@ class GraphNormFunction(torch.autograd.Function):
         return dX, dw, db, dms, None, None
 
 
+class GraphNormActFunction(torch.autograd.Function):
+    """act(GraphNorm(X)) + R in one kernel per direction (``sir_graph_norm_act_fwd`` / ``_bwd``):
+    the stack loop's ``norm -> activation -> + resid`` (ogbn-arxiv/model.py:65-73,
+    ogbg-molhiv/model.py:76-84; R = None: zinc/model.py:54-55).  The same ops as the three torch
+    calls, so the same bits; R's gradient is the incoming gradient itself."""
+
+    @staticmethod
+    def forward(ctx, X, weight, bias, mean_scale, off, eps, act, slope, R):
+        X = X.contiguous().float()
+        B = off.numel() - 1
+        F = X.shape[1]
+        Y = torch.empty_like(X)
+        mean = torch.empty((B, F), device=X.device, dtype=torch.float32)
+        std = torch.empty_like(mean)
+        w = weight.contiguous().float()
+        b = bias.contiguous().float() if bias is not None else None
+        ms = mean_scale.contiguous().float() if mean_scale is not None else None
+        Rc = R.contiguous() if R is not None else None
+        _native.graph_norm_act_fwd(off, X, w, b, ms, eps, act, slope, Rc, Y, mean, std)
+        ctx.save_for_backward(X, w, b if b is not None else w, ms if ms is not None else w, mean, std, off)
+        ctx.has_b, ctx.has_ms, ctx.has_r = bias is not None, mean_scale is not None, R is not None
+        ctx.act, ctx.slope = act, slope
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        X, w, b, ms, mean, std, off = ctx.saved_tensors
+        b = b if ctx.has_b else None
+        ms = ms if ctx.has_ms else None
+        dY = dY.contiguous().float()
+        dX = torch.empty_like(X)
+        parts = torch.empty((3 if ms is not None else 2,) + tuple(mean.shape), device=X.device, dtype=torch.float32)
+        _native.graph_norm_act_bwd(off, X, dY, w, b, ms, mean, std, ctx.act, ctx.slope, dX, parts[0],
+                                   parts[2] if ms is not None else None, parts[1])
+        sums = parts.sum(1)
+        return (dX, sums[0], sums[1] if ctx.has_b else None, sums[2] if ms is not None else None, None, None, None,
+                None, dY if ctx.has_r else None)
+
+
+def _act_code(m):
+    """(code, slope) of an activation module the fused kernel applies, else None."""
+    if isinstance(m, nn.ReLU):
+        return _native.ACT_RELU, 0.0
+    if isinstance(m, nn.LeakyReLU):
+        return _native.ACT_LEAKY, float(m.negative_slope)
+    if isinstance(m, nn.Identity):
+        return _native.ACT_IDENTITY, 0.0
+    return None
+
+
 class GraphNorm(nn.Module):
     """``models/norm.py:7-29`` GraphNorm, fused (see module docstring)."""
 
@@ -69,3 +119,18 @@ class GraphNorm(nn.Module):
         b = self.bias if isinstance(self.bias, torch.Tensor) else None
         ms = self.mean_scale if isinstance(self.mean_scale, torch.Tensor) else None
         return GraphNormFunction.apply(feats, self.weight, b, ms, off, float(self.eps))
+
+    def forward_act(self, graphs, feats, activation, resid=None):
+        """``activation(self(graphs, feats)) + resid`` (resid None: no add) in one kernel per
+        direction, or None when the activation / operands are not the fused kernel's, or a hook
+        waits on either module's call (the caller then runs the three steps itself)."""
+        code = _act_code(activation)
+        hooked = any(len(h) for m in (self, activation) for h in (m._forward_pre_hooks, m._forward_hooks,
+                                                                 m._backward_hooks, m._backward_pre_hooks))
+        if (code is None or hooked or feats.dim() != 2 or not feats.is_cuda
+                or (resid is not None and (resid.dtype != torch.float32 or resid.shape != feats.shape))):
+            return None
+        off = node_offsets(graphs, feats.device)
+        b = self.bias if isinstance(self.bias, torch.Tensor) else None
+        ms = self.mean_scale if isinstance(self.mean_scale, torch.Tensor) else None
+        return GraphNormActFunction.apply(feats, self.weight, b, ms, off, float(self.eps), code[0], code[1], resid)

@@ -44,6 +44,13 @@ class SIRStack(nn.Module):
             if self.order == "zinc":
                 feats = feats + resid
             if self.norms is not None:
+                # norm -> act (-> + resid) as one op when the norm offers it (sirgcn.GraphNorm:
+                # one kernel per direction; None: not for this activation / these operands)
+                fuse = getattr(self.norms[i], "forward_act", None)
+                out = fuse(graph, feats, self.activation, resid if self.order == "arxiv" else None) if fuse else None
+                if out is not None:
+                    feats = out
+                    continue
                 feats = self.norms[i](graph, feats)
             feats = self.activation(feats)
             if self.order == "arxiv":

@@ -453,6 +453,35 @@ def test_gemm_tn_small_lt_arrangements(cfg, R, M, N, monkeypatch):
     assert e_ours <= max(2 * e_torch, 2e-7), (e_ours, e_torch)
 
 
+@pytest.mark.parametrize("M,n1,n2,K", [(1582, 300, 300, 300), (97, 36, 100, 68), (1, 4, 8, 4), (4099, 128, 64, 256)])
+@pytest.mark.parametrize("trans", [False, True])
+def test_gemm_nt_direct2_two_part_weight_bit_identical(M, n1, n2, K, trans):
+    """sir_gemm_nt_direct2 reads [W; W2] in place (split inside a tile for 300 = 4 x 64 + 44) and adds
+    the bias to the first rows' outputs only: the same bits as sir_gemm_nt_direct on the
+    concatenated weight with the zero-padded bias (dropout included)."""
+    g = torch.Generator(device=DEV).manual_seed(M + n1 + n2 + K)
+    if trans:   # weight [K1 + K2, N]: A has K1 + K2 columns
+        A = torch.randn(M, n1 + n2, device=DEV, generator=g)
+        W = torch.randn(n1, K, device=DEV, generator=g)
+        W2 = torch.randn(n2, K, device=DEV, generator=g)
+        ref = _native.gemm_nt_direct(A, torch.cat([W, W2], 0), True)
+        got = _native.gemm_nt_direct2(A, W, W2, True)
+        assert torch.equal(got, ref)
+        return
+    A = torch.randn(M, K, device=DEV, generator=g)
+    W = torch.randn(n1, K, device=DEV, generator=g)
+    W2 = torch.randn(n2, K, device=DEV, generator=g)
+    b = torch.randn(n1, device=DEV, generator=g)
+    Wc, bc = torch.cat([W, W2], 0), torch.nn.functional.pad(b, (0, n2))
+    for drop in (None, (9, 0.3)):
+        ref = _native.gemm_nt_direct(A, Wc, False, bc, drop=drop)
+        got = _native.gemm_nt_direct2(A, W, W2, False, b, drop=drop)
+        assert torch.equal(got, ref)
+    assert torch.equal(_native.gemm_nt_direct2(A, W, W2), _native.gemm_nt_direct(A, Wc, False))
+    with pytest.raises(RuntimeError, match="split"):
+        _native.gemm_nt_direct2(A, W[:0], W2, False)
+
+
 def test_gemm_nt_direct_dropout_epilogue_and_errors():
     """The QK dropout in the direct kernel's epilogue: the kept entries are exactly the undropped
     result times 1/(1-p), the same hashed mask as the packed-weight kernels, ~p dropped."""

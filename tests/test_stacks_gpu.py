@@ -263,6 +263,25 @@ def test_cfg2_zinc_shaped_4_layers_autocast(dt, tol):
         assert e <= max(tol, 1.25 * e_amp), (what, e, e_amp)
 
 
+@pytest.mark.parametrize("name", ["cfg5", "cfg2"])
+def test_fused_norm_activation_residual_bit_identical(name, monkeypatch):
+    """The stack's norm -> activation (-> + resid) as one GraphNorm kernel per direction
+    (GraphNorm.forward_act: arxiv order for cfg5, zinc order with R = None for cfg2, in fp32 here)
+    gives the same bits as the three separate steps, forward and every gradient."""
+    g = make_graph(name, small=True)
+    X, dY = make_inputs(name, g.num_nodes(), DEV)
+    ours, _ = _stacks(name)
+    for m in ours.modules():          # dropout off: the two runs must draw nothing
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    fused = _run(ours, g, X, dY)
+    monkeypatch.setattr(GraphNorm, "forward_act", lambda self, *a, **k: None)
+    plain = _run(ours, g, X, dY)
+    assert torch.equal(fused[0], plain[0]) and torch.equal(fused[1], plain[1])
+    for k in plain[2]:
+        assert torch.equal(fused[2][k], plain[2][k]), k
+
+
 @pytest.mark.parametrize("name", ["cfg1", "cfg5"])
 def test_small_batches_on_the_product_gemm_route(name, monkeypatch):
     """The product's own GEMM routing (linalg.MIN_ROWS / MIN_ROWS_16 at their defaults — the suite
