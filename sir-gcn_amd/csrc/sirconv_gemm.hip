@@ -1634,34 +1634,36 @@ k_gemm_reduce2(const float* __restrict__ part, int P, int64_t count, int Nc, flo
 //   EPI 1 (TN): part[p][op0 line][op1 line] (+ column sums of op0)  (op0 = A cols, op1 = B cols)
 template <bool C0, bool C1, int W0, int W1, int WK, int NS>
 struct Lt {
+    static constexpr int NT = 64 * W0 * W1 * WK;                              // threads (4 or 8 waves)
     static constexpr int L0 = 32 * W0, L1 = 32 * W1, KS = 32 * WK;
     static constexpr int F0 = L0 * KS, F1 = L1 * KS;                          // floats per stage image
     static constexpr int BUF = F0 + F1;
-    static constexpr int N0 = L0 * KS / 1024, N1 = L1 * KS / 1024;            // DMAs per thread per step
+    static constexpr int N0 = L0 * KS / (4 * NT), N1 = L1 * KS / (4 * NT);    // DMAs per thread per step
     static constexpr int D = N0 + N1;
     static constexpr int RED = (WK - 1) * W0 * W1 * 16 * 64;                  // partial-tile floats
     static constexpr int CRED = 2 * W0 * 32 * WK;                             // column-sum halves
     static constexpr int LDS = (NS * BUF > RED + CRED ? NS * BUF : RED + CRED);
-    static_assert(W0 * W1 * WK == 4, "4 waves");
-    static_assert(N0 >= 1 && N1 >= 1, "a DMA per thread");
+    static_assert(NT == 256 || NT == 512, "4 or 8 waves");
+    static_assert(N0 >= 1 && N1 >= 1 && N0 * 4 * NT == L0 * KS && N1 * 4 * NT == L1 * KS, "whole DMAs per thread");
     static_assert(NS >= 2 && (NS - 2) * D <= 63, "vmcnt range");
+    static_assert(LDS * 4 <= 160 * 1024, "LDS");
 };
 
 __device__ __attribute__((aligned(16))) float g_lt_zero[4];    // source of the DMAs past the operand
 
 // one operand of the block: element (line, k) of the block's tile at x[line * ld + k] (CONTIG) or
 // x[k * ld + line]; lines >= `lines` and k >= `klen` read as zeros (k in 4-aligned groups: klen % 4 == 0
-// for CONTIG operands, checked by the launchers).  Thread t fills the 16-byte slots u = t + 256 i
-// (i < N) of every step's image (wave-instruction i of wave w: slots 256 i + 64 w + lane); the
+// for CONTIG operands, checked by the launchers).  Thread t of NT fills the 16-byte slots u = t + NT i
+// (i < N) of every step's image (wave-instruction i of wave w: slots NT i + 64 w + lane); the
 // slot's source at step 0 and its k offset are set up once, a step adds s * KS (CONTIG) or
 // s * KS * ld (strided) elements.  TWO: the operand's weight-row index (the line for CONTIG, k for
 // strided) continues from `split` on in a second array x2 (row r >= split at x2 + (r - split) ld2):
 // the layer's [W_Q; W_K] read as it lies, no concatenated copy.  `row0`: the weight row of the
 // tile's line / k 0; x2 is offset to the tile along the other index (k for CONTIG, line otherwise).
-template <bool CONTIG, int L, int KS, bool TWO = false>
+template <bool CONTIG, int L, int KS, int NT, bool TWO = false>
 struct LtOp {
     static constexpr int NC = KS / 4;                                 // 16-byte slots per image line
-    static constexpr int N = L * KS / 1024;
+    static constexpr int N = L * KS / (4 * NT);
     static constexpr bool SPLIT_K = TWO && !CONTIG;                  // the part is chosen per step
     const float* src[N];
     const float* src2[SPLIT_K ? N : 1];
@@ -1680,7 +1682,7 @@ struct LtOp {
         }
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            const int u = t + 256 * i;
+            const int u = t + NT * i;
             int line, k;
             if constexpr (CONTIG) { line = u / NC; k = 4 * ((u % NC) ^ swz(u / NC)); }
             else { k = u / (L / 4); line = 4 * (u % (L / 4)); }
@@ -1742,7 +1744,7 @@ __device__ uint64_t* g_lt_trace;
 #define SIR_LT_TRACE_AT(i, v) do { } while (0)
 #endif
 template <bool C0, bool C1, int W0, int W1, int WK, int NS, int EPI>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * W0 * W1 * WK)
 k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X1, int64_t ld1, int64_t n0lines,
           int64_t n1lines, int64_t klen_all, int nt0, int nt1, int64_t rps, const float* __restrict__ bias,
           float* __restrict__ C, int64_t ldc, float* __restrict__ csum_part, Drop drop,
@@ -1765,10 +1767,10 @@ k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X
     const int64_t v0 = p * rps;
     const int klen = (int)(klen_all - v0 < rps ? klen_all - v0 : rps);
     // NT (EPI 0): op0 is the weight, possibly in two parts (X0 rows < split0, X0b the rest)
-    const LtOp<C0, G::L0, G::KS, EPI == 0> o0(C0 ? X0 + a0 * ld0 + v0 : X0 + v0 * ld0 + a0, ld0, lines0, klen, t,
+    const LtOp<C0, G::L0, G::KS, G::NT, EPI == 0> o0(C0 ? X0 + a0 * ld0 + v0 : X0 + v0 * ld0 + a0, ld0, lines0, klen, t,
                                               X0b == nullptr ? nullptr : (C0 ? X0b + v0 : X0b + a0), ld0b, split0,
                                               C0 ? a0 : v0);
-    const LtOp<C1, G::L1, G::KS> o1(C1 ? X1 + a1 * ld1 + v0 : X1 + v0 * ld1 + a1, ld1, lines1, klen, t);
+    const LtOp<C1, G::L1, G::KS, G::NT> o1(C1 ? X1 + a1 * ld1 + v0 : X1 + v0 * ld1 + a1, ld1, lines1, klen, t);
     const int nsteps = klen > 0 ? (klen + G::KS - 1) / G::KS : 0;
     constexpr bool CS = EPI == 1;
     const bool do_cs = CS && csum_part != nullptr && t1 == 0 && w1 == 0;
@@ -1778,9 +1780,9 @@ k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X
     auto issue = [&](int s) {
         float* img = lds + (s % NS) * G::BUF;
 #pragma unroll
-        for (int i = 0; i < G::N0; ++i) dma16(o0.at(i, s), img + (256 * i + 64 * w) * 4);
+        for (int i = 0; i < G::N0; ++i) dma16(o0.at(i, s), img + (G::NT * i + 64 * w) * 4);
 #pragma unroll
-        for (int i = 0; i < G::N1; ++i) dma16(o1.at(i, s), img + G::F0 + (256 * i + 64 * w) * 4);
+        for (int i = 0; i < G::N1; ++i) dma16(o1.at(i, s), img + G::F0 + (G::NT * i + 64 * w) * 4);
     };
     // the epilogue's bias and dropout seed, loaded ahead of the loop (their latency off the tail)
     float4 bb[4];
@@ -1811,8 +1813,8 @@ k_gemm_lt(const float* __restrict__ X0, int64_t ld0, const float* __restrict__ X
         const float* img = lds + (s % NS) * G::BUF;
         if ((s * WK + wk) * 32 < klen) {
             float x0[16], x1[16];
-            LtOp<C0, G::L0, G::KS, EPI == 0>::read(img, w0 * 32 + j, wk, h, x0);
-            LtOp<C1, G::L1, G::KS>::read(img + G::F0, w1 * 32 + j, wk, h, x1);
+            LtOp<C0, G::L0, G::KS, G::NT, EPI == 0>::read(img, w0 * 32 + j, wk, h, x0);
+            LtOp<C1, G::L1, G::KS, G::NT>::read(img + G::F0, w1 * 32 + j, wk, h, x1);
 #ifdef SIR_LT_TRACE
             if (s == 1) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1897,12 +1899,13 @@ static int64_t gemm_small_rows() {
 #define SIR_TN_S_ROWS 512       // k_gemm_tn_s: node rows per split (<= 16 splits)
 #endif
 // LDS-tiled small GEMMs (k_gemm_lt) and their wave arrangement (W0 x W1 tiles of 32 x 32, WK
-// k-ways).  NT: 1 = 2x2x1, 2 = 1x2x2, 3 = 2x1x2 (default: 64 weight lines x 32 rows), 4 = 1x1x4,
-// 5 = 1x4x1; TN: 1 = 2x2x1, 2 = 1x2x2 (default), 3 = 1x1x4; 0 = the 4-wave k_gemm_nt_sw /
+// k-ways).  NT: 1 = 2x2x1, 2 = 1x2x2, 3 = 2x1x2 (64 weight lines x 32 rows), 4 = 1x1x4, 5 = 1x4x1,
+// 8 waves: 6 = 2x1x4, 7 = 1x2x4, 8 = 2x2x2; default by shape (nt_lt_auto); TN: 1 = 2x2x1, 2 = 1x2x2 (default),
+// 3 = 1x1x4, 8 waves: 4 = 1x2x4, 5 = 2x2x2; 0 = the 4-wave k_gemm_nt_sw /
 // k_gemm_tn_s.  env SIR_LT_NT / SIR_LT_TN override per call (A/B runs, the arrangement tests);
 // measured in profiles/r05_small_gemm.txt.
 #ifndef SIR_LT_NT
-#define SIR_LT_NT 3
+#define SIR_LT_NT -1            // -1: by shape (nt_lt_auto)
 #endif
 #ifndef SIR_LT_TN
 #define SIR_LT_TN 2
@@ -1968,16 +1971,29 @@ static void launch_nt_lt(const float* A, int64_t lda, int64_t M, int K, const Nt
     using G = Lt<!TRANS, true, W0, W1, WK, SIR_LT_NS>;
     const int nt0 = (N + G::L0 - 1) / G::L0;
     const int64_t nt1 = (M + G::L1 - 1) / G::L1;
-    hipLaunchKernelGGL((k_gemm_lt<!TRANS, true, W0, W1, WK, SIR_LT_NS, 0>), dim3((unsigned)(nt0 * nt1)), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_gemm_lt<!TRANS, true, W0, W1, WK, SIR_LT_NS, 0>), dim3((unsigned)(nt0 * nt1)), dim3(G::NT), 0, st,
                        w.W, w.ldw, A, lda, (int64_t)N, M, (int64_t)K, nt0, (int)nt1, (int64_t)K, bias, C, ldc, nullptr,
                        drop, w.W2, w.ldw2, w.split, w.bias_cols);
+}
+
+// The arrangement by shape: every block is latency-bound (one block's steps set the time, not the
+// CU's bandwidth: half the rows take as long), so the most k-ways whose grid still fits one round
+// on the CUs wins — 8 waves as 32 features x 64 rows x 4 k-ways (7), else 64 x 64 x 2 k-ways (8),
+// else the 4-wave 64 x 32 x 2 (3) at 2+ blocks per CU (profiles/r05_small_gemm.txt: config 5's
+// QK 11.9 -> 10.3 us, R / dY W_R 8.5 / 9.4 -> 7.8 / 8.0, dX 15.1 -> 11.2).
+static int nt_lt_auto(int64_t M, int N) {
+    const int64_t ncu = device_cu_count();
+    if ((int64_t)((N + 31) / 32) * ((M + 63) / 64) <= ncu) return 7;
+    if ((int64_t)((N + 63) / 64) * ((M + 63) / 64) <= ncu) return 8;
+    return 3;
 }
 
 hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, const float* W, int64_t ldw, int trans,
                               int N, const float* bias, float* C, int64_t ldc, hipStream_t st, const Drop& drop,
                               const float* W2, int64_t ldw2, int64_t split, int64_t bias_cols) {
     if (M == 0 || N == 0) return hipSuccess;
-    const int lt = lt_env("SIR_LT_NT", SIR_LT_NT);
+    int lt = lt_env("SIR_LT_NT", SIR_LT_NT);
+    if (lt < 0) lt = nt_lt_auto(M, N);
     const NtW w{W, ldw, W2, ldw2, W2 != nullptr ? split : INT64_MAX, bias_cols};
     // k_gemm_lt: 16-byte loads of both operands (and of W2), every byte offset of a tile's resource in 31 bits
     if (lt > 0 && K % 4 == 0 && N % 4 == 0 && aligned16(A, lda) && aligned16(W, ldw) && ((uintptr_t)bias & 15u) == 0
@@ -1995,6 +2011,12 @@ hipError_t run_gemm_nt_direct(const float* A, int64_t lda, int64_t M, int K, con
         case 9: launch_nt_lt<true, 1, 1, 4>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
         case 10: launch_nt_lt<false, 1, 4, 1>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
         case 11: launch_nt_lt<true, 1, 4, 1>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 12: launch_nt_lt<false, 2, 1, 4>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;   // 8 waves
+        case 13: launch_nt_lt<true, 2, 1, 4>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 14: launch_nt_lt<false, 1, 2, 4>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 15: launch_nt_lt<true, 1, 2, 4>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 16: launch_nt_lt<false, 2, 2, 2>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
+        case 17: launch_nt_lt<true, 2, 2, 2>(A, lda, M, K, w, N, bias, C, ldc, st, drop); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
@@ -2140,6 +2162,28 @@ int64_t gemm_tn_workspace(int64_t R, int64_t Mc, int64_t Nc) {
     return P * (Mc * Nc + Mc) * 4;                         // partial products + column sums
 }
 
+// k_gemm_lt TN arrangements (SIR_LT_TN): 1 = 2x2x1, 2 = 1x2x2, 3 = 1x1x4, 4 = 1x2x4 and 5 = 2x2x2 (8 waves)
+static int lt_tn_w0(int lt) { return (lt == 1 || lt == 5) ? 2 : 1; }
+static int lt_tn_w1(int lt) { return lt == 3 ? 1 : 2; }
+static int lt_tn_ks(int lt) { return 32 * (lt == 1 ? 1 : (lt == 2 || lt == 5) ? 2 : 4); }
+static int64_t lt_tn_tiles(int lt, int Mc, int Nc) {
+    const int a = 32 * lt_tn_w0(lt), b = 32 * lt_tn_w1(lt);
+    return (int64_t)((Mc + a - 1) / a) * ((Nc + b - 1) / b);
+}
+template <int W0, int W1, int WK>
+static void launch_tn_lt(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
+                         float* part, bool colsum, hipStream_t st) {
+    using G = Lt<false, false, W0, W1, WK, SIR_LT_NS>;
+    const int nt0 = (Mc + G::L0 - 1) / G::L0, nt1 = (Nc + G::L1 - 1) / G::L1;
+    const int64_t tiles = (int64_t)nt0 * nt1;
+    int64_t rl = 0;
+    const int Pl = gemm_tn_splits_lt(R, tiles, G::KS, &rl);
+    float* cp = colsum ? part + (int64_t)Pl * Mc * Nc : nullptr;
+    hipLaunchKernelGGL((k_gemm_lt<false, false, W0, W1, WK, SIR_LT_NS, 1>), dim3((unsigned)(Pl * tiles)), dim3(G::NT), 0,
+                       st, A, lda, B, ldb, (int64_t)Mc, (int64_t)Nc, R, nt0, nt1, rl, nullptr, part, (int64_t)0, cp,
+                       Drop{});
+}
+
 hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t R, int Mc, int Nc,
                        float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st) {
     if (Mc == 0 || Nc == 0) return hipSuccess;
@@ -2150,30 +2194,23 @@ hipError_t run_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb,
     float* part = static_cast<float*>(workspace);
     float* cpart = colsum != nullptr ? part + (int64_t)P * Mc * Nc : nullptr;
     const int lt = lt_env("SIR_LT_TN", SIR_LT_TN);
-    if (small && lt > 0 && aligned16(A, lda) && aligned16(B, ldb) && (Mc + 31) / 32 * ((Nc + 31) / 32) < (1 << 24)) {
-        const int W0 = lt == 1 ? 2 : 1, W1 = lt == 1 ? 2 : (lt == 2 ? 2 : 1), WK = 4 / (W0 * W1);
-        const int64_t tiles = (int64_t)((Mc + 32 * W0 - 1) / (32 * W0)) * ((Nc + 32 * W1 - 1) / (32 * W1));
-        int64_t rl = 0;
-        const int Pl = gemm_tn_splits_lt(R, tiles, 32 * WK, &rl);
-        if (rl * std::max(lda, ldb) < ((int64_t)1 << 29)) {
-            float* cp = colsum != nullptr ? part + (int64_t)Pl * Mc * Nc : nullptr;
-            const int nt0 = (Mc + 32 * W0 - 1) / (32 * W0), nt1 = (Nc + 32 * W1 - 1) / (32 * W1);
-            const dim3 grid((unsigned)((int64_t)Pl * tiles));
-            if (lt == 1)
-                hipLaunchKernelGGL((k_gemm_lt<false, false, 2, 2, 1, SIR_LT_NS, 1>), grid, dim3(256), 0, st, A, lda, B, ldb,
-                                   (int64_t)Mc, (int64_t)Nc, R, nt0, nt1, rl, nullptr, part, (int64_t)0, cp, Drop{});
-            else if (lt == 2)
-                hipLaunchKernelGGL((k_gemm_lt<false, false, 1, 2, 2, SIR_LT_NS, 1>), grid, dim3(256), 0, st, A, lda, B, ldb,
-                                   (int64_t)Mc, (int64_t)Nc, R, nt0, nt1, rl, nullptr, part, (int64_t)0, cp, Drop{});
-            else
-                hipLaunchKernelGGL((k_gemm_lt<false, false, 1, 1, 4, SIR_LT_NS, 1>), grid, dim3(256), 0, st, A, lda, B, ldb,
-                                   (int64_t)Mc, (int64_t)Nc, R, nt0, nt1, rl, nullptr, part, (int64_t)0, cp, Drop{});
-            const int64_t count = (int64_t)Mc * Nc;
-            const int64_t nbm = (count + 255) / 256, nbc = colsum != nullptr ? (Mc + 255) / 256 : 0;
-            hipLaunchKernelGGL(k_gemm_reduce2, dim3((unsigned)(nbm + nbc)), dim3(256), 0, st, part, Pl, count, Nc, C, ldc,
-                               cp, Mc, colsum, nbm);
-            return hipGetLastError();
+    if (small && lt > 0 && lt <= 5 && aligned16(A, lda) && aligned16(B, ldb) && (Mc + 31) / 32 * ((Nc + 31) / 32) < (1 << 24)) {
+        switch (lt) {
+        case 1: launch_tn_lt<2, 2, 1>(A, lda, B, ldb, R, Mc, Nc, part, colsum != nullptr, st); break;
+        case 2: launch_tn_lt<1, 2, 2>(A, lda, B, ldb, R, Mc, Nc, part, colsum != nullptr, st); break;
+        case 3: launch_tn_lt<1, 1, 4>(A, lda, B, ldb, R, Mc, Nc, part, colsum != nullptr, st); break;
+        case 4: launch_tn_lt<1, 2, 4>(A, lda, B, ldb, R, Mc, Nc, part, colsum != nullptr, st); break;   // 8 waves
+        default: launch_tn_lt<2, 2, 2>(A, lda, B, ldb, R, Mc, Nc, part, colsum != nullptr, st); break;  // 8 waves
         }
+        const int64_t tiles = lt_tn_tiles(lt, Mc, Nc);
+        int64_t rl = 0;
+        const int Pl = gemm_tn_splits_lt(R, tiles, lt_tn_ks(lt), &rl);
+        float* cp = colsum != nullptr ? part + (int64_t)Pl * Mc * Nc : nullptr;
+        const int64_t count = (int64_t)Mc * Nc;
+        const int64_t nbm = (count + 255) / 256, nbc = colsum != nullptr ? (Mc + 255) / 256 : 0;
+        hipLaunchKernelGGL(k_gemm_reduce2, dim3((unsigned)(nbm + nbc)), dim3(256), 0, st, part, Pl, count, Nc, C, ldc,
+                           cp, Mc, colsum, nbm);
+        return hipGetLastError();
     }
     if (small) {
         const int smt = (Mc + 31) / 32, snt = (Nc + 31) / 32;

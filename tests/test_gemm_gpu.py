@@ -402,12 +402,13 @@ def test_gemm_nt_direct_vs_fp64(M, K, N, trans, with_bias):
     assert torch.equal(C, _native.gemm_nt_direct(A, W, trans, b)), "deterministic"
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5", "6", "7", "8"])
 @pytest.mark.parametrize("M,K,N", [(1582, 300, 600), (1582, 600, 300), (33, 36, 12), (97, 68, 132), (1, 32, 4)])
 @pytest.mark.parametrize("trans", [False, True])
 def test_gemm_nt_direct_lt_arrangements(cfg, M, K, N, trans, monkeypatch):
     """Every wave arrangement of the LDS-tiled small kernel (SIR_LT_NT: 1 = 2x2 tiles, 2 = 1x2 tiles x
-    2 k-ways, 3 = 2x1 x 2, 4 = 1 tile x 4 k-ways, 5 = 1x4; 0 = the 4-wave k_gemm_nt_sw) vs fp64 with
+    2 k-ways, 3 = 2x1 x 2, 4 = 1 tile x 4 k-ways, 5 = 1x4; 8 waves: 6 = 2x1 x 4, 7 = 1x2 x 4, 8 = 2x2 x 2;
+    0 = the 4-wave k_gemm_nt_sw) vs fp64 with
     bias and dropout, ragged tiles, a row whose scale grows along K; a weight view not 16-byte aligned
     takes k_gemm_nt_sw whatever the setting."""
     monkeypatch.setenv("SIR_LT_NT", cfg)
@@ -430,11 +431,12 @@ def test_gemm_nt_direct_lt_arrangements(cfg, M, K, N, trans, monkeypatch):
     _check(C2, A.double(), Wt.double(), torch.addmm(b, A, Wt), b, f"nt unaligned lt{cfg}")
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("R,M,N", [(1582, 600, 300), (1582, 300, 300), (37, 64, 128), (70, 36, 100), (3000, 4, 8)])
 def test_gemm_tn_small_lt_arrangements(cfg, R, M, N, monkeypatch):
     """The small TN route per LDS arrangement (SIR_LT_TN: 1 = 2x2 tiles, 2 = 1x2 x 2 k-ways, 3 = 1 x 4
-    k-ways; 0 = k_gemm_tn_s): product and column sums vs fp64, deterministic, ragged rows and tiles."""
+    k-ways; 8 waves: 4 = 1x2 x 4, 5 = 2x2 x 2; 0 = k_gemm_tn_s): product and column sums vs fp64,
+    deterministic, ragged rows and tiles."""
     monkeypatch.setenv("SIR_LT_TN", cfg)
     monkeypatch.setenv("SIR_GEMM_SMALL_ROWS", ROUTES["small"])
     g = torch.Generator(device=DEV).manual_seed(R + M + N + int(cfg))

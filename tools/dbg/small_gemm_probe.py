@@ -66,7 +66,7 @@ def main():
         var = "SIR_LT_NT" if "nt_direct" in name else ("SIR_LT_TN" if "gemm_tn" in name else None)
         for c in (lt if var else ["-"]):
             if var:
-                if var == "SIR_LT_TN" and int(c) > 3:
+                if var == "SIR_LT_TN" and int(c) > 5:
                     continue
                 os.environ[var] = c
             te = timeit(fn)
