@@ -565,6 +565,46 @@ int sir_graph_norm_fwd(const int64_t* off, int64_t B, int64_t F, const float* X,
                   nullptr);
 }
 
+
+int sir_resid_act_fwd(const void* Y, int64_t ldy, int dtype, const float* R, int64_t ldr, float* out, int64_t ldo,
+                      int64_t M, int64_t N, int act, float slope, int order, void* stream) {
+    const char* fn = "sir_resid_act_fwd";
+    if (M < 0 || N <= 0 || N % 4 != 0 || N > (1 << 30)) return fail(SIR_EINVAL, fn, "bad shape (N % 4 == 0)");
+    if (dtype != SIR_DTYPE_F32 && dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "bad dtype");
+    if (act != SIR_ACT_IDENTITY && act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU)
+        return fail(SIR_EINVAL, fn, "act must be identity, relu or leaky_relu");
+    if (order != 0 && order != 1) return fail(SIR_EINVAL, fn, "order must be 0 (zinc) or 1 (arxiv)");
+    if (ldy < N || ldr < N || ldo < N || ldy % 4 || ldr % 4 || ldo % 4)
+        return fail(SIR_EINVAL, fn, "leading dimensions must be >= N and multiples of 4");
+    if (M > 0 && (Y == nullptr || R == nullptr || out == nullptr)) return fail(SIR_EINVAL, fn, "NULL buffer");
+    if (!al16(R) || !al16(out) || (dtype == SIR_DTYPE_F32 ? !al16(Y) : (reinterpret_cast<uintptr_t>(Y) & 7u) != 0))
+        return fail(SIR_EINVAL, fn, "rows must be 16-B aligned (8-B for 16-bit Y)");
+    return finish(fn, sir::run_resid_act_fwd(Y, ldy, dtype, R, ldr, out, ldo, M, (int)N, act, slope, order,
+                                             static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_resid_act_bwd(const float* D, int64_t ldd, const void* Y, int64_t ldy, int dtype, const float* R, int64_t ldr,
+                      void* dY, int64_t lddy, float* dR, int64_t lddr, int64_t M, int64_t N, int act, float slope,
+                      int order, void* stream) {
+    const char* fn = "sir_resid_act_bwd";
+    if (M < 0 || N <= 0 || N % 4 != 0 || N > (1 << 30)) return fail(SIR_EINVAL, fn, "bad shape (N % 4 == 0)");
+    if (dtype != SIR_DTYPE_F32 && dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "bad dtype");
+    if (act != SIR_ACT_IDENTITY && act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU)
+        return fail(SIR_EINVAL, fn, "act must be identity, relu or leaky_relu");
+    if (order != 0 && order != 1) return fail(SIR_EINVAL, fn, "order must be 0 (zinc) or 1 (arxiv)");
+    if (ldd < N || ldy < N || lddy < N || ldd % 4 || ldy % 4 || lddy % 4 ||
+        (order == 0 && (ldr < N || ldr % 4 || (dR != nullptr && (lddr < N || lddr % 4)))))
+        return fail(SIR_EINVAL, fn, "leading dimensions must be >= N and multiples of 4");
+    if (M > 0 && (D == nullptr || Y == nullptr || dY == nullptr || (order == 0 && R == nullptr)))
+        return fail(SIR_EINVAL, fn, "NULL buffer");
+    const bool y16 = dtype != SIR_DTYPE_F32;
+    if (!al16(D) || (y16 ? (reinterpret_cast<uintptr_t>(Y) & 7u) || (reinterpret_cast<uintptr_t>(dY) & 7u)
+                         : !al16(Y) || !al16(dY)) || (order == 0 && (!al16(R) || !al16(dR))))
+        return fail(SIR_EINVAL, fn, "rows must be 16-B aligned (8-B for 16-bit Y, dY)");
+    return finish(fn, sir::run_resid_act_bwd(D, ldd, Y, ldy, dtype, R, ldr, dY, lddy, order == 0 ? dR : nullptr, lddr, M,
+                                             (int)N, act, slope, order, static_cast<hipStream_t>(stream)), nullptr);
+}
+
 int sir_graph_norm_act_fwd(const int64_t* off, int64_t B, int64_t F, const float* X, int64_t ldx,
                            const float* weight, const float* bias, const float* mean_scale, float eps, int act,
                            float slope, const float* R, int64_t ldr, float* Y, int64_t ldy, float* mean, float* std_,

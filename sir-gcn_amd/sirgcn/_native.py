@@ -32,6 +32,9 @@ SIGNATURES = {
     "sir_graph_norm_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _F, _P, _I64, _P, _P, _P]),
     "sir_graph_norm_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I64,
                                           _P, _P, _P, _P]),
+    "sir_resid_act_fwd": (ctypes.c_int, [_P, _I64, _I, _P, _I64, _P, _I64, _I64, _I64, _I, _F, _I, _P]),
+    "sir_resid_act_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _F, _I,
+                                         _P]),
     "sir_graph_norm_act_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _F, _I, _F, _P, _I64, _P, _I64,
                                               _P, _P, _P]),
     "sir_graph_norm_act_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I, _F, _P,
@@ -431,6 +434,31 @@ def graph_norm_fwd(off, X, weight, bias, mean_scale, eps, Y, mean, std):
         rc = lib.sir_graph_norm_fwd(_ptr(off), B, F, _ptr(X), _ld(X, F), _ptr(weight), _ptr(bias),
                                     _ptr(mean_scale), float(eps), _ptr(Y), _ld(Y, F), _ptr(mean), _ptr(std),
                                     _stream(Y.device))
+    _check(rc, lib)
+
+
+_DT_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}     # SIR_DTYPE_F32 / BF16 / F16
+
+
+def resid_act_fwd(Y, R, act, slope, order, out):
+    """out = act(Y + R) (order 0) or act(Y) + R (order 1) in one pass (``sir_resid_act_fwd``)."""
+    lib = load()
+    M, N = Y.shape
+    with _Timed("sir_resid_act_fwd", out.device):
+        rc = lib.sir_resid_act_fwd(_ptr(Y), Y.stride(0), _DT_CODE[Y.dtype], _ptr(R), R.stride(0), _ptr(out),
+                                   out.stride(0), M, N, int(act), float(slope), int(order), _stream(out.device))
+    _check(rc, lib)
+
+
+def resid_act_bwd(D, Y, R, act, slope, order, dY, dR=None):
+    """Backward of :func:`resid_act_fwd` (``sir_resid_act_bwd``): dY in Y's type; order 0 also dR."""
+    lib = load()
+    M, N = Y.shape
+    with _Timed("sir_resid_act_bwd", dY.device):
+        rc = lib.sir_resid_act_bwd(_ptr(D), D.stride(0), _ptr(Y), Y.stride(0), _DT_CODE[Y.dtype], _ptr(R),
+                                   R.stride(0) if R is not None else 0, _ptr(dY), dY.stride(0), _ptr(dR),
+                                   dR.stride(0) if dR is not None else 0, M, N, int(act), float(slope), int(order),
+                                   _stream(dY.device))
     _check(rc, lib)
 
 

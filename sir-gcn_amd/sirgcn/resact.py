@@ -1,0 +1,66 @@
+"""The stack loop's residual + activation around a SIRConv layer without a norm, one native pass
+per direction (``sir_resid_act_fwd`` / ``_bwd``):
+
+* zinc order (``zinc/model.py:53-56``): ``h = act(conv(g, h) + h)``;
+* arxiv order without a norm (``ogbn-arxiv/model.py:65-73``): ``h = act(conv(g, h)) + h``.
+
+Bit-identical to torch's separate add / activation kernels and their autograd (including the
+autocast dtypes: a 16-bit conv output, an fp32 residual); replaces two kernels forward and two or
+three backward (the 16-bit gradient cast included).
+"""
+import torch
+from torch import nn
+
+from . import _native
+
+
+def act_code(m):
+    """(code, slope) of an activation module the native pass applies, else None."""
+    if isinstance(m, nn.ReLU):
+        return _native.ACT_RELU, 0.0
+    if isinstance(m, nn.LeakyReLU):
+        return _native.ACT_LEAKY, float(m.negative_slope)
+    if isinstance(m, nn.Identity):
+        return _native.ACT_IDENTITY, 0.0
+    return None
+
+
+def _ok(t, dtypes):
+    return (t.is_cuda and t.dtype in dtypes and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 4 == 0
+            and t.data_ptr() % (16 if t.dtype == torch.float32 else 8) == 0)
+
+
+class ResidActFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Y, R, act, slope, order):
+        out = torch.empty(Y.shape, device=Y.device, dtype=torch.float32)
+        _native.resid_act_fwd(Y, R, act, slope, order, out)
+        ctx.save_for_backward(Y, R if order == 0 else None)
+        ctx.act, ctx.slope, ctx.order = act, slope, order
+        return out
+
+    @staticmethod
+    def backward(ctx, D):
+        Y, R = ctx.saved_tensors
+        D = D.contiguous()
+        dY = torch.empty_like(Y)
+        if ctx.order == 0:
+            dR = torch.empty(Y.shape, device=Y.device, dtype=torch.float32)
+            _native.resid_act_bwd(D, Y, R, ctx.act, ctx.slope, 0, dY, dR)
+            return dY, dR, None, None, None
+        _native.resid_act_bwd(D, Y, None, ctx.act, ctx.slope, 1, dY)
+        return dY, D, None, None, None
+
+
+def resid_act(y, resid, activation, order):
+    """``activation(y + resid)`` (order "zinc") or ``activation(y) + resid`` ("arxiv") in one pass,
+    or None when the activation / operands are not the native pass's (or a hook waits on the
+    activation's call): the caller then runs the torch ops itself."""
+    code = act_code(activation)
+    hooked = any(len(h) for h in (activation._forward_pre_hooks, activation._forward_hooks,
+                                  activation._backward_hooks, activation._backward_pre_hooks))
+    if (code is None or hooked or order not in ("zinc", "arxiv") or y.shape != resid.shape or y.dim() != 2
+            or y.shape[1] % 4 != 0 or not _ok(y, (torch.float32, torch.bfloat16, torch.float16))
+            or not _ok(resid, (torch.float32,))):
+        return None
+    return ResidActFunction.apply(y, resid, code[0], code[1], 0 if order == "zinc" else 1)

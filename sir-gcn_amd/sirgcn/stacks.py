@@ -19,6 +19,15 @@ MI355X modules (tests, ``bench.py --workload``):
 from torch import nn
 
 
+def _resid_act(y, resid, activation, order):
+    """sirgcn.resact.resid_act for GPU tensors (imported lazily: the stack also runs the reference's
+    own modules on the CPU, where it returns None)."""
+    if not (getattr(y, "is_cuda", False) and getattr(resid, "is_cuda", False)):
+        return None
+    from .resact import resid_act
+    return resid_act(y, resid, activation, order)
+
+
 class SIRStack(nn.Module):
     def __init__(self, conv_cls, hidden, num_layers, activation, agg_type="sum", order="arxiv",
                  norm_cls=None, conv_activation=None, feat_dropout=0):
@@ -41,6 +50,12 @@ class SIRStack(nn.Module):
                 continue
             resid = feats
             feats = conv(graph, feats)
+            if self.norms is None:
+                # + resid and the activation in one pass when the operands allow (sirgcn.resact)
+                fused = _resid_act(feats, resid, self.activation, self.order)
+                if fused is not None:
+                    feats = fused
+                    continue
             if self.order == "zinc":
                 feats = feats + resid
             if self.norms is not None:

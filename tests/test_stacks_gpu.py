@@ -263,20 +263,33 @@ def test_cfg2_zinc_shaped_4_layers_autocast(dt, tol):
         assert e <= max(tol, 1.25 * e_amp), (what, e, e_amp)
 
 
-@pytest.mark.parametrize("name", ["cfg5", "cfg2"])
-def test_fused_norm_activation_residual_bit_identical(name, monkeypatch):
+@pytest.mark.parametrize("name,autocast", [("cfg5", None), ("cfg2", None), ("cfg2", torch.bfloat16),
+                                           ("cfg2", torch.float16), ("cfg3", None), ("cfg3", torch.bfloat16)])
+def test_fused_norm_activation_residual_bit_identical(name, autocast, monkeypatch):
     """The stack's norm -> activation (-> + resid) as one GraphNorm kernel per direction
-    (GraphNorm.forward_act: arxiv order for cfg5, zinc order with R = None for cfg2, in fp32 here)
-    gives the same bits as the three separate steps, forward and every gradient."""
+    (GraphNorm.forward_act: cfg5) and, without a norm, the residual + activation as one pass per
+    direction (sirgcn.resact: cfg2's zinc order act(conv + h), cfg3's arxiv order act(conv) + h,
+    under autocast with the 16-bit conv output) give the same bits as the separate torch steps,
+    forward and every gradient."""
+    import sirgcn.stacks as st
     g = make_graph(name, small=True)
     X, dY = make_inputs(name, g.num_nodes(), DEV)
     ours, _ = _stacks(name)
     for m in ours.modules():          # dropout off: the two runs must draw nothing
         if isinstance(m, torch.nn.Dropout):
             m.p = 0.0
-    fused = _run(ours, g, X, dY)
+    seen = []
+    orig = st._resid_act
+    def spy(*a):
+        r = orig(*a)
+        seen.append(r is not None)
+        return r
+    monkeypatch.setattr(st, "_resid_act", spy)
+    fused = _run(ours, g, X, dY, autocast=autocast)
+    assert name == "cfg5" or (seen and all(seen)), f"the fused residual pass did not run: {seen}"
     monkeypatch.setattr(GraphNorm, "forward_act", lambda self, *a, **k: None)
-    plain = _run(ours, g, X, dY)
+    monkeypatch.setattr(st, "_resid_act", lambda *a: None)
+    plain = _run(ours, g, X, dY, autocast=autocast)
     assert torch.equal(fused[0], plain[0]) and torch.equal(fused[1], plain[1])
     for k in plain[2]:
         assert torch.equal(fused[2][k], plain[2][k]), k
