@@ -61,16 +61,21 @@ __device__ inline float widen(uint32_t bits16) {
         return (float)__builtin_bit_cast(_Float16, (unsigned short)bits16);
 }
 
-template <bool BF>
-__global__ void __launch_bounds__(512)
+// BM x BN output tile per block of BM + BN threads: 256 x 256 (8 waves of 128 x 64, TMT x TNT = 4 x 2
+// MFMA tiles) or, for the narrow gradients of H <= 128 layers (config 2's 128 x 128 and 256 x 128),
+// 128 x 128 (4 waves of 64 x 64) — the 256-wide tile left three quarters of its MFMAs and half its
+// loads on columns past Mc / Nc there.
+template <bool BF, int BM = 256, int BN = 256, int WN = 4, int TMT = 4, int TNT = 2>
+__global__ void __launch_bounds__(BM + BN)
 k_gemm_tn16(const unsigned short* __restrict__ A, int64_t lda, const unsigned short* __restrict__ B, int64_t ldb,
             int64_t R, int Mc, int Nc, float* __restrict__ part, float* __restrict__ csum_part, int n_mtiles,
             int n_ntiles, int64_t rows_per_split) {
-    constexpr int WN = 4, TMT = 4, TNT = 2;
-    constexpr int BM = 256, BN = 256;
+    constexpr int SLOTS = BM / 2 + BN / 2;                       // column pairs per block (a power of 2)
     constexpr int PLANE_A = BM * 32, PLANE_B = BN * 32;          // one k16 step: 32 B per column
     constexpr int A_BYTES = 2 * PLANE_A, B_BYTES = 2 * PLANE_B;
     constexpr int STAGE = A_BYTES + B_BYTES;
+    static_assert((SLOTS & (SLOTS - 1)) == 0 && (BM / 2) % 64 == 0, "slot layout");
+    static_assert((BM / (TMT * 32)) * (BN / (TNT * 32)) == (BM + BN) / 64 && BN / (TNT * 32) == WN, "wave tiling");
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
     const int t = threadIdx.x;
@@ -82,10 +87,10 @@ k_gemm_tn16(const unsigned short* __restrict__ A, int64_t lda, const unsigned sh
     const int64_t v_end = (v_begin + rows_per_split < R) ? v_begin + rows_per_split : R;
     const int nc = v_end > v_begin ? (int)((v_end - v_begin + KC16 - 1) / KC16) : 0;
 
-    // loader: slot = column pair (slots [0, 128) of A, [128, 256) of B: wave-uniform), kse = which
+    // loader: slot = column pair (slots [0, BM/2) of A, the rest of B: wave-uniform), kse = which
     // 16 rows of the chunk (= the k16 step whose plane the pair's pieces go to)
-    const int slot = t & 255, kse = t >> 8;
-    const bool is_a = (__builtin_amdgcn_readfirstlane(t >> 6) & 2) == 0;    // slot < 128, wave-uniform
+    const int slot = t & (SLOTS - 1), kse = t / SLOTS;
+    const bool is_a = (__builtin_amdgcn_readfirstlane(t >> 6) % (SLOTS / 64)) < (BM / 2) / 64;   // wave-uniform
     const int pr = is_a ? slot : slot - BM / 2;
     const int c0 = 2 * pr;
     const bool col_ok = is_a ? (m0 + c0 < Mc) : (n0 + c0 < Nc);
@@ -543,6 +548,15 @@ k_pack16(const float* __restrict__ W, int64_t ldw, int N, int K, int trans, int 
 
 }  // namespace
 
+#ifndef SIR_TN16_NARROW
+#define SIR_TN16_NARROW 1       // 128 x 128 tiles when Mc or Nc <= 128 (env SIR_TN16_NARROW=0: always 256 x 256)
+#endif
+static bool tn16_narrow(int Mc, int Nc) {
+    const char* e = getenv("SIR_TN16_NARROW");
+    const int on = (e != nullptr && e[0] != 0) ? atoi(e) : SIR_TN16_NARROW;
+    return on && (Mc <= 128 || Nc <= 128);
+}
+
 hipError_t run_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t R, int Mc, int Nc, int dtype,
                          float* C, int64_t ldc, float* colsum, void* workspace, hipStream_t st) {
     if (Mc == 0 || Nc == 0) return hipSuccess;
@@ -553,13 +567,24 @@ hipError_t run_gemm_tn16(const void* A, int64_t lda, const void* B, int64_t ldb,
     float* cpart = colsum != nullptr ? part + (int64_t)P * Mc * Nc : nullptr;
     const auto* a = static_cast<const unsigned short*>(A);
     const auto* b = static_cast<const unsigned short*>(B);
-    const dim3 grid((unsigned)(P * nmt * nnt));
-    if (dtype == SIR_DTYPE_BF16)
-        hipLaunchKernelGGL(k_gemm_tn16<true>, grid, dim3(512), 0, st, a, lda, b, ldb, R, Mc, Nc, part, cpart, nmt, nnt,
-                           rps);
-    else
-        hipLaunchKernelGGL(k_gemm_tn16<false>, grid, dim3(512), 0, st, a, lda, b, ldb, R, Mc, Nc, part, cpart, nmt, nnt,
-                           rps);
+    if (tn16_narrow(Mc, Nc)) {      // 128 x 128 tiles, same row splits (the workspace is unchanged)
+        const int nm = (Mc + 127) / 128, nn = (Nc + 127) / 128;
+        const dim3 grid((unsigned)(P * nm * nn));
+        if (dtype == SIR_DTYPE_BF16)
+            hipLaunchKernelGGL((k_gemm_tn16<true, 128, 128, 2, 2, 2>), grid, dim3(256), 0, st, a, lda, b, ldb, R, Mc, Nc,
+                               part, cpart, nm, nn, rps);
+        else
+            hipLaunchKernelGGL((k_gemm_tn16<false, 128, 128, 2, 2, 2>), grid, dim3(256), 0, st, a, lda, b, ldb, R, Mc, Nc,
+                               part, cpart, nm, nn, rps);
+    } else {
+        const dim3 grid((unsigned)(P * nmt * nnt));
+        if (dtype == SIR_DTYPE_BF16)
+            hipLaunchKernelGGL(k_gemm_tn16<true>, grid, dim3(512), 0, st, a, lda, b, ldb, R, Mc, Nc, part, cpart, nmt, nnt,
+                               rps);
+        else
+            hipLaunchKernelGGL(k_gemm_tn16<false>, grid, dim3(512), 0, st, a, lda, b, ldb, R, Mc, Nc, part, cpart, nmt, nnt,
+                               rps);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = run_gemm_reduce(part, P, (int64_t)Mc * Nc, Nc, C, ldc, st);

@@ -179,6 +179,21 @@ def test_gemm_tn16_vs_fp64(dt, R, M, N):
     assert e_ours <= max(2 * e_torch, 1e-6), (e_ours, e_torch)
 
 
+@pytest.mark.parametrize("R,M,N", [(60000, 256, 128), (229532, 128, 128), (5000, 100, 300), (3000, 128, 512)])
+def test_gemm_tn16_narrow_tiles_bit_identical(R, M, N, monkeypatch):
+    """The 128 x 128-tile TN16 kernel (taken when M or N <= 128: config 2's H = 128 gradients) sums
+    the same rows, chunks and MFMAs per output as the 256 x 256 one: bit-identical, column sums too."""
+    g = torch.Generator(device=DEV).manual_seed(R + M + N)
+    A = torch.randn(R, M, device=DEV, generator=g).to(torch.bfloat16)
+    B = torch.randn(R, N, device=DEV, generator=g).to(torch.bfloat16)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SIR_TN16_NARROW", v)
+        out[v] = _native.gemm_tn16(A, B, colsum=True)
+    assert torch.equal(out["1"][0], out["0"][0]) and torch.equal(out["1"][1], out["0"][1])
+    _check(out["1"][0], A.double().t(), B.double(), A.float().t() @ B.float(), None, f"tn16 narrow R={R}")
+
+
 def test_gemm_tn16_strided_and_wide_range():
     """lda > M (a column slice of a wider tensor, as dQK[:, :H]), values spread over many binades
     (bf16 keeps fp32's exponent range; no scaling is involved), and errors are loud."""
