@@ -8,31 +8,39 @@ backend ``nccl``):
   ≈E/world in-edges each (prefix sum of in-degree).  Rank p owns rows [r_p, r_{p+1}): their
   features X, Q, S, Y, the in-edges into them (so S needs no reduction) and dX.
 * **Halo layout.** A message u→v needs K[u].  Rank p's *halo* is the set of remote sources of its
-  in-edges.  Each owner's block of it (the rows rank p requests from that owner, ascending id) is cut
-  into ``chunks`` equal parts, and the halo is stored CHUNK-MAJOR: ``K_ext = [own rows | chunk 0 |
-  chunk 1 | ...]``, each chunk holding its part of every owner's block in owner order.  Edge
-  columns are remapped once, at plan time, to positions in ``K_ext``, so the single-GPU kernels run
-  on it unchanged.
-* **Forward: a pipelined exchange.**  K is projected for the own rows, and the halo arrives as
-  ``chunks`` sparse all-to-alls (RCCL alltoallv over the xGMI mesh: every chunk moves 1/chunks of
-  the rows of EVERY peer, so each one uses all links at once), all queued at once on RCCL's stream.
-  The edges of each destination row are stored in segments by source — own sources and halo chunk
-  0 first, then the edges whose halo row is in chunk 1, 2, ... — and the edge pass runs segment by
-  segment as the chunks land (``SIR_AGG_ACCUMULATE``: S[v] += the segment's sum); chunk 0 lands
-  under the Q GEMM and the packing of the later chunks.  Every row sums its segments in the same
-  fixed order, so the result is deterministic (not bit-identical to one GPU, whose rows sum in edge
-  id order: tests hold it to the parity bar).  On the power-law S2 graph the halo is 1.15 M rows per
-  rank at 8 ranks against the 1.77 M a dense all-gather moves.
+  in-edges.  Every owner's row range is cut into ``chunks`` parts (``part_bounds``), and a halo row
+  belongs to chunk c when it lies in part c of its owner's range; the halo is stored CHUNK-MAJOR:
+  ``K_ext = [own rows | chunk 0 | chunk 1 | ...]``, each chunk holding its part of every owner's
+  block in owner order.  Edge columns are remapped once, at plan time, to positions in ``K_ext``,
+  so the single-GPU kernels run on it unchanged.
+* **Forward: a pipelined exchange.**  K is projected part by part of the own range, and chunk c
+  (the rows of part c that peers need) is packed and sent as soon as part c exists — ``chunks``
+  sparse all-to-alls (RCCL alltoallv over the xGMI mesh: every chunk moves rows to EVERY peer, so
+  each one uses all links at once).  The edges of each destination row are stored in segments by
+  source — own sources and halo chunk 0 first, then the edges whose halo row is in chunk 1, 2, ...
+  — and the edge pass runs segment by segment as the chunks land (``SIR_AGG_ACCUMULATE``: S[v] +=
+  the segment's sum); the Q GEMM runs under the first chunk.  Every row sums its segments in the
+  same fixed order, so the result is deterministic (not bit-identical to one GPU, whose rows sum in
+  edge id order: tests hold it to the parity bar).  On the power-law S2 graph the halo is 1.15 M
+  rows per rank at 8 ranks against the 1.77 M a dense all-gather moves.
 * **Backward: the transpose, also pipelined.**  The dK pass runs first over the HALO rows of
   ``K_ext``, chunk by chunk, each chunk's partial dK sent back to its owners (reverse alltoallv) as
-  soon as it is computed; the dQ pass and the dK pass over the own rows (one launch, as on one GPU),
-  the dW_R / dX_Q / dW_Q GEMMs then run under the exchange.  Received rows are added per chunk and
-  peer in a fixed order (deterministic; no reduce-scatter of a dense [V, H] buffer).
-* **Weight gradients**: one all-reduce of a flat buffer (``allreduce_grads``).
+  soon as it is computed; the dQ pass and the dK pass over the own rows (one launch, as on one GPU)
+  and the dW_R / dW_Q GEMMs run under the exchange.  Reverse chunk c carries only rows of the
+  owner's part c, so part c's dK is completed (one gather-based segment sum over [own partial |
+  received rows], fixed order, no atomics) as soon as chunk c lands, and its dX rows follow at once
+  as ONE K = 2H GEMM on [dQ | dK] against [W_Q; W_K] (with dW_K's partial over the part).
+* **Weight gradients**: reduced inside the backward with ``reduce_in_backward=True`` — dW_R / db_R
+  and dW_Q / db_Q start their all-reduce under the exchange, dW_K after the last part — else one
+  all-reduce of a flat buffer (``allreduce_grads``).
 * **Feature dropout** (``conv.py:35,60-61``, training with p > 0): Q and K draw hashed masks from
-  two device seeds in the GEMM epilogues.  The backward edge passes run without it and the owner
-  applies the masks to its own dQ / dK rows once complete (``sir_dropout_apply``): a halo row's dK
-  partial is summed over ranks before the mask of its owner can apply.
+  two device seeds in the GEMM epilogues, hashed with the GLOBAL row index (independent masks per
+  rank).  The backward edge passes run without it and the owner applies the masks to its own dQ /
+  dK rows once complete (``sir_dropout_apply``): a halo row's dK partial is summed over ranks
+  before the mask of its owner can apply.
+* **agg_type='max'** (``conv.py:46-47``): the halo K rows are gathered by the same chunked
+  exchange (``HaloGather``, its backward the reverse exchange) and the fused max layer
+  (``edgemlp.EdgeMaxLinearQK``) runs on [own | halo] rows.
 * **Autocast** (``DistSIRConvFunction16``): 16-bit K_ext rows, edge passes and both exchanges in
   the 16-bit type — half the wire bytes.
 * ``sym`` needs GLOBAL out-degrees: own-row out-degree histograms are completed by the same reverse
