@@ -264,25 +264,30 @@ __device__ inline uint32_t pack2(float a, float b, bool bf) {
            ((uint32_t)__builtin_bit_cast(unsigned short, (_Float16)b) << 16);
 }
 
-template <bool BF, bool A32, bool C32, int KC, int NC, int NS>
+template <bool BF, bool A32, bool C32, int KC, int NC, int NS, int BFT = 256>
 __global__ void __launch_bounds__(512)
 k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __restrict__ Wp, int Npad,
             const float* __restrict__ bias, int N, void* __restrict__ C, int64_t ldc, unsigned short* __restrict__ Acopy,
             int64_t ldac, int n_ftiles, int n_tiles, int tiles_per_block, Drop drop) {
     drop = drop_resolve(drop);
-    constexpr int BD = 256, BFT = 256, WF = 4, TDT = 4, TFT = 2;
+    // BFT features per tile: 256, or 128 for the narrow outputs of H <= 128 layers (config 2's Y, G
+    // and dX), where the 256-wide tile spent half its MFMAs and weight loads past N
+    constexpr int BD = 256, TFT = 2, WF = BFT / (TFT * 32), WD = 8 / WF, TDT = BD / (WD * 32);
     constexpr int KS = KC / 16;                       // k16 planes per chunk
-    constexpr int PLANE = 256 * 32;                   // one k16 plane of 256 rows
-    constexpr int STAGE = 2 * KS * PLANE;             // A planes, then W planes
+    constexpr int PLANE = 256 * 32;                   // one k16 plane of the 256 data rows
+    constexpr int PLANE_W = BFT * 32;                 // one k16 plane of the tile's weight rows
+    constexpr int STAGE = KS * (PLANE + PLANE_W);     // A planes, then W planes
     constexpr int EA = A32 ? 4 : 2;                   // bytes per A element
     constexpr int AV = (KC / 2) * EA / 16;            // u4v A loads per thread and chunk
-    constexpr int WV = KS * PLANE * 1 / (16 * 512);   // u4v W pieces per thread and chunk
+    constexpr int WV = KS * PLANE_W / (16 * 512);     // u4v W pieces per thread and chunk
     constexpr int EC = C32 ? 4 : 2;
     static_assert(KC == 32 || KC == 64, "chunk");
+    static_assert(BFT == 256 || BFT == 128, "feature tile");
     static_assert(WV >= 1, "weight loader");
     static_assert(NS >= 2 && NS <= NC && NC % NS == 0, "register sets: a tile's chunks map to sets the same way");
+    constexpr int IMG_ROWS = 32 * WD;                 // epilogue image: one 32-row band per data wave
     constexpr int EPITCH = BFT * EC + 16;             // epilogue image row pitch (bytes)
-    constexpr int EPI_BYTES = SIR_NT16_EPI ? 64 * EPITCH : 0;
+    constexpr int EPI_BYTES = SIR_NT16_EPI ? IMG_ROWS * EPITCH : 0;
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE + 512 * 4 + EPI_BYTES];
     float* const bias_l = reinterpret_cast<float*>(lds + 2 * STAGE);
     char* const epi = lds + 2 * STAGE + 512 * 4;
@@ -327,7 +332,8 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
         for (int i = 0; i < AV; ++i) av[set][i] = __builtin_amdgcn_raw_buffer_load_b128(p.a, aoff + 16 * i, c * KC * EA, 0);
 #pragma unroll
         for (int i = 0; i < WV; ++i)
-            wv[set][i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, ((i * 512 + t) >> 9) * Npad * 32 + ((i * 512 + t) & 511) * 16,
+            wv[set][i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, ((i * 512 + t) / (PLANE_W / 16)) * Npad * 32 +
+                                                                         ((i * 512 + t) % (PLANE_W / 16)) * 16,
                                                               (c * KS * Npad + p.f0) * 32, 0);
     };
     auto store = [&](int set, int buf, const TileP& p, int c) {
@@ -354,7 +360,7 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
         for (int i = 0; i < KC / 16; ++i)
             *reinterpret_cast<u4v*>(st + (kh * (KS / 2) + (i >> 1)) * PLANE + fimg(rho, i & 1)) = q[i];
 #pragma unroll
-        for (int i = 0; i < WV; ++i) *reinterpret_cast<u4v*>(st + KS * PLANE + (i * 512 + t) * 16) = wv[set][i];
+        for (int i = 0; i < WV; ++i) *reinterpret_cast<u4v*>(st + KS * PLANE + (i * 512 + t) * 16) = wv[set][i];   // W planes
     };
 
     f16v acc[TFT][TDT];
@@ -366,7 +372,7 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
             u4v wf[TFT], df[TDT];
 #pragma unroll
             for (int a = 0; a < TFT; ++a)
-                wf[a] = *reinterpret_cast<const u4v*>(st + (KS + ks) * PLANE + fimg(f_w + 32 * a + r, h));
+                wf[a] = *reinterpret_cast<const u4v*>(st + KS * PLANE + ks * PLANE_W + fimg(f_w + 32 * a + r, h));
 #pragma unroll
             for (int b = 0; b < TDT; ++b)
                 df[b] = *reinterpret_cast<const u4v*>(st + ks * PLANE + fimg(d_w + 32 * b + r, h));
@@ -443,7 +449,7 @@ k_gemm_nt16(const void* __restrict__ A, int64_t lda, int64_t M, const u4v* __res
             __syncthreads();
             constexpr int PR = BFT * EC / 16;                 // 16-B pieces per image row
 #pragma unroll
-            for (int i = 0; i < 64 * PR / 512; ++i) {
+            for (int i = 0; i < IMG_ROWS * PR / 512; ++i) {
                 const int q = tq + 512 * i;
                 const int ir = q / PR, c16 = q % PR;
                 const u4v v = *reinterpret_cast<const u4v*>(epi + ir * EPITCH + c16 * 16);
@@ -647,10 +653,13 @@ hipError_t run_gemm_pack16(const float* W, int64_t ldw, int N, int K, int trans,
 #define SIR_NT16_NS32 2         // the same for an fp32 A
 #endif
 
-template <bool BF, bool A32, bool C32>
-static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, const void* packed, int N, const float* bias,
-                              void* C, int64_t ldc, unsigned short* Acopy, int64_t ldac, hipStream_t st, const Drop& drop) {
-    const int np = (N + 255) / 256 * 256, nft = np / 256;
+#ifndef SIR_NT16_NARROW
+#define SIR_NT16_NARROW 1       // 128-feature tiles for N <= 128 (env SIR_NT16_NARROW=0: always 256)
+#endif
+template <bool BF, bool A32, bool C32, int BFT>
+static hipError_t launch_nt16_w(const void* A, int64_t lda, int64_t M, int K, const void* packed, int N, const float* bias,
+                                void* C, int64_t ldc, unsigned short* Acopy, int64_t ldac, hipStream_t st, const Drop& drop) {
+    const int np = (N + 255) / 256 * 256, nft = (N + BFT - 1) / BFT;
     const int64_t ntiles = (M + 255) / 256 * nft;
     const int ncu = device_cu_count();
     const int tpb = (int)((ntiles + ncu - 1) / ncu);
@@ -659,15 +668,25 @@ static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, cons
     constexpr int KC = (SIR_NT16_KC == 64 && !A32) ? 64 : 32;
     constexpr int NS = A32 ? SIR_NT16_NS32 : SIR_NT16_NS;
     const int nc = K / KC;
-#define SIR_NT16_L(NCV, NSV)                                                                                           \
-    hipLaunchKernelGGL((k_gemm_nt16<BF, A32, C32, KC, NCV, NSV>), dim3((unsigned)nblk), dim3(512), 0, st, A, lda, M, wp, \
-                       np, bias, N, C, ldc, Acopy, ldac, nft, (int)ntiles, tpb, drop)
+#define SIR_NT16_L(NCV, NSV)                                                                                   \
+    hipLaunchKernelGGL((k_gemm_nt16<BF, A32, C32, KC, NCV, NSV, BFT>), dim3((unsigned)nblk), dim3(512), 0, st, A, lda, \
+                       M, wp, np, bias, N, C, ldc, Acopy, ldac, nft, (int)ntiles, tpb, drop)
     if (nc == 256 / KC) SIR_NT16_L(256 / KC, (NS <= 256 / KC ? NS : 256 / KC));
     else if (nc == 512 / KC) SIR_NT16_L(512 / KC, NS);
     else if (nc == 128 / KC) SIR_NT16_L(128 / KC, (NS <= 128 / KC ? NS : 128 / KC));
     else return hipErrorInvalidValue;
 #undef SIR_NT16_L
     return hipGetLastError();
+}
+
+template <bool BF, bool A32, bool C32>
+static hipError_t launch_nt16(const void* A, int64_t lda, int64_t M, int K, const void* packed, int N, const float* bias,
+                              void* C, int64_t ldc, unsigned short* Acopy, int64_t ldac, hipStream_t st, const Drop& drop) {
+    const char* e = getenv("SIR_NT16_NARROW");
+    const int narrow = (e != nullptr && e[0] != 0) ? atoi(e) : SIR_NT16_NARROW;
+    if (narrow && N <= 128)
+        return launch_nt16_w<BF, A32, C32, 128>(A, lda, M, K, packed, N, bias, C, ldc, Acopy, ldac, st, drop);
+    return launch_nt16_w<BF, A32, C32, 256>(A, lda, M, K, packed, N, bias, C, ldc, Acopy, ldac, st, drop);
 }
 
 hipError_t run_gemm_nt16(const void* A, int64_t lda, int a_dtype, int64_t M, int K, const void* packed, int N, int dtype,

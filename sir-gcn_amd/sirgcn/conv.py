@@ -351,6 +351,9 @@ class SIRConv(nn.Module):
         self.linear_relation = nn.Linear(hidden_dim, output_dim, bias=outer_bias)
         self._agg_type = agg_type
         self.chunk = DEFAULT_CHUNK
+        # a one-element device seed handed in by a caller that drew the seeds of several layers in
+        # one op (sirgcn.stacks.SIRStack), consumed by the next forward's _drop
+        self.step_seed = None
 
     def _drop(self, device):
         """(seed, p) of this forward's fused feature dropout (conv.py:35,60-61), or None (eval / p = 0).
@@ -359,8 +362,12 @@ class SIRConv(nn.Module):
         host sync, the CPU RNG stream is untouched, and a forward captured in a HIP graph draws a
         fresh mask on every replay (the captured randint is graph-safe philox)."""
         if not (self.training and self.dropout.p > 0):
+            self.step_seed = None
             return None
-        return torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64), float(self.dropout.p)
+        seed, self.step_seed = self.step_seed, None
+        if seed is None or seed.device != torch.device(device):
+            seed = torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
+        return seed, float(self.dropout.p)
 
     def _linear(self, x, W, b):
         """nn.Linear on the native GEMMs (``linalg.linear``; torch's F.linear when disabled or for
@@ -394,6 +401,12 @@ class SIRConv(nn.Module):
         return QK
 
     def forward(self, graph, feat):
+        try:
+            return self._forward(graph, feat)
+        finally:
+            self.step_seed = None          # a handed-in seed serves this one forward, whatever route ran
+
+    def _forward(self, graph, feat):
         if isinstance(feat, tuple):          # expand_as_pair: (src feats, dst feats)
             feat_key, feat_query = feat
         else:

@@ -660,8 +660,11 @@ class DistSIRConvFunction16(torch.autograd.Function):
     the single-GPU ``SIRConvFunction16`` dataflow per rank — 16-bit projections on the native
     16-bit MFMA GEMMs (X.to(dt) fused into the first one), 16-bit ``K_ext`` rows and edge passes
     (fp32 math inside) — with both pipelined halo exchanges in the 16-bit storage type: half the
-    xGMI bytes of the fp32 layer.  The received dK rows are added in that type (one more rounding
-    per peer than the single-GPU sum; within the AMP tolerance)."""
+    xGMI bytes of the fp32 layer.  Two roundings more than the single-GPU autocast layer, both within
+    the AMP tolerance and pinned by ``tests/test_dist_gpu.py::test_autocast_edge_cut_16bit_wire``
+    (default 4 chunks, sum / sym / mean): S is accumulated segment by segment in the 16-bit storage
+    type (one rounding per halo chunk; ``mean`` divides the rounded sum), and the received dK rows
+    are added in that type (one more rounding per peer)."""
 
     @staticmethod
     def forward(ctx, X, W_Q, b_Q, W_K, W_R, b_R, dg, agg, act, slope, backend, use_mask, grad_on, dt, drop=None,

@@ -44,6 +44,15 @@ class SIRStack(nn.Module):
         self.norms = nn.ModuleList([norm_cls(hidden) for _ in range(num_layers)]) if norm_cls else None
 
     def forward(self, graph, feats):
+        if self.training and getattr(feats, "is_cuda", False):
+            # the dropout seeds of every layer in ONE device draw (sirgcn SIRConv's step_seed): one
+            # RNG launch per step instead of one per layer (small batches are launch-bound)
+            drawing = [c for c in self.convs if hasattr(c, "step_seed") and c.dropout.p > 0]
+            if drawing:
+                import torch
+                seeds = torch.randint(0, 2 ** 62, (len(drawing),), device=feats.device, dtype=torch.int64)
+                for j, c in enumerate(drawing):
+                    c.step_seed = seeds[j:j + 1]
         for i, conv in enumerate(self.convs):
             if self.order == "plain":
                 feats = conv(graph, feats)

@@ -229,6 +229,31 @@ def _nt16_ref(A, W, bias, dt, trans):
     return ref
 
 
+@pytest.mark.parametrize("M,K,N", [(229532, 128, 128), (70001, 256, 128), (4133, 512, 96), (300, 128, 8)])
+@pytest.mark.parametrize("a32,c32", [(False, False), (True, False), (False, True)])
+def test_gemm_nt16_narrow_tiles_bit_identical(M, K, N, a32, c32, monkeypatch):
+    """The 128-feature-tile NT16 kernel (taken for N <= 128: config 2's Y, G and dX) computes every
+    output with the same chunks, MFMAs and epilogue as the 256-wide one: bit-identical (16-bit and
+    fp32 outputs, the rounded A copy, bias, the dropout epilogue)."""
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(M + K + N)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    if not a32:
+        A = A.to(dt)
+    W = torch.randn(N, K, device=DEV, generator=g) * K ** -0.5
+    b = torch.randn(N, device=DEV, generator=g).to(dt).float()
+    pk = _native.gemm_pack16(W, dt)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SIR_NT16_NARROW", v)
+        acopy = torch.full((M, K), 7.0, device=DEV, dtype=dt) if a32 else None
+        C = _native.gemm_nt16(A, pk, b, torch.float32 if c32 else None, acopy, drop=(3, 0.25))
+        out[v] = (C, acopy)
+    assert torch.equal(out["1"][0], out["0"][0])
+    if a32:
+        assert torch.equal(out["1"][1], out["0"][1])
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("a32", [False, True])
 @pytest.mark.parametrize("M,K,N,trans,with_bias", [(4133, 256, 512, False, True), (2000, 256, 256, False, True),

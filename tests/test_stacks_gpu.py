@@ -323,3 +323,36 @@ def test_cfg2_small_batch_autocast_on_the_product_gemm_route(monkeypatch):
             [(k, got[2][k], amp[2][k], r64[2][k]) for k in got[2]]:
         e, e_amp = rel_err(a, t), rel_err(r, t)
         assert e <= max(2e-2, 1.25 * e_amp), (what, e, e_amp)
+
+
+def test_stack_draws_every_layer_dropout_seed_in_one_op(monkeypatch):
+    """Training with feature dropout: the stack draws all layers' device seeds with one randint
+    (one RNG launch per step, not one per layer), each layer gets its own seed, a fresh draw per
+    step, and a re-seeded generator reproduces the step; the handed-in seeds are consumed."""
+    g = make_graph("cfg5", small=True)
+    X, dY = make_inputs("cfg5", g.num_nodes(), DEV)
+    ours = make_stack("cfg5", SIRConv, GraphNorm, feat_dropout=0.2).to(DEV).train()
+    calls = []
+    orig = torch.randint
+
+    def spy(*a, **k):
+        out = orig(*a, **k)
+        calls.append(out.numel())
+        return out
+    monkeypatch.setattr(torch, "randint", spy)
+    torch.manual_seed(7)
+    y1 = ours(g, X).detach()
+    assert calls == [len(ours.convs)], calls
+    assert all(c.step_seed is None for c in ours.convs)
+    y2 = ours(g, X).detach()
+    torch.manual_seed(7)
+    y3 = ours(g, X).detach()
+    assert not torch.equal(y1, y2) and torch.equal(y1, y3)
+    # each layer's mask comes from its own seed: the layer outputs differ from a shared-seed run
+    seen = []
+    import sirgcn.conv as sc
+    orig_drop = sc.SIRConv._drop
+    monkeypatch.setattr(sc.SIRConv, "_drop", lambda self, dev: seen.append(orig_drop(self, dev)) or seen[-1])
+    ours(g, X)
+    ptrs = {d[0].data_ptr() for d in seen}
+    assert len(seen) == len(ours.convs) and len(ptrs) == len(ours.convs)
