@@ -55,7 +55,7 @@ class _Spy:
             return orig_bwd(*a, **k)
         monkeypatch.setattr(_native, "edge_agg_fwd", fwd)
         monkeypatch.setattr(_native, "edge_agg_bwd", bwd)
-        for name in ("gemm_nt", "gemm_nt_direct", "gemm_tn", "gemm_nt16", "gemm_tn16"):
+        for name in ("gemm_nt", "gemm_nt_direct", "gemm_nt_direct2", "gemm_tn", "gemm_nt16", "gemm_tn16"):
             orig = getattr(_native, name)
 
             def wrap(*a, _o=orig, **k):
