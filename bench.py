@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--agg", default="sum", choices=["sum", "mean", "sym", "max"],
                     help="max: the fused per-edge W_R + running max (sirgcn.edgemlp), an MFMA-bound kernel")
+    ap.add_argument("--max-bwd", default="materialised", choices=["materialised", "routed"],
+                    help="agg max: the edge-materialised backward (default) or the routed one (no [E, *] buffer, "
+                         "sirgcn.edgemlp.EdgeMaxLinear.sparse_bwd)")
     ap.add_argument("--dtype", default=None, choices=["f32", "bf16", "f16"],
                     help="feature dtype (16-bit = the autocast path); default f32 (cfg2: bf16)")
     ap.add_argument("--chunk", type=int, default=None)
@@ -343,6 +346,9 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
     torch.manual_seed(4)
     p_drop = args.dropout or 0.0
     conv = SIRConv(H, H, H, nn.LeakyReLU(0.2, inplace=True), p_drop, agg_type=args.agg).to(dev)
+    if args.agg == "max" and args.max_bwd == "routed":
+        from sirgcn.edgemlp import EdgeMaxLinear
+        EdgeMaxLinear.sparse_bwd = True
     if args.chunk:
         conv.chunk = args.chunk
     X_full = torch.randn(V, H, generator=torch.Generator().manual_seed(3))
@@ -402,7 +408,7 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
            "config": {"workload": f"cfg4 {args.graph}: Chung-Lu power-law V={V} E={E} alpha={alpha}; 1 SIRConv layer "
                                   f"d_in=H=d_out={H}, agg={args.agg}, LeakyReLU(0.2), {dtn}, feat_dropout={p_drop}"
                                   f"{' (autocast)' if dtn != 'f32' else ''}; fwd+bwd incl. projections",
-                      "graph": args.graph, "V": V, "E": E, "hidden": H, "agg": args.agg,
+                      "graph": args.graph, "V": V, "E": E, "hidden": H, "agg": args.agg, **({"max_bwd": args.max_bwd} if args.agg == "max" else {}),
                       "parallelism": f"edge-cut dst-range x{world}, pipelined sparse halo all-to-alls" if world > 1
                       else "single GPU"}}
     if rehearsal:

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 13
+#define SIR_ABI_VERSION 14
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57).  SIR_AGG_ACCUMULATE,
  * OR'd into the forward's `agg` (SUM / SYM): S[v] = S[v] + the sum over the given items' edges, rows
@@ -335,6 +335,27 @@ int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
                          int64_t H, int64_t O, const float* K, int64_t ldk, const float* Q, int64_t ldq,
                          const float* dY, int64_t ldy, const int32_t* arg, int64_t lda, int act1, float slope,
                          const float* W, float* dK, int64_t lddk, float* partial, void* stream);
+
+/* agg_type='max' backward from the arg-max routing alone (conv.py:46-47; ABI 14): dY[v][o] reaches only
+ * the first arg-max edge arg[v][o] (a dst-CSR position in [rowptr[v], rowptr[v+1]), else none), so
+ *   dA_e = sum_{o : arg[v][o] = e} dY[v][o] W[o, :],  dz_e = act1'(Q[v] + K[u]) dA_e,
+ *   dQ[v] = sum_e dz_e (dst CSR),  dK[u] = sum_e dz_e (src CSR),
+ *   dW[o, :] = sum_v dY[v][o] act1(Q[v] + K[col[arg[v][o]]]),  db[o] = sum_v dY[v][o]
+ * with V * O * H multiply-adds per product (not E * O * H) and no [E, H] / [E, O] buffer.  Workspace:
+ * ent = 8 * V * O bytes (V * O < 2^31), ecnt_d / ecnt_s = 8 * E bytes each, partial = max(n_slots) * H
+ * floats, dbpart = route_blocks * O4 floats (O4 = O rounded up to 4) and wpart = dw_ranges * O * H floats (the sizes from
+ * sir_edge_max_bwd_sparse_parts; sum each over its rows in row order for db / dW, e.g. sir_col_sum).
+ * pinv[dst-CSR position] = src-CSR position (the inverse of the source CSR's perm).  H % 4 == 0,
+ * H <= 512, O <= 256, Q / K / W rows 16-B aligned.  Deterministic (no atomics). */
+int sir_edge_max_bwd_sparse_parts(int64_t n_items_d, int64_t V, int64_t* route_blocks, int64_t* dw_ranges);
+int sir_edge_max_bwd_sparse(const int32_t* rowptr_d, const int32_t* col_d, const int32_t* items_d, int64_t n_items_d,
+                            const int32_t* splits_d, int64_t n_splits_d, const int32_t* col_s,
+                            const int32_t* items_s, int64_t n_items_s, const int32_t* splits_s, int64_t n_splits_s,
+                            const int32_t* pinv, int64_t V, int64_t E, int64_t H, int64_t O,
+                            const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* dY, int64_t ldy,
+                            const int32_t* arg, int64_t lda, int act1, float slope, const float* W,
+                            float* dQ, int64_t lddq, float* dK, int64_t lddk, float* partial, void* ent,
+                            void* ecnt_d, void* ecnt_s, float* dbpart, float* wpart, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * GraphNorm (models/norm.py:7-29) on a batched graph: graph b owns node rows [off[b], off[b+1])

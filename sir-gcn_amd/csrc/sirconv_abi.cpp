@@ -524,6 +524,61 @@ int sir_edge_max_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_
                   nullptr);
 }
 
+static int64_t maxb_route_blocks(int64_t n_items) {
+    const int64_t b = (n_items + 3) / 4;
+    return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+}
+
+int sir_edge_max_bwd_sparse_parts(int64_t n_items_d, int64_t V, int64_t* route_blocks, int64_t* dw_ranges) {
+    const char* fn = "sir_edge_max_bwd_sparse_parts";
+    if (route_blocks == nullptr || dw_ranges == nullptr || n_items_d < 0 || V < 0)
+        return fail(SIR_EINVAL, fn, "bad argument");
+    *route_blocks = maxb_route_blocks(n_items_d);
+    *dw_ranges = sir::maxb_dw_ranges(V);
+    return SIR_OK;
+}
+
+int sir_edge_max_bwd_sparse(const int32_t* rowptr_d, const int32_t* col_d, const int32_t* items_d, int64_t n_items_d,
+                            const int32_t* splits_d, int64_t n_splits_d, const int32_t* col_s,
+                            const int32_t* items_s, int64_t n_items_s, const int32_t* splits_s, int64_t n_splits_s,
+                            const int32_t* pinv, int64_t V, int64_t E, int64_t H, int64_t O,
+                            const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* dY, int64_t ldy,
+                            const int32_t* arg, int64_t lda, int act1, float slope, const float* W,
+                            float* dQ, int64_t lddq, float* dK, int64_t lddk, float* partial, void* ent,
+                            void* ecnt_d, void* ecnt_s, float* dbpart, float* wpart, void* stream) {
+    const char* fn = "sir_edge_max_bwd_sparse";
+    if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
+    if (H <= 0 || H % 4 != 0 || H > 512 || O <= 0 || O > 256)
+        return fail(SIR_EUNSUPPORTED, fn, "H % 4 == 0, H <= 512, O <= 256");
+    if (V < 0 || E < 0 || n_items_d < 0 || n_items_s < 0 || n_splits_d < 0 || n_splits_s < 0 ||
+        n_items_d > INT32_MAX || n_items_s > INT32_MAX || E > INT32_MAX)
+        return fail(SIR_EINVAL, fn, "bad size");
+    if (V * O >= (int64_t)INT32_MAX) return fail(SIR_EUNSUPPORTED, fn, "V * O must be < 2^31");
+    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || lddq < H || lddk < H || lddq % 4 || lddk % 4 || !al16(Q) ||
+        !al16(K) || !al16(W) || !al16(dQ) || !al16(dK))
+        return fail(SIR_EUNSUPPORTED, fn, "Q / K / W / dQ / dK rows must be 16-B aligned (ld % 4 == 0, ld >= H)");
+    if (V > 0 && (rowptr_d == nullptr || items_d == nullptr || Q == nullptr || dY == nullptr || ldy < O ||
+                  arg == nullptr || lda < O || W == nullptr || dQ == nullptr || dbpart == nullptr ||
+                  wpart == nullptr || ent == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer / leading dimension");
+    if (E > 0 && (col_d == nullptr || col_s == nullptr || items_s == nullptr || pinv == nullptr || K == nullptr ||
+                  dK == nullptr || ecnt_d == nullptr || ecnt_s == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL edge buffer");
+    if ((n_splits_d > 0 && splits_d == nullptr) || (n_splits_s > 0 && splits_s == nullptr) ||
+        ((n_splits_d > 0 || n_splits_s > 0) && partial == nullptr))
+        return fail(SIR_EINVAL, fn, "split rows need partial");
+    sir::MaxBwdArgs a{};
+    a.rowptr_d = rowptr_d; a.col_d = col_d; a.items_d = items_d; a.n_items_d = n_items_d;
+    a.splits_d = splits_d; a.n_splits_d = n_splits_d;
+    a.col_s = col_s; a.items_s = items_s; a.n_items_s = n_items_s; a.splits_s = splits_s; a.n_splits_s = n_splits_s;
+    a.pinv = pinv; a.H = (int)H; a.O = (int)O; a.V = V;
+    a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.dY = dY; a.ldy = ldy; a.arg = arg; a.lda = lda;
+    a.act1 = act1; a.slope = slope; a.W = W; a.dQ = dQ; a.lddq = lddq; a.dK = dK; a.lddk = lddk;
+    a.partial = partial; a.ent = ent; a.ecnt_d = ecnt_d; a.ecnt_s = ecnt_s; a.dbpart = dbpart;
+    a.route_blocks = maxb_route_blocks(n_items_d); a.wpart = wpart;
+    return finish(fn, sir::run_max_bwd_sparse(a, static_cast<hipStream_t>(stream)), nullptr);
+}
+
 int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
                          const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
                          int64_t H, int64_t O, const float* K, int64_t ldk, const float* Q, int64_t ldq,

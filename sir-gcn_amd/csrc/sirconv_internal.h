@@ -156,6 +156,26 @@ hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStr
 int mlp_bwd_blocks(int64_t n_items, int H, int F);
 hipError_t run_mlp_bwd(const EdgeMlpArgs& a, bool dst, int red, int act1, int act2, hipStream_t st);
 
+// agg_type='max' backward from the arg-max routing (sirconv_maxbwd.hip): no [E, *] tensor
+struct MaxBwdArgs {
+    const int* rowptr_d; const int* col_d; const int32_t* items_d; int64_t n_items_d;
+    const int32_t* splits_d; int64_t n_splits_d;
+    const int* col_s; const int32_t* items_s; int64_t n_items_s; const int32_t* splits_s; int64_t n_splits_s;
+    const int* pinv;                    // dst-CSR position -> src-CSR position
+    int H, O; int64_t V;                // V = destination rows
+    const float* Q; int64_t ldq; const float* K; int64_t ldk;
+    const float* dY; int64_t ldy; const int* arg; int64_t lda;
+    int act1; float slope; const float* W;
+    float* dQ; int64_t lddq; float* dK; int64_t lddk;
+    float* partial;                     // split rows: max(n_slots) * H
+    void* ent;                          // int2 [V * O]
+    void* ecnt_d; void* ecnt_s;         // int2 [E] each
+    float* dbpart; int64_t route_blocks;   // [route_blocks, O]
+    float* wpart;                       // [maxb_dw_ranges(V), O, H]
+};
+int64_t maxb_dw_ranges(int64_t V);
+hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st);
+
 // projection GEMMs, sirconv_gemm.hip
 int64_t gemm_pack_bytes(int64_t N, int64_t K);
 hipError_t run_gemm_pack(const float* W, int64_t ldw, int N, int K, int trans, void* packed, hipStream_t st);

@@ -6,11 +6,13 @@ whose message runs a Linear on every edge, without any [E, *] tensor in the forw
   H, F <= 256 (the config-1 shape is H = F = 64; the DictionaryLookup sweep reaches H = F = 200,
   ``dictionary-lookup/README.md:8``).
 * ``agg_type='max'`` (``conv.py:46-47``: ``linear_relation`` per edge, DGL ``fn.max``):
-  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge) and two
-  backwards: fused for H, O <= 256 (``sir_edge_max_bwd_*``: dY routed to the arg edges, z and a
-  recomputed per edge, dW_R / db_R per-block partials — no [E, *] tensor), taken when the
-  edge-materialised one (edge activations recomputed once into [E, H] buffers, native gather /
-  split-fp16 GEMM / segment kernels — faster) would not fit its memory budget.
+  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge) and three
+  backwards: the edge-materialised one by default (edge activations recomputed once into [E, H]
+  buffers, native gather / split-fp16 GEMM / segment kernels, over destination-row ranges past a memory
+  budget); the routed one (``sir_edge_max_bwd_sparse``, H <= 512, O <= 256, opt-in ``sparse_bwd``: the
+  (v, o) pairs grouped by their arg edge, dA_e from the W_R rows of e's routed outputs only, dW_R from
+  a_{arg} per (v, o) — V O H multiply-adds per product instead of E O H, no [E, *] tensor); the dense
+  fused one (fp32 MFMA, opt-in ``fused_bwd``).
 
 Everything is fp32, under autocast too: there the reference runs the per-edge Linear (and sigma)
 in 16 bits, these kernels take Q, K widened to fp32 and return the result cast back to QK's dtype —
@@ -182,14 +184,19 @@ class EdgeMLPSum(torch.autograd.Function):
 class EdgeMaxLinear(torch.autograd.Function):
     """Y[v] = max_e (W_R act1(Q[v] + K[u]) + b_R), first arg-max edge (DGL fn.max), empty rows 0.
 
-    Backward route (``fused_bwd``): ``None`` (default) — the edge-materialised backward (z recomputed
-    once into [E, H], dM [E, O]; its GEMMs on the split-fp16 MFMA kernels), over the whole graph when its
-    buffers, E (2H + O) 4 bytes, stay within ``materialised_budget`` (48 GiB, and 40 % of the free device
-    memory), else over destination-row ranges that each fit it (the S2 shape, 123 GB of buffers: 4
-    ranges; r05: 710 -> see DESIGN §8 ms per S2 step against the fused route); ``True`` — the fused
+    Backward route (``fused_bwd``): ``None`` (default) — with ``sparse_bwd`` the routed backward
+    (``max_bwd_sparse``: H % 4 == 0, H <= 512, O <= 256; no [E, *] buffer, V O H multiply-adds per product),
+    else the edge-materialised one (z recomputed once into [E, H], dM [E, O]; its GEMMs on the split-fp16
+    MFMA kernels), over the whole
+    graph when its buffers, E (2H + O) 4 bytes, stay within ``materialised_budget`` (48 GiB, and 40 % of
+    the free device memory), else over destination-row ranges that each fit it; ``True`` — the fused
     backward (no [E, *] buffer; its three edge-contracted products on fp32 MFMA, 14x slower at S2);
     ``False`` — the materialised one (tests)."""
     fused_bwd = None
+    # True: the routed backward (no [E, *] buffer) for H % 4 == 0, H <= 512, O <= 256 when fused_bwd is None.
+    # Off by default: its dW_R pass (a_{arg} gathered per (v, o), L1-bound) makes it slower than the
+    # edge-materialised route at S1 / S2 (36.0 vs 30.4 ms S1 max step, 138 vs 120 ms S2 max; DESIGN §4)
+    sparse_bwd = False
     materialised_budget = 48 << 30
 
     @staticmethod
@@ -258,6 +265,8 @@ def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
     fused = EdgeMaxLinear.fused_bwd
     if fused and max_bwd_fused(H, O):
         return _max_bwd_fused(plan, Q, K, W, arg, dY, H, act1, slope, dQ, dK)
+    if fused is None and EdgeMaxLinear.sparse_bwd and max_bwd_sparse(H, O, plan.dst.n_rows):
+        return _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK)
     per_edge = (2 * H + O) * 4
     # free device memory as the caching allocator sees it: the driver's free bytes plus the blocks it
     # has reserved but not handed out (a warm training loop holds most memory there)
@@ -360,6 +369,55 @@ def _max_bwd_materialised(dcsr, scsr, Q, K, W, arg, dY, act1, slope, dQ, dK):
     part = torch.empty((max(n_slots, 1) * H,), device=dev, dtype=torch.float32) if n_slots else None
     _native.segment_sum(dcsr, dZ, dQ, partial=part)                     # dQ
     _native.segment_sum(scsr, dZ, dK, perm=scsr.perm, partial=part)     # dK
+    return dW, db
+
+
+def max_bwd_sparse(H, O, V):
+    """The routed backward (``sir_edge_max_bwd_sparse``) covers H % 4 == 0, H <= 512, O <= 256."""
+    return H % 4 == 0 and 0 < H <= 512 and 0 < O <= 256 and V * O < 2 ** 31 - 1
+
+
+def _src_pinv(plan):
+    """dst-CSR position -> src-CSR position (the inverse of the source CSR's perm), cached on the plan."""
+    pinv = getattr(plan, "_pinv", None)
+    if pinv is None:
+        perm = plan.src.perm
+        pinv = torch.empty_like(perm)
+        pinv[perm.long()] = torch.arange(perm.numel(), device=perm.device, dtype=perm.dtype)
+        plan._pinv = pinv
+    return pinv
+
+
+def _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
+    """``sir_edge_max_bwd_sparse``: the (v, o) pairs grouped by their arg edge (a routing table of
+    8 V O + 16 E bytes), dA_e from the |L_e| W_R rows its routed outputs name, dQ / dK by row passes of
+    both CSRs, dW_R from a_{arg} gathered per (v, o) — V O H multiply-adds per product, no [E, *] buffer."""
+    lib = _native.load()
+    P = _native._ptr
+    H, O = Q.shape[1], W.shape[0]
+    d, s = plan.dst, plan.src
+    V, E = d.n_rows, d.col.numel()
+    dev = dY.device
+    W = W.contiguous()
+    rb, nr = ctypes.c_int64(0), ctypes.c_int64(0)
+    _native._check(lib.sir_edge_max_bwd_sparse_parts(d.n_items, V, ctypes.byref(rb), ctypes.byref(nr)), lib)
+    ent = torch.empty((max(V * O, 1),), device=dev, dtype=torch.int64)
+    ecnt_d = torch.empty((max(E, 1),), device=dev, dtype=torch.int64)
+    ecnt_s = torch.empty((max(E, 1),), device=dev, dtype=torch.int64)
+    part = torch.empty((max(d.n_slots, s.n_slots, 1) * H,), device=dev, dtype=torch.float32)
+    dbpart = torch.empty((rb.value, (O + 3) // 4 * 4), device=dev, dtype=torch.float32)
+    wpart = torch.empty((nr.value, O * H), device=dev, dtype=torch.float32)
+    pinv = _src_pinv(plan) if E else None
+    with _native._Timed("sir_edge_max_bwd_sparse", dev):
+        rc = lib.sir_edge_max_bwd_sparse(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits,
+                                         P(s.col), P(s.items), s.n_items, P(s.splits), s.n_splits, P(pinv), V, E,
+                                         H, O, P(Q), Q.stride(0), P(K), K.stride(0), P(dY), dY.stride(0), P(arg),
+                                         arg.stride(0), act1, float(slope), P(W), P(dQ), dQ.stride(0), P(dK),
+                                         dK.stride(0), P(part), P(ent), P(ecnt_d), P(ecnt_s), P(dbpart), P(wpart),
+                                         _native._stream(dev))
+    _native._check(rc, lib)
+    db = _native.col_sum(dbpart)[:O]                # per-block partials summed in block order
+    dW = _native.col_sum(wpart).view(O, H)          # per-range partials summed in range order
     return dW, db
 
 

@@ -332,6 +332,7 @@ def test_max_backward_row_ranges_match_whole_graph(monkeypatch):
     m = SIRConv(32, 256, 256, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
     g = Graph(src, dst, V)
     monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", None)
+    monkeypatch.setattr(EdgeMaxLinear, "sparse_bwd", False)
     whole = _run(m, g, X, dY)
     calls = []
     orig = edgemlp._max_bwd_ranges
@@ -343,3 +344,102 @@ def test_max_backward_row_ranges_match_whole_graph(monkeypatch):
     for k in whole:
         e = float((ranged[k].double() - whole[k].double()).norm() / whole[k].double().norm().clamp_min(1e-30))
         assert e < 1e-6, (k, e)
+
+
+def _no_edge_buffers(monkeypatch):
+    """Make every edge-materialised / fused max backward fail if the layer reaches it."""
+    from sirgcn import edgemlp
+
+    def boom(*a, **k):
+        raise AssertionError("a max backward other than the routed one was reached")
+    for name in ("_max_bwd_materialised", "_max_bwd_fused", "_max_bwd_ranges"):
+        monkeypatch.setattr(edgemlp, name, boom)
+
+
+@pytest.mark.parametrize("chunk", [256, 64, 4])
+@pytest.mark.parametrize("act", ["leaky", "relu", "gelu"])
+@pytest.mark.parametrize("H,O", [(256, 256), (256, 40), (64, 64), (300, 24), (128, 256), (100, 200), (512, 256),
+                                 (4, 1)])
+def test_max_routed_backward_vs_oracle_first_wins(act, H, O, chunk, monkeypatch):
+    """The routed max backward (sir_edge_max_bwd_sparse, opt-in for H % 4 == 0, H <= 512, O <= 256):
+    dY reaches each (v, o)'s first arg-max edge only, dA from the routed W_R rows, no [E, *] buffer —
+    against the fp32 / fp64 oracle on hub rows split at every chunk, isolated rows, exact ties."""
+    from sirgcn.edgemlp import EdgeMaxLinear
+    _no_generic(monkeypatch)
+    _no_edge_buffers(monkeypatch)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", None)
+    monkeypatch.setattr(EdgeMaxLinear, "sparse_bwd", True)
+    src, dst, V, gen = _graph(3 * H + O + chunk)
+    d = 32
+    X, dY = torch.randn(V, d, generator=gen), torch.randn(V, O, generator=gen)
+    torch.manual_seed(O + 1)
+    mod = {"leaky": nn.LeakyReLU(0.2), "relu": nn.ReLU(), "gelu": nn.GELU()}[act]
+    m = SIRConv(d, H, O, mod, 0, agg_type="max").to(DEV)
+    m.chunk = chunk
+    g = Graph(src, dst, V)
+    cap = {}
+    got = _run(m, g, X, dY, capture=cap)
+    cond = _tie_condition(m, src, dst, V, X, act, cap, f"max routed {act} H{H} O{O} c{chunk}")
+    r32 = _oracle(m, src, dst, V, X, dY, "max", act, torch.float32, **cond)
+    r64 = _oracle(m, src, dst, V, X, dY, "max", act, torch.float64, **cond)
+    for k, kr in (("Y", "Y"), ("dX", "dX"), ("linear_query.weight", "dW_Q"), ("linear_query.bias", "db_Q"),
+                  ("linear_key.weight", "dW_K"), ("linear_relation.weight", "dW_R"),
+                  ("linear_relation.bias", "db_R")):
+        assert_parity(got[k], r32[kr], r64[kr], 1e-5, f"max routed {act} H{H} O{O} c{chunk} {k}", strict=(k == "Y"))
+
+
+@pytest.mark.parametrize("other", [True, False])
+def test_max_routed_backward_agrees_with_other_routes(other, monkeypatch):
+    """Routed vs fused (True) / edge-materialised (False) max backward: the same first arg-max routing,
+    gradients agree to fp32 rounding; the routed one is bit-identical run to run."""
+    from sirgcn.edgemlp import EdgeMaxLinear
+    src, dst, V, gen = _graph(97)
+    X, dY = torch.randn(V, 32, generator=gen), torch.randn(V, 96, generator=gen)
+    torch.manual_seed(19)
+    m = SIRConv(32, 128, 96, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
+    g = Graph(src, dst, V)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", None)
+    monkeypatch.setattr(EdgeMaxLinear, "sparse_bwd", True)
+    a = _run(m, g, X, dY)
+    a2 = _run(m, g, X, dY)
+    for k in a:
+        assert torch.equal(a[k], a2[k]), k
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", other)
+    b = _run(m, g, X, dY)
+    for k in a:
+        e = (a[k] - b[k]).norm() / b[k].norm().clamp_min(1e-30)
+        assert e < 1e-5, (k, float(e))
+
+
+def test_max_routed_backward_s1_scale_deterministic_without_edge_buffers(monkeypatch):
+    """S1-scale max layer (V=500k, E=10M, H=O=256) through the routed backward: twice bit-identically,
+    with the backward's peak memory far below one [E, H] fp32 buffer (10 GB): no edge-sized tensor."""
+    from sirgcn.edgemlp import EdgeMaxLinear
+    from sirgcn.synth import powerlaw_graph
+    _no_edge_buffers(monkeypatch)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", None)
+    monkeypatch.setattr(EdgeMaxLinear, "sparse_bwd", True)
+    V, E, H = 500_000, 10_000_000, 256
+    g = powerlaw_graph(V, E, 0.8, seed=1)
+    torch.manual_seed(2)
+    m = SIRConv(H, H, H, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    X = torch.randn(V, H, device=DEV, generator=gen).requires_grad_(True)
+    dY = torch.randn(V, H, device=DEV, generator=gen)
+    grads = []
+    for _ in range(2):
+        X.grad = None
+        m.zero_grad(set_to_none=True)
+        Y = m(g, X)
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        Y.backward(dY)
+        torch.cuda.synchronize()
+        peak = torch.cuda.max_memory_allocated() - base
+        assert peak < E * H * 4 // 2, f"backward peak {peak / 2**30:.2f} GiB: an edge-sized buffer?"
+        grads.append([X.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+        del Y
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+        assert torch.isfinite(a).all()
