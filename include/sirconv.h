@@ -357,6 +357,15 @@ int sir_edge_max_bwd_sparse(const int32_t* rowptr_d, const int32_t* col_d, const
                             float* dQ, int64_t lddq, float* dK, int64_t lddk, float* partial, void* ent,
                             void* ecnt_d, void* ecnt_s, float* dbpart, float* wpart, void* stream);
 
+/* dW_R / db_R of the edge-materialised max backward without dM [E, O] (ABI 14): A [E, H] = act1(z_e) in
+ * dst-CSR order, dW[o, :] = sum_v dY[v][o] A[arg[v][o], :], db[o] = sum_v dY[v][o] (arg[v][o] in
+ * [rowptr[v], rowptr[v+1]), else no term).  wpart: sir_max_dw_rows_parts(V, H) rows of ldw >= O * H + O4
+ * floats (O4 = O rounded up to 4): [dW (O x H, row-major) | db (O4)] per row; sum them in row order (e.g.
+ * sir_col_sum).  O <= 256, H % 4 == 0, A rows 16-B aligned.  Deterministic. */
+int64_t sir_max_dw_rows_parts(int64_t V, int64_t H);
+int sir_max_dw_rows(const int32_t* rowptr, int64_t V, const int32_t* arg, int64_t lda, const float* dY, int64_t ldy,
+                    const float* A, int64_t ldA, int64_t O, int64_t H, float* wpart, int64_t ldw, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * GraphNorm (models/norm.py:7-29) on a batched graph: graph b owns node rows [off[b], off[b+1])
  * (off = int64 [B+1], the prefix sum of batch_num_nodes).  Per graph and feature:

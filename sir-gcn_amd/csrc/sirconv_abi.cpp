@@ -579,6 +579,24 @@ int sir_edge_max_bwd_sparse(const int32_t* rowptr_d, const int32_t* col_d, const
     return finish(fn, sir::run_max_bwd_sparse(a, static_cast<hipStream_t>(stream)), nullptr);
 }
 
+int64_t sir_max_dw_rows_parts(int64_t V, int64_t H) {
+    if (V < 0 || H <= 0) return 0;
+    return sir::max_dw_rows_ranges(V, (int)H);
+}
+
+int sir_max_dw_rows(const int32_t* rowptr, int64_t V, const int32_t* arg, int64_t lda, const float* dY, int64_t ldy,
+                    const float* A, int64_t ldA, int64_t O, int64_t H, float* wpart, int64_t ldw, void* stream) {
+    const char* fn = "sir_max_dw_rows";
+    if (O <= 0 || O > 256 || H <= 0 || H % 4 != 0 || H > INT32_MAX) return fail(SIR_EUNSUPPORTED, fn, "O <= 256, H % 4 == 0");
+    if (V < 0 || V > INT32_MAX) return fail(SIR_EINVAL, fn, "bad V");
+    if (ldw < O * H + ((O + 3) / 4) * 4 || ldw % 4) return fail(SIR_EINVAL, fn, "ldw >= O * H + O4, ldw % 4 == 0");
+    if (ldA < H || ldA % 4 || !al16(A) || !al16(wpart)) return fail(SIR_EUNSUPPORTED, fn, "A rows 16-B aligned");
+    if (V > 0 && (rowptr == nullptr || arg == nullptr || lda < O || dY == nullptr || ldy < O || wpart == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer / leading dimension");
+    return finish(fn, sir::run_max_dw_rows(rowptr, V, arg, lda, dY, ldy, A, ldA, (int)O, (int)H, wpart, ldw,
+                                           static_cast<hipStream_t>(stream)), nullptr);
+}
+
 int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
                          const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
                          int64_t H, int64_t O, const float* K, int64_t ldk, const float* Q, int64_t ldq,

@@ -338,6 +338,135 @@ k_maxb_dw(const int* __restrict__ rowptr, const int* __restrict__ col, const int
     }
 }
 
+// ------------------------------------------------------------------------------ dW_R from materialised A
+// The edge-materialised max backward's dW_R / db_R without dM [E, O] or the dense TN GEMM: A [E, H] holds
+// a_e = act1(z_e) in dst-CSR order, so dW_R[o, :] = sum_v dY[v][o] A[arg[v][o], :] reads each row's A rows
+// contiguously.  Block = 512 lanes, lane = (output o <= 256, 32-column half of the 64 columns c0 = 64 blockIdx.x); grid.y =
+// destination-row ranges.  Consecutive rows are batched up to 4 rows / 64 edges: the batch's A columns (and
+// its rows' arg / dY) are loaded one batch ahead into registers and staged in LDS; each lane adds dY[v][o] A[arg][cols] from
+// LDS; a row longer than 64 edges is a batch of its own whose lanes read their arg rows from global memory.
+// Partials [range][O * H (+ O: db_R on the first column block)], summed in range order afterwards.
+constexpr int MDW_ROWS = 4, MDW_EDGES = 64, MDW_PITCH = 68, MDW_WIN = 1024;
+
+__global__ void __launch_bounds__(512)
+k_max_dw_rows(const int* __restrict__ rowptr, const int* __restrict__ arg, int64_t lda,
+              const float* __restrict__ dY, int64_t ldy, const float* __restrict__ A, int64_t ldA,
+              int V, int O, int H, int rows_per, float* __restrict__ wpart, int64_t ldw) {
+    __shared__ float sA[MDW_EDGES * MDW_PITCH];
+    __shared__ int sRp[MDW_WIN + 1];                          // rowptr[wb .. wb + MDW_WIN]
+    const int t = threadIdx.x;
+    const int o = t & 255, hc = t >> 8;                      // output, half of the 64-column block
+    const bool ook = o < O;
+    const int c0 = 64 * blockIdx.x;
+    const int cl = 32 * hc;                                  // this lane's 32 columns: c0 + cl ..
+    const int r0 = blockIdx.y * rows_per;
+    const int r1 = (r0 + rows_per) < V ? (r0 + rows_per) : V;
+    float4 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float db = 0.f;
+    int wb = r0;
+    auto fill = [&]() {                                      // the rowptr window (all threads, then a barrier)
+        for (int i = t; i <= MDW_WIN && wb + i <= V; i += 512) sRp[i] = rowptr[wb + i];
+        __syncthreads();
+    };
+    auto rp = [&](int r) { return sRp[r - wb]; };
+    // batch = rows [br, be) with edges [rowptr[br], rowptr[be]); hub = one row over MDW_EDGES edges
+    auto form = [&](int br, int& be, bool& hub) {
+        const int base = rp(br);
+        be = br + 1;
+        hub = rp(br + 1) - base > MDW_EDGES;
+        if (!hub)
+            while (be < r1 && be - br < MDW_ROWS && rp(be + 1) - base <= MDW_EDGES) ++be;
+    };
+    float4 pre[MDW_EDGES / 32];
+    int pa[MDW_ROWS];
+    float py[MDW_ROWS];
+    auto load = [&](int br, int be, bool hub) {
+        const int base = rp(br);
+        const int ne = rp(be) - base;
+#pragma unroll
+        for (int k = 0; k < MDW_EDGES / 32; ++k) {
+            const int i = t + 512 * k;             // float4 index: edge i / 16, quad i % 16
+            const int e = i >> 4, q = i & 15;
+            pre[k] = (!hub && e < ne && c0 + 4 * q < H) ? ld4(A + (int64_t)(base + e) * ldA + c0 + 4 * q)
+                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    int na[MDW_ROWS];
+    float ny[MDW_ROWS];
+    auto load_args = [&](int br, int be) {                   // into na / ny: one batch ahead
+#pragma unroll
+        for (int j = 0; j < MDW_ROWS; ++j) {
+            const int r = br + j;
+            na[j] = (ook && r < be) ? arg[(int64_t)r * lda + o] : -1;
+            ny[j] = (ook && r < be) ? dY[(int64_t)r * ldy + o] : 0.f;
+        }
+    };
+    int br = r0, be = r0;
+    bool hub = false;
+    if (br < r1) { fill(); form(br, be, hub); load(br, be, hub); load_args(br, be); }
+    while (br < r1) {
+#pragma unroll
+        for (int j = 0; j < MDW_ROWS; ++j) { pa[j] = na[j]; py[j] = ny[j]; }
+        // stage the current batch (and cache its row bounds), then put the next batch in flight
+#pragma unroll
+        for (int k = 0; k < MDW_EDGES / 32; ++k) {
+            const int i = t + 512 * k;
+            *reinterpret_cast<float4*>(&sA[(i >> 4) * MDW_PITCH + 4 * (i & 15)]) = pre[k];
+        }
+        const int cbr = br, cbe = be;
+        const bool chub = hub;
+        int crp[MDW_ROWS + 1];
+#pragma unroll
+        for (int j = 0; j <= MDW_ROWS; ++j) crp[j] = (cbr + j <= cbe) ? rp(cbr + j) : 0;
+        __syncthreads();
+        br = be;
+        if (br < r1) {
+            if (br + MDW_ROWS + 1 > wb + MDW_WIN) { wb = br; fill(); }
+            form(br, be, hub);
+            load(br, be, hub);
+            load_args(br, be);
+        }
+        const int base = crp[0];
+#pragma unroll
+        for (int j = 0; j < MDW_ROWS; ++j) {
+            if (cbr + j >= cbe) break;
+            const int a = pa[j];
+            if (a < crp[j] || a >= crp[j + 1]) continue;            // no arg edge (empty row)
+            const float y = py[j];
+            if (hc == 0) db += y;
+            if (chub) {                                                 // hub row: arg rows from global memory
+                const float* ap = A + (int64_t)a * ldA + c0 + cl;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float4 v = (c0 + cl + 4 * q < H) ? ld4(ap + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    acc[q].x = fmaf(y, v.x, acc[q].x); acc[q].y = fmaf(y, v.y, acc[q].y);
+                    acc[q].z = fmaf(y, v.z, acc[q].z); acc[q].w = fmaf(y, v.w, acc[q].w);
+                }
+            } else {
+                const float* ap = &sA[(a - base) * MDW_PITCH + cl];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
+                    acc[q].x = fmaf(y, v.x, acc[q].x); acc[q].y = fmaf(y, v.y, acc[q].y);
+                    acc[q].z = fmaf(y, v.z, acc[q].z); acc[q].w = fmaf(y, v.w, acc[q].w);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (ook) {
+        float* wp = wpart + (int64_t)blockIdx.y * ldw;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (c0 + cl + 4 * q < H) *reinterpret_cast<float4*>(wp + (int64_t)o * H + c0 + cl + 4 * q) = acc[q];
+        if (blockIdx.x == 0 && hc == 0) wp[(int64_t)O * H + o] = db;
+    }
+    if (blockIdx.x == 0 && hc == 0 && t >= O && t < ((O + 3) & ~3))
+        wpart[(int64_t)blockIdx.y * ldw + (int64_t)O * H + t] = 0.f;
+}
+
 #ifndef SIR_MAXB_U
 #define SIR_MAXB_U 4
 #endif
@@ -361,6 +490,26 @@ int64_t maxb_dw_ranges(int64_t V) {
     int64_t r = 64;
     while (r > 1 && V / r < 16) r >>= 1;
     return r;
+}
+
+int64_t max_dw_rows_ranges(int64_t V, int H) {
+    // two 512-thread blocks a CU (110 VGPRs): 512 / (H / 64) column blocks' worth of row ranges, at least
+    // 64 rows a range
+    const int64_t nc = (H + 63) / 64;
+    int64_t r = 512 / (nc > 0 ? nc : 1);
+    if (r < 1) r = 1;
+    while (r > 1 && V / r < 64) r >>= 1;
+    return r;
+}
+
+hipError_t run_max_dw_rows(const int* rowptr, int64_t V, const int* arg, int64_t lda, const float* dY, int64_t ldy,
+                           const float* A, int64_t ldA, int O, int H, float* wpart, int64_t ldw, hipStream_t st) {
+    if (V == 0) return hipSuccess;
+    const int64_t R = max_dw_rows_ranges(V, H);
+    const int rows_per = (int)((V + R - 1) / R);
+    hipLaunchKernelGGL(k_max_dw_rows, dim3((unsigned)((H + 63) / 64), (unsigned)R), dim3(512), 0, st, rowptr, arg,
+                       lda, dY, ldy, A, ldA, (int)V, O, H, rows_per, wpart, ldw);
+    return hipGetLastError();
 }
 
 hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st) {

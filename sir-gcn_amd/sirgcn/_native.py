@@ -85,6 +85,8 @@ SIGNATURES = {
     "sir_edge_max_bwd_sparse": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _P, _I64, _I64,
                                                _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I, _F, _P,
                                                _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "sir_max_dw_rows_parts": (ctypes.c_int64, [_I64, _I64]),
+    "sir_max_dw_rows": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P]),
     "sir_edge_mlp_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
                                             _P, _P, _I, _I, _F, _I, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "sir_edge_mlp_bwd_src": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
@@ -687,3 +689,20 @@ def dropout_apply(X, drop, col0=0):
         rc = lib.sir_dropout_apply(_ptr(X), X.stride(0), M, N, STORAGE[X.dtype], col0, _drop(drop), _stream(X.device))
     _check(rc, lib)
     return X
+
+
+def max_dw_rows(dcsr, arg, dY, A, O):
+    """dW_R [O, H], db_R [O] of the materialised max backward from A [E, H] (dst-CSR order) and the
+    arg edges, without dM (``sir_max_dw_rows``)."""
+    lib = load()
+    H = A.shape[1]
+    V = dcsr.n_rows
+    R = max(int(lib.sir_max_dw_rows_parts(V, H)), 1)
+    ldw = O * H + (O + 3) // 4 * 4
+    wpart = torch.empty((R, ldw), device=A.device, dtype=torch.float32)
+    with _Timed("sir_max_dw_rows", A.device):
+        rc = lib.sir_max_dw_rows(_ptr(dcsr.rowptr), V, _ptr(arg), arg.stride(0), _ptr(dY), dY.stride(0), _ptr(A),
+                                 A.stride(0), O, H, _ptr(wpart), ldw, _stream(A.device))
+    _check(rc, lib)
+    tot = col_sum(wpart)
+    return tot[:O * H].view(O, H), tot[O * H:O * H + O]

@@ -197,6 +197,7 @@ class EdgeMaxLinear(torch.autograd.Function):
     # Off by default: its dW_R pass (a_{arg} gathered per (v, o), L1-bound) makes it slower than the
     # edge-materialised route at S1 / S2 (36.0 vs 30.4 ms S1 max step, 138 vs 120 ms S2 max)
     sparse_bwd = False
+    dw_rows = True              # materialised route: dW_R / db_R from A and the arg edges (sir_max_dw_rows)
     materialised_budget = 48 << 30
 
     @staticmethod
@@ -355,7 +356,11 @@ def _max_bwd_materialised(dcsr, scsr, Q, K, W, arg, dY, act1, slope, dQ, dK):
         A = _act(Z, act1, slope)
     dM = torch.empty((E, O), device=dev, dtype=torch.float32)
     _native.segment_max_bwd(dcsr, arg, dY, dM)                     # dY to the first arg-max edge
-    dW, db = linalg.mm_tn(dM, A, colsum=True)                      # dW_R = dM^T A, db_R = sum dM
+    if EdgeMaxLinear.dw_rows and O <= 256 and H % 4 == 0 and A.is_contiguous():
+        # dW_R[o] = sum_v dY[v][o] A[arg[v][o]]: each row's A rows read once, V O H multiply-adds
+        dW, db = _native.max_dw_rows(dcsr, arg, dY, A, O)
+    else:
+        dW, db = linalg.mm_tn(dM, A, colsum=True)                  # dW_R = dM^T A, db_R = sum dM
     if relu_family:     # dZ = sigma'(z) * (dM W_R) with sigma' read off A in the GEMM's epilogue
         dZ = linalg.mm_w_dact(dM, W, A, act1, slope, gate_mask=smask)
         del A, Z, dM

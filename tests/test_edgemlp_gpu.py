@@ -443,3 +443,31 @@ def test_max_routed_backward_s1_scale_deterministic_without_edge_buffers(monkeyp
     for a, b in zip(*grads):
         assert torch.equal(a, b)
         assert torch.isfinite(a).all()
+
+
+@pytest.mark.parametrize("chunk", [256, 4])
+@pytest.mark.parametrize("H,O", [(256, 256), (128, 96), (300, 24), (64, 1), (512, 256)])
+def test_max_dw_rows_matches_tn_gemm(H, O, chunk, monkeypatch):
+    """The materialised max backward's dW_R / db_R from A and the arg edges (sir_max_dw_rows: row batches
+    staged in LDS, hub rows read from global) against the same backward on dM^T A (the TN GEMM): fp32
+    rounding apart; dQ / dK untouched (bit-identical); run to run bit-identical."""
+    from sirgcn.edgemlp import EdgeMaxLinear
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", False)
+    src, dst, V, gen = _graph(5 * H + O + chunk, V=700, E=9000)
+    X, dY = torch.randn(V, 32, generator=gen), torch.randn(V, O, generator=gen)
+    torch.manual_seed(H + O)
+    m = SIRConv(32, H, O, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
+    m.chunk = chunk
+    g = Graph(src, dst, V)
+    monkeypatch.setattr(EdgeMaxLinear, "dw_rows", True)
+    a = _run(m, g, X, dY)
+    a2 = _run(m, g, X, dY)
+    monkeypatch.setattr(EdgeMaxLinear, "dw_rows", False)
+    b = _run(m, g, X, dY)
+    for k in a:
+        assert torch.equal(a[k], a2[k]), k
+        if k in ("linear_relation.weight", "linear_relation.bias"):
+            e = float((a[k].double() - b[k].double()).norm() / b[k].double().norm().clamp_min(1e-30))
+            assert e < 2e-6, (k, e)
+        else:
+            assert torch.equal(a[k], b[k]), k
