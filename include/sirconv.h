@@ -344,7 +344,8 @@ int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
  * with V * O * H multiply-adds per product (not E * O * H) and no [E, H] / [E, O] buffer.  Workspace:
  * ent = 8 * V * O bytes (V * O < 2^31), ecnt_d / ecnt_s = 8 * E bytes each, partial = max(n_slots) * H
  * floats, dbpart = route_blocks * O4 floats (O4 = O rounded up to 4) and wpart = dw_ranges * O * H floats (the sizes from
- * sir_edge_max_bwd_sparse_parts; sum each over its rows in row order for db / dW, e.g. sir_col_sum).
+ * sir_edge_max_bwd_sparse_parts; sum each over its rows in row order for db / dW, e.g. sir_col_sum;
+ * wpart NULL skips the dW pass, for a caller that has A and uses sir_max_dw_rows).
  * pinv[dst-CSR position] = src-CSR position (the inverse of the source CSR's perm).  H % 4 == 0,
  * H <= 512, O <= 256, Q / K / W rows 16-B aligned.  Deterministic (no atomics). */
 int sir_edge_max_bwd_sparse_parts(int64_t n_items_d, int64_t V, int64_t* route_blocks, int64_t* dw_ranges);

@@ -559,7 +559,7 @@ int sir_edge_max_bwd_sparse(const int32_t* rowptr_d, const int32_t* col_d, const
         return fail(SIR_EUNSUPPORTED, fn, "Q / K / W / dQ / dK rows must be 16-B aligned (ld % 4 == 0, ld >= H)");
     if (V > 0 && (rowptr_d == nullptr || items_d == nullptr || Q == nullptr || dY == nullptr || ldy < O ||
                   arg == nullptr || lda < O || W == nullptr || dQ == nullptr || dbpart == nullptr ||
-                  wpart == nullptr || ent == nullptr))
+                  ent == nullptr))
         return fail(SIR_EINVAL, fn, "NULL buffer / leading dimension");
     if (E > 0 && (col_d == nullptr || col_s == nullptr || items_s == nullptr || pinv == nullptr || K == nullptr ||
                   dK == nullptr || ecnt_d == nullptr || ecnt_s == nullptr))

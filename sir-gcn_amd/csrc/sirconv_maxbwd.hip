@@ -569,8 +569,8 @@ hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st) {
         else if (opad == 128) e1 = both(std::integral_constant<int, 128>());
         else e1 = both(std::integral_constant<int, 256>());
         if (e1 != hipSuccess) return e1;
-        // 3. dW_R partials
-        if (a.V > 0) {
+        // 3. dW_R partials (wpart NULL: the caller computes dW_R itself, e.g. sir_max_dw_rows)
+        if (a.V > 0 && a.wpart != nullptr) {
             const int nct = (H + 31) / 32;
             const int not_ = (O + 63) / 64;
             const int64_t R = maxb_dw_ranges(a.V);

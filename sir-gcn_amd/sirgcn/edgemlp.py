@@ -197,6 +197,8 @@ class EdgeMaxLinear(torch.autograd.Function):
     # Off by default: its dW_R pass (a_{arg} gathered per (v, o), L1-bound) makes it slower than the
     # edge-materialised route at S1 / S2 (36.0 vs 30.4 ms S1 max step, 138 vs 120 ms S2 max)
     sparse_bwd = False
+    # True: A [E, H] materialised for dW_R (sir_max_dw_rows), dQ / dK from the routed passes (no dM, no dZ)
+    hybrid_bwd = True
     dw_rows = True              # materialised route: dW_R / db_R from A and the arg edges (sir_max_dw_rows)
     materialised_budget = 48 << 30
 
@@ -273,6 +275,10 @@ def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
     # has reserved but not handed out (a warm training loop holds most memory there)
     avail = torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
     budget = min(EdgeMaxLinear.materialised_budget, int(0.4 * avail))
+    V = plan.dst.n_rows
+    if (fused is None and EdgeMaxLinear.hybrid_bwd and max_bwd_sparse(H, O, V)
+            and E * (H * 4 + 16) + V * O * 8 <= budget):
+        return _max_bwd_hybrid(plan, Q, K, W, arg, dY, act1, slope, dQ, dK)
     if E * per_edge > budget and E > 0:
         # the [E, *] buffers exceed the budget: the same dataflow over destination-row ranges of
         # <= budget / per_edge edges each (the S2 shape: 123 GB of buffers -> 3 ranges of <= 48 GiB)
@@ -382,6 +388,23 @@ def max_bwd_sparse(H, O, V):
     return H % 4 == 0 and 0 < H <= 512 and 0 < O <= 256 and V * O < 2 ** 31 - 1
 
 
+def _max_bwd_hybrid(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
+    """A = act1(z) materialised once ([E, H], dst-CSR order) for dW_R / db_R (``sir_max_dw_rows``); dQ / dK
+    from the routed passes (``sir_edge_max_bwd_sparse`` without its dW pass): no dM [E, O], no dZ [E, H]."""
+    H, O = Q.shape[1], W.shape[0]
+    d = plan.dst
+    E = d.col.numel()
+    dev = dY.device
+    A = torch.empty((max(E, 1), H), device=dev, dtype=torch.float32)[:E]
+    if act1 in (_native.ACT_RELU, _native.ACT_LEAKY, _native.ACT_IDENTITY):
+        _native.edge_gather_act(d, Q, K, act1, slope, A)
+    else:
+        _native.edge_gather_add(d, Q, K, A)
+        A = _act(A, act1, slope)
+    _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK, with_dw=False)
+    return _native.max_dw_rows(d, arg, dY, A, O)
+
+
 def _src_pinv(plan):
     """dst-CSR position -> src-CSR position (the inverse of the source CSR's perm), cached on the plan."""
     pinv = getattr(plan, "_pinv", None)
@@ -393,7 +416,7 @@ def _src_pinv(plan):
     return pinv
 
 
-def _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
+def _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK, with_dw=True):
     """``sir_edge_max_bwd_sparse``: the (v, o) pairs grouped by their arg edge (a routing table of
     8 V O + 16 E bytes), dA_e from the |L_e| W_R rows its routed outputs name, dQ / dK by row passes of
     both CSRs, dW_R from a_{arg} gathered per (v, o) — V O H multiply-adds per product, no [E, *] buffer."""
@@ -411,7 +434,7 @@ def _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
     ecnt_s = torch.empty((max(E, 1),), device=dev, dtype=torch.int64)
     part = torch.empty((max(d.n_slots, s.n_slots, 1) * H,), device=dev, dtype=torch.float32)
     dbpart = torch.empty((rb.value, (O + 3) // 4 * 4), device=dev, dtype=torch.float32)
-    wpart = torch.empty((nr.value, O * H), device=dev, dtype=torch.float32)
+    wpart = torch.empty((nr.value, O * H), device=dev, dtype=torch.float32) if with_dw else None
     pinv = _src_pinv(plan) if E else None
     with _native._Timed("sir_edge_max_bwd_sparse", dev):
         rc = lib.sir_edge_max_bwd_sparse(P(d.rowptr), P(d.col), P(d.items), d.n_items, P(d.splits), d.n_splits,
@@ -421,6 +444,8 @@ def _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
                                          dK.stride(0), P(part), P(ent), P(ecnt_d), P(ecnt_s), P(dbpart), P(wpart),
                                          _native._stream(dev))
     _native._check(rc, lib)
+    if not with_dw:
+        return None, None
     db = _native.col_sum(dbpart)[:O]                # per-block partials summed in block order
     dW = _native.col_sum(wpart).view(O, H)          # per-range partials summed in range order
     return dW, db

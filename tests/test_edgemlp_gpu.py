@@ -471,3 +471,32 @@ def test_max_dw_rows_matches_tn_gemm(H, O, chunk, monkeypatch):
             assert e < 2e-6, (k, e)
         else:
             assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("act", [nn.LeakyReLU(0.2), nn.ReLU(), nn.GELU(), nn.LeakyReLU(-0.3)])
+@pytest.mark.parametrize("chunk", [256, 4])
+def test_max_hybrid_backward_matches_materialised(act, chunk, monkeypatch):
+    """The default max backward when it fits (A materialised for dW_R via sir_max_dw_rows, dQ / dK from the
+    routed passes: no dM, no dZ buffer) against the edge-materialised one: fp32 rounding apart, and
+    bit-identical run to run."""
+    from sirgcn import edgemlp
+    from sirgcn.edgemlp import EdgeMaxLinear
+    calls = []
+    orig = edgemlp._max_bwd_hybrid
+    monkeypatch.setattr(edgemlp, "_max_bwd_hybrid", lambda *a: calls.append(1) or orig(*a))
+    src, dst, V, gen = _graph(211 + chunk, V=700, E=9000)
+    X, dY = torch.randn(V, 32, generator=gen), torch.randn(V, 96, generator=gen)
+    torch.manual_seed(23)
+    m = SIRConv(32, 128, 96, act, 0, agg_type="max").to(DEV)
+    m.chunk = chunk
+    g = Graph(src, dst, V)
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", None)
+    a = _run(m, g, X, dY)
+    a2 = _run(m, g, X, dY)
+    assert calls, "the hybrid route was not taken"
+    monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", False)
+    b = _run(m, g, X, dY)
+    for k in a:
+        assert torch.equal(a[k], a2[k]), k
+        e = float((a[k].double() - b[k].double()).norm() / b[k].double().norm().clamp_min(1e-30))
+        assert e < 2e-6, (k, e)
