@@ -3,7 +3,7 @@
 # FETCH_SIZE / WRITE_SIZE passes of the S2 f32 and bf16 steps (tools/pmc_traffic.py), the S2 bf16 line
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/final5
+O=${O:-gpurun_out/final5}
 mkdir -p $O
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 tail -1 $O/smoke.log

@@ -3,7 +3,7 @@
 # cfg5 / cfg2 / S1-max kernel summaries
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/final5
+O=${O:-gpurun_out/final5}
 mkdir -p $O
 line() { n=$1; shift; timeout -k 10 500 python -u bench.py "$@" --no-cpu-baseline --no-aux > $O/b_$n.json 2> $O/b_$n.err || { tail -5 $O/b_$n.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/b_$n.json')); print('$n', d['ms_per_step'], d.get('ms_per_step_median'), d['value'])"; }
