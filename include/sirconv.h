@@ -364,6 +364,12 @@ int sir_edge_max_bwd_sparse(const int32_t* rowptr_d, const int32_t* col_d, const
  * floats (O4 = O rounded up to 4): [dW (O x H, row-major) | db (O4)] per row; sum them in row order (e.g.
  * sir_col_sum).  O <= 256, H % 4 == 0, A rows 16-B aligned.  Deterministic. */
 int64_t sir_max_dw_rows_parts(int64_t V, int64_t H);
+/* The same dW_R / db_R without A: a = act1(Q[v] + K[col[e]]) recomputed per row batch (dst CSR rowptr /
+ * col), so with sir_edge_max_bwd_sparse (wpart NULL) the max backward holds no [E, *] buffer.  Same wpart
+ * layout and sizes as sir_max_dw_rows; Q / K rows 16-B aligned. */
+int sir_max_dw_qk(const int32_t* rowptr, const int32_t* col, int64_t V, const int32_t* arg, int64_t lda,
+                  const float* dY, int64_t ldy, const float* Q, int64_t ldq, const float* K, int64_t ldk, int64_t O,
+                  int64_t H, int act1, float slope, float* wpart, int64_t ldw, void* stream);
 int sir_max_dw_rows(const int32_t* rowptr, int64_t V, const int32_t* arg, int64_t lda, const float* dY, int64_t ldy,
                     const float* A, int64_t ldA, int64_t O, int64_t H, float* wpart, int64_t ldw, void* stream);
 

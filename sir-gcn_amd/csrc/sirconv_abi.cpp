@@ -597,6 +597,23 @@ int sir_max_dw_rows(const int32_t* rowptr, int64_t V, const int32_t* arg, int64_
                                            static_cast<hipStream_t>(stream)), nullptr);
 }
 
+int sir_max_dw_qk(const int32_t* rowptr, const int32_t* col, int64_t V, const int32_t* arg, int64_t lda,
+                  const float* dY, int64_t ldy, const float* Q, int64_t ldq, const float* K, int64_t ldk, int64_t O,
+                  int64_t H, int act1, float slope, float* wpart, int64_t ldw, void* stream) {
+    const char* fn = "sir_max_dw_qk";
+    if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
+    if (O <= 0 || O > 256 || H <= 0 || H % 4 != 0 || H > INT32_MAX) return fail(SIR_EUNSUPPORTED, fn, "O <= 256, H % 4 == 0");
+    if (V < 0 || V > INT32_MAX) return fail(SIR_EINVAL, fn, "bad V");
+    if (ldw < O * H + ((O + 3) / 4) * 4 || ldw % 4) return fail(SIR_EINVAL, fn, "ldw >= O * H + O4, ldw % 4 == 0");
+    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || !al16(Q) || !al16(K) || !al16(wpart))
+        return fail(SIR_EUNSUPPORTED, fn, "Q / K rows 16-B aligned");
+    if (V > 0 && (rowptr == nullptr || col == nullptr || arg == nullptr || lda < O || dY == nullptr || ldy < O ||
+                  wpart == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL buffer / leading dimension");
+    return finish(fn, sir::run_max_dw_qk(rowptr, col, V, arg, lda, dY, ldy, Q, ldq, K, ldk, (int)O, (int)H, act1, slope,
+                                         wpart, ldw, static_cast<hipStream_t>(stream)), nullptr);
+}
+
 int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const int32_t* perm_s,
                          const int32_t* items, int64_t n_items, const int32_t* splits, int64_t n_splits,
                          int64_t H, int64_t O, const float* K, int64_t ldk, const float* Q, int64_t ldq,

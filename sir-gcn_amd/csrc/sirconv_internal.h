@@ -175,6 +175,9 @@ struct MaxBwdArgs {
 };
 int64_t maxb_dw_ranges(int64_t V);
 int64_t max_dw_rows_ranges(int64_t V, int H);
+hipError_t run_max_dw_qk(const int* rowptr, const int* col, int64_t V, const int* arg, int64_t lda, const float* dY,
+                         int64_t ldy, const float* Q, int64_t ldq, const float* K, int64_t ldk, int O, int H, int act1,
+                         float slope, float* wpart, int64_t ldw, hipStream_t st);
 hipError_t run_max_dw_rows(const int* rowptr, int64_t V, const int* arg, int64_t lda, const float* dY, int64_t ldy,
                            const float* A, int64_t ldA, int O, int H, float* wpart, int64_t ldw, hipStream_t st);
 hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st);

@@ -467,6 +467,179 @@ k_max_dw_rows(const int* __restrict__ rowptr, const int* __restrict__ arg, int64
         wpart[(int64_t)blockIdx.y * ldw + (int64_t)O * H + t] = 0.f;
 }
 
+// dW_R / db_R with the activations recomputed in the batch staging instead of read from A [E, H]: each
+// non-hub batch gathers K[col[e]] of its edges and Q of its rows, stages a = act1(Q[v] + K[u]) in LDS and
+// accumulates as k_max_dw_rows does (hub rows: each lane gathers its arg edge's K row).  The batch's
+// column ids are loaded two batches ahead, its K / Q columns one batch ahead (raw, activated at staging).
+// With the routed dQ / dK passes this leaves the max backward without any [E, *] buffer.
+template <int ACT1>
+__global__ void __launch_bounds__(512)
+k_max_dw_qk(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ arg, int64_t lda,
+            const float* __restrict__ dY, int64_t ldy, const float* __restrict__ Q, int64_t ldq,
+            const float* __restrict__ K, int64_t ldk, int V, int O, int H, float slope, int rows_per,
+            float* __restrict__ wpart, int64_t ldw) {
+    __shared__ float sA[MDW_EDGES * MDW_PITCH];
+    __shared__ int sRp[MDW_WIN + 1];                          // rowptr[wb .. wb + MDW_WIN]
+    const int t = threadIdx.x;
+    const int o = t & 255, hc = t >> 8;                      // output, half of the 64-column block
+    const bool ook = o < O;
+    const int c0 = 64 * blockIdx.x;
+    const int cl = 32 * hc;                                  // this lane's 32 accumulated columns
+    const int qq = t & 15;                                   // staging: this thread's quad of the 64 columns
+    const bool qok = c0 + 4 * qq < H;
+    const int r0 = blockIdx.y * rows_per;
+    const int r1 = (r0 + rows_per) < V ? (r0 + rows_per) : V;
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = zero4;
+    float db = 0.f;
+    int wb = r0;
+    auto fill = [&]() {
+        for (int i = t; i <= MDW_WIN && wb + i <= V; i += 512) sRp[i] = rowptr[wb + i];
+        __syncthreads();
+    };
+    auto rp = [&](int r) { return sRp[r - wb]; };
+    auto form = [&](int br, int& be, bool& hub) {
+        const int base = rp(br);
+        be = br + 1;
+        hub = rp(br + 1) - base > MDW_EDGES;
+        if (!hub)
+            while (be < r1 && be - br < MDW_ROWS && rp(be + 1) - base <= MDW_EDGES) ++be;
+    };
+    // staging edges of this thread: e_k = t / 16 + 32 k (k < 2), quad qq
+    auto load_cols = [&](int br, int be, bool hub, int* cn) {
+        const int base = rp(br), ne = rp(be) - base;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int e = (t >> 4) + 32 * k;
+            cn[k] = (!hub && e < ne) ? col[base + e] : -1;
+        }
+    };
+    auto load_qk = [&](int br, int be, const int* cn, float4* kq, float4* qq4) {
+        const int base = rp(br);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int ge = base + (t >> 4) + 32 * k;        // global edge position
+            int r = br;
+#pragma unroll
+            for (int j = 1; j < MDW_ROWS; ++j)
+                if (br + j < be && ge >= rp(br + j)) r = br + j;
+            const bool ok = cn[k] >= 0 && qok;
+            kq[k] = ok ? ld4(K + (int64_t)cn[k] * ldk + c0 + 4 * qq) : zero4;
+            qq4[k] = ok ? ld4(Q + (int64_t)r * ldq + c0 + 4 * qq) : zero4;
+        }
+    };
+    int pa[MDW_ROWS], na[MDW_ROWS];
+    float py[MDW_ROWS], ny[MDW_ROWS];
+    auto load_args = [&](int br, int be) {
+#pragma unroll
+        for (int j = 0; j < MDW_ROWS; ++j) {
+            const int r = br + j;
+            na[j] = (ook && r < be) ? arg[(int64_t)r * lda + o] : -1;
+            ny[j] = (ook && r < be) ? dY[(int64_t)r * ldy + o] : 0.f;
+        }
+    };
+    if (r0 >= r1) goto done;
+    {
+        fill();
+        // batch c (current, K / Q in kq / qv), n1 (next: columns in cn1)
+        int br = r0, be, bn, ben;
+        bool hub, hubn;
+        int cn0[2], cn1[2];
+        float4 kq[2], qv[2];
+        form(br, be, hub);
+        load_cols(br, be, hub, cn0);
+        load_qk(br, be, cn0, kq, qv);
+        load_args(br, be);
+        bn = be;
+        if (bn < r1) {
+            if (bn + MDW_ROWS + 1 > wb + MDW_WIN) { __syncthreads(); wb = bn; fill(); }
+            form(bn, ben, hubn);
+            load_cols(bn, ben, hubn, cn1);
+        }
+        while (br < r1) {
+            // stage batch c: a = act1(Q[v] + K[u])
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int e = (t >> 4) + 32 * k;
+                float4 a;
+                a.x = sig<ACT1>(qv[k].x + kq[k].x, slope); a.y = sig<ACT1>(qv[k].y + kq[k].y, slope);
+                a.z = sig<ACT1>(qv[k].z + kq[k].z, slope); a.w = sig<ACT1>(qv[k].w + kq[k].w, slope);
+                *reinterpret_cast<float4*>(&sA[e * MDW_PITCH + 4 * qq]) = a;
+            }
+#pragma unroll
+            for (int j = 0; j < MDW_ROWS; ++j) { pa[j] = na[j]; py[j] = ny[j]; }
+            const int cbr = br, cbe = be;
+            const bool chub = hub;
+            int crp[MDW_ROWS + 1];
+#pragma unroll
+            for (int j = 0; j <= MDW_ROWS; ++j) crp[j] = (cbr + j <= cbe) ? rp(cbr + j) : 0;
+            __syncthreads();
+            // next batch: its K / Q columns in flight; the one after: its column ids
+            br = bn; be = ben; hub = hubn;
+            if (br < r1) {
+                load_qk(br, be, cn1, kq, qv);
+                load_args(br, be);
+                bn = be;
+                if (bn < r1) {
+                    if (bn + MDW_ROWS + 1 > wb + MDW_WIN) {
+                        // the window moves to batch br (its bounds stay readable); every thread is past
+                        // its reads of the old window first
+                        __syncthreads();
+                        wb = br; fill();
+                    }
+                    form(bn, ben, hubn);
+                    load_cols(bn, ben, hubn, cn1);
+                }
+            }
+            const int base = crp[0];
+#pragma unroll
+            for (int j = 0; j < MDW_ROWS; ++j) {
+                if (cbr + j >= cbe) break;
+                const int a = pa[j];
+                if (a < crp[j] || a >= crp[j + 1]) continue;            // no arg edge (empty row)
+                const float y = py[j];
+                if (hc == 0) db += y;
+                if (chub) {                                             // hub row: the arg edge's K row
+                    const int u = col[a];
+                    const float* kp = K + (int64_t)u * ldk + c0 + cl;
+                    const float* qp = Q + (int64_t)(cbr + j) * ldq + c0 + cl;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        if (c0 + cl + 4 * q < H) {
+                            const float4 kv = ld4(kp + 4 * q), qv4 = ld4(qp + 4 * q);
+                            acc[q].x = fmaf(y, sig<ACT1>(qv4.x + kv.x, slope), acc[q].x);
+                            acc[q].y = fmaf(y, sig<ACT1>(qv4.y + kv.y, slope), acc[q].y);
+                            acc[q].z = fmaf(y, sig<ACT1>(qv4.z + kv.z, slope), acc[q].z);
+                            acc[q].w = fmaf(y, sig<ACT1>(qv4.w + kv.w, slope), acc[q].w);
+                        }
+                    }
+                } else {
+                    const float* ap = &sA[(a - base) * MDW_PITCH + cl];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
+                        acc[q].x = fmaf(y, v.x, acc[q].x); acc[q].y = fmaf(y, v.y, acc[q].y);
+                        acc[q].z = fmaf(y, v.z, acc[q].z); acc[q].w = fmaf(y, v.w, acc[q].w);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+done:
+    if (ook) {
+        float* wp = wpart + (int64_t)blockIdx.y * ldw;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (c0 + cl + 4 * q < H) *reinterpret_cast<float4*>(wp + (int64_t)o * H + c0 + cl + 4 * q) = acc[q];
+        if (blockIdx.x == 0 && hc == 0) wp[(int64_t)O * H + o] = db;
+    }
+    if (blockIdx.x == 0 && hc == 0 && t >= O && t < ((O + 3) & ~3))
+        wpart[(int64_t)blockIdx.y * ldw + (int64_t)O * H + t] = 0.f;
+}
+
 #ifndef SIR_MAXB_U
 #define SIR_MAXB_U 4
 #endif
@@ -510,6 +683,20 @@ hipError_t run_max_dw_rows(const int* rowptr, int64_t V, const int* arg, int64_t
     hipLaunchKernelGGL(k_max_dw_rows, dim3((unsigned)((H + 63) / 64), (unsigned)R), dim3(512), 0, st, rowptr, arg,
                        lda, dY, ldy, A, ldA, (int)V, O, H, rows_per, wpart, ldw);
     return hipGetLastError();
+}
+
+hipError_t run_max_dw_qk(const int* rowptr, const int* col, int64_t V, const int* arg, int64_t lda, const float* dY,
+                         int64_t ldy, const float* Q, int64_t ldq, const float* K, int64_t ldk, int O, int H, int act1,
+                         float slope, float* wpart, int64_t ldw, hipStream_t st) {
+    if (V == 0) return hipSuccess;
+    const int64_t R = max_dw_rows_ranges(V, H);
+    const int rows_per = (int)((V + R - 1) / R);
+    return maxb_acts(act1, [&](auto A1) -> hipError_t {
+        constexpr int X1 = decltype(A1)::value;
+        hipLaunchKernelGGL((k_max_dw_qk<X1>), dim3((unsigned)((H + 63) / 64), (unsigned)R), dim3(512), 0, st, rowptr,
+                           col, arg, lda, dY, ldy, Q, ldq, K, ldk, (int)V, O, H, slope, rows_per, wpart, ldw);
+        return hipGetLastError();
+    });
 }
 
 hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st) {

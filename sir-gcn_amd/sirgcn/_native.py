@@ -87,6 +87,8 @@ SIGNATURES = {
                                                _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "sir_max_dw_rows_parts": (ctypes.c_int64, [_I64, _I64]),
     "sir_max_dw_rows": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P]),
+    "sir_max_dw_qk": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _F, _P,
+                                     _I64, _P]),
     "sir_edge_mlp_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
                                             _P, _P, _I, _I, _F, _I, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "sir_edge_mlp_bwd_src": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
@@ -703,6 +705,24 @@ def max_dw_rows(dcsr, arg, dY, A, O):
     with _Timed("sir_max_dw_rows", A.device):
         rc = lib.sir_max_dw_rows(_ptr(dcsr.rowptr), V, _ptr(arg), arg.stride(0), _ptr(dY), dY.stride(0), _ptr(A),
                                  A.stride(0), O, H, _ptr(wpart), ldw, _stream(A.device))
+    _check(rc, lib)
+    tot = col_sum(wpart)
+    return tot[:O * H].view(O, H), tot[O * H:O * H + O]
+
+
+def max_dw_qk(dcsr, arg, dY, Q, K, O, act1, slope):
+    """dW_R [O, H], db_R [O] of the max backward with a = act1(Q[v] + K[u]) recomputed per row batch
+    (``sir_max_dw_qk``): no A buffer."""
+    lib = load()
+    H = Q.shape[1]
+    V = dcsr.n_rows
+    R = max(int(lib.sir_max_dw_rows_parts(V, H)), 1)
+    ldw = O * H + (O + 3) // 4 * 4
+    wpart = torch.empty((R, ldw), device=Q.device, dtype=torch.float32)
+    with _Timed("sir_max_dw_qk", Q.device):
+        rc = lib.sir_max_dw_qk(_ptr(dcsr.rowptr), _ptr(dcsr.col), V, _ptr(arg), arg.stride(0), _ptr(dY), dY.stride(0),
+                               _ptr(Q), Q.stride(0), _ptr(K), K.stride(0), O, H, int(act1), float(slope), _ptr(wpart),
+                               ldw, _stream(Q.device))
     _check(rc, lib)
     tot = col_sum(wpart)
     return tot[:O * H].view(O, H), tot[O * H:O * H + O]

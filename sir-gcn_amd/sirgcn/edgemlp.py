@@ -199,6 +199,7 @@ class EdgeMaxLinear(torch.autograd.Function):
     sparse_bwd = False
     # True: A [E, H] materialised for dW_R (sir_max_dw_rows), dQ / dK from the routed passes (no dM, no dZ)
     hybrid_bwd = True
+    dw_qk = True                # hybrid route: dW_R from Q, K recomputed per row batch (no A buffer)
     dw_rows = True              # materialised route: dW_R / db_R from A and the arg edges (sir_max_dw_rows)
     materialised_budget = 48 << 30
 
@@ -395,6 +396,10 @@ def _max_bwd_hybrid(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
     d = plan.dst
     E = d.col.numel()
     dev = dY.device
+    if EdgeMaxLinear.dw_qk:
+        # dW_R with the activations recomputed per row batch: no [E, *] buffer anywhere in the backward
+        _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK, with_dw=False)
+        return _native.max_dw_qk(d, arg, dY, Q, K, O, act1, slope)
     A = torch.empty((max(E, 1), H), device=dev, dtype=torch.float32)[:E]
     if act1 in (_native.ACT_RELU, _native.ACT_LEAKY, _native.ACT_IDENTITY):
         _native.edge_gather_act(d, Q, K, act1, slope, A)

@@ -473,9 +473,10 @@ def test_max_dw_rows_matches_tn_gemm(H, O, chunk, monkeypatch):
             assert torch.equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("dw_qk", [True, False])
 @pytest.mark.parametrize("act", [nn.LeakyReLU(0.2), nn.ReLU(), nn.GELU(), nn.LeakyReLU(-0.3)])
 @pytest.mark.parametrize("chunk", [256, 4])
-def test_max_hybrid_backward_matches_materialised(act, chunk, monkeypatch):
+def test_max_hybrid_backward_matches_materialised(act, chunk, dw_qk, monkeypatch):
     """The default max backward when it fits (A materialised for dW_R via sir_max_dw_rows, dQ / dK from the
     routed passes: no dM, no dZ buffer) against the edge-materialised one: fp32 rounding apart, and
     bit-identical run to run."""
@@ -484,6 +485,7 @@ def test_max_hybrid_backward_matches_materialised(act, chunk, monkeypatch):
     calls = []
     orig = edgemlp._max_bwd_hybrid
     monkeypatch.setattr(edgemlp, "_max_bwd_hybrid", lambda *a: calls.append(1) or orig(*a))
+    monkeypatch.setattr(EdgeMaxLinear, "dw_qk", dw_qk)
     src, dst, V, gen = _graph(211 + chunk, V=700, E=9000)
     X, dY = torch.randn(V, 32, generator=gen), torch.randn(V, 96, generator=gen)
     torch.manual_seed(23)
