@@ -277,8 +277,9 @@ def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
     avail = torch.cuda.mem_get_info(dev)[0] + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
     budget = min(EdgeMaxLinear.materialised_budget, int(0.4 * avail))
     V = plan.dst.n_rows
-    if (fused is None and EdgeMaxLinear.hybrid_bwd and max_bwd_sparse(H, O, V)
-            and E * (H * 4 + 16) + V * O * 8 <= budget):
+    # the hybrid's buffers: the routing table (16 B per edge, 8 per (v, o)) and, without dw_qk, A [E, H]
+    hyb = E * (16 + (0 if EdgeMaxLinear.dw_qk else 4 * H)) + V * O * 8
+    if fused is None and EdgeMaxLinear.hybrid_bwd and max_bwd_sparse(H, O, V) and hyb <= budget:
         return _max_bwd_hybrid(plan, Q, K, W, arg, dY, act1, slope, dQ, dK)
     if E * per_edge > budget and E > 0:
         # the [E, *] buffers exceed the budget: the same dataflow over destination-row ranges of
