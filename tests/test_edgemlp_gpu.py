@@ -333,6 +333,7 @@ def test_max_backward_row_ranges_match_whole_graph(monkeypatch):
     g = Graph(src, dst, V)
     monkeypatch.setattr(EdgeMaxLinear, "fused_bwd", None)
     monkeypatch.setattr(EdgeMaxLinear, "sparse_bwd", False)
+    monkeypatch.setattr(EdgeMaxLinear, "hybrid_bwd", False)     # the edge-materialised route under test
     whole = _run(m, g, X, dY)
     calls = []
     orig = edgemlp._max_bwd_ranges
