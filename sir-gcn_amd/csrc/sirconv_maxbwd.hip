@@ -259,8 +259,17 @@ __global__ void k_maxb_combine(const int4* __restrict__ splits, int H, const flo
                                float* __restrict__ out, int64_t ldo) {
     const int4 sp = splits[blockIdx.x];
     for (int f = threadIdx.x; f < H; f += blockDim.x) {
+        const float* p = partial + (int64_t)sp.y * H + f;
         float s = 0.f;
-        for (int k = 0; k < sp.z; ++k) s += partial[(int64_t)(sp.y + k) * H + f];
+        int k = 0;
+        for (; k + 8 <= sp.z; k += 8) {          // 8 loads in flight, added in slot order
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = p[(int64_t)(k + i) * H];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s += v[i];
+        }
+        for (; k < sp.z; ++k) s += p[(int64_t)k * H];
         out[(int64_t)sp.x * ldo + f] = s;
     }
 }
