@@ -345,7 +345,8 @@ int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
  * ent = 8 * V * O bytes (V * O < 2^31), ecnt_d / ecnt_s = 8 * E bytes each, partial = max(n_slots) * H
  * floats, dbpart = route_blocks * O4 floats (O4 = O rounded up to 4) and wpart = dw_ranges * O * H floats (the sizes from
  * sir_edge_max_bwd_sparse_parts; sum each over its rows in row order for db / dW, e.g. sir_col_sum;
- * wpart NULL skips the dW pass, for a caller that has A and uses sir_max_dw_rows).
+ * wpart NULL skips the dW pass, for a caller that has A and uses sir_max_dw_rows).  With no work items
+ * (n_items_d == 0) dbpart, and with V == 0 wpart, is written as zeros.
  * pinv[dst-CSR position] = src-CSR position (the inverse of the source CSR's perm).  H % 4 == 0,
  * H <= 512, O <= 256, Q / K / W rows 16-B aligned.  Deterministic (no atomics). */
 int sir_edge_max_bwd_sparse_parts(int64_t n_items_d, int64_t V, int64_t* route_blocks, int64_t* dw_ranges);
@@ -362,7 +363,8 @@ int sir_edge_max_bwd_sparse(const int32_t* rowptr_d, const int32_t* col_d, const
  * dst-CSR order, dW[o, :] = sum_v dY[v][o] A[arg[v][o], :], db[o] = sum_v dY[v][o] (arg[v][o] in
  * [rowptr[v], rowptr[v+1]), else no term).  wpart: sir_max_dw_rows_parts(V, H) rows of ldw >= O * H + O4
  * floats (O4 = O rounded up to 4): [dW (O x H, row-major) | db (O4)] per row; sum them in row order (e.g.
- * sir_col_sum).  O <= 256, H % 4 == 0, A rows 16-B aligned.  Deterministic. */
+ * sir_col_sum).  O <= 256, H % 4 == 0, A rows 16-B aligned.  Deterministic.  V == 0: the one row of
+ * wpart (sir_max_dw_rows_parts(0, H) == 1) is written as zeros (wpart may then be NULL). */
 int64_t sir_max_dw_rows_parts(int64_t V, int64_t H);
 /* The same dW_R / db_R without A: a = act1(Q[v] + K[col[e]]) recomputed per row batch (dst CSR rowptr /
  * col), so with sir_edge_max_bwd_sparse (wpart NULL) the max backward holds no [E, *] buffer.  Same wpart

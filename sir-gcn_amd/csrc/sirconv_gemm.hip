@@ -153,6 +153,14 @@ __device__ inline void split8_mix(float4 a, float4 b, float s, h8& hi, h8& lo) {
     hi = __builtin_bit_cast(h8, u4{h0, h1, h2, h3});
     lo = __builtin_bit_cast(h8, u4{l0, l1, l2, l3});
 }
+// the same split written as fused ops for the backend's v_fma_mix patterns (x s exact: fma(x, s, -hi)
+// == x s - hi, one rounding to fp16 either way)
+#define SIR_SPLIT1F(x, i) { const _Float16 h_ = (_Float16)__builtin_fmaf((x), s, 0.f); hi[i] = h_; lo[i] = (_Float16)__builtin_fmaf((x), s, -(float)h_); }
+__device__ inline void split8_fma(float4 a, float4 b, float s, h8& hi, h8& lo) {
+    SIR_SPLIT1F(a.x, 0) SIR_SPLIT1F(a.y, 1) SIR_SPLIT1F(a.z, 2) SIR_SPLIT1F(a.w, 3)
+    SIR_SPLIT1F(b.x, 4) SIR_SPLIT1F(b.y, 5) SIR_SPLIT1F(b.z, 6) SIR_SPLIT1F(b.w, 7)
+}
+#undef SIR_SPLIT1F
 #define SIR_SPLIT1(x, i) { const float y_ = (x) * s; const _Float16 h_ = (_Float16)y_; hi[i] = h_; lo[i] = (_Float16)(y_ - (float)h_); }
 __device__ inline void split8(float4 a, float4 b, float s, h8& hi, h8& lo) {
     SIR_SPLIT1(a.x, 0) SIR_SPLIT1(a.y, 1) SIR_SPLIT1(a.z, 2) SIR_SPLIT1(a.w, 3)
@@ -560,6 +568,16 @@ k_gemm_nt(const float* __restrict__ A, int64_t lda, int64_t M, int K,
 #ifndef SIR_NT_P_KSB
 #define SIR_NT_P_KSB 1
 #endif
+#ifndef SIR_NT_MAX3
+#define SIR_NT_MAX3 1           // 1: the row maximum of a chunk by v_max3 with |.| modifiers (fmax4_mix)
+#endif
+// hi / lo split of the persistent NT kernel: 1 = v_fma_mix in asm (split8_mix), 2 = the same as fused C ops
+// (split8_fma), 0 = plain C; all bit-identical.  Round-6 A/B over QK / Y / G / dX at S2: 5.71 ms (0) ->
+// 5.57 ms (1 with SIR_NT_MAX3; 2 VGPRs spilled outside the chunk loop), fused C 5.72, MAX3 alone 5.65
+// (profiles/r06_ab_gemm_nt_split.txt)
+#ifndef SIR_NT_SPLIT_MIX
+#define SIR_NT_SPLIT_MIX 1
+#endif
 #ifndef SIR_NT_P_EPI
 #define SIR_NT_P_EPI 1          // persistent NT epilogue through LDS with whole-row stores (1) or fragment stores (0)
 #endif
@@ -653,7 +671,7 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
         char* st = lds + buf * STAGE;
         float m = 0.f;
 #pragma unroll
-        for (int i = 0; i < FPT / 4; ++i) m = fmax4(m, dv[set][i]);
+        for (int i = 0; i < FPT / 4; ++i) m = SIR_NT_MAX3 ? fmax4_mix(m, dv[set][i]) : fmax4(m, dv[set][i]);
         m = fmaxf(m, __shfl_xor(m, 1));
         const int se_old = first ? SE_INIT : se_run, se = next_se(se_old, bexp(m));
         se_run = se;
@@ -666,7 +684,13 @@ k_gemm_nt_p(const float* __restrict__ A, int64_t lda, int64_t M, const u4v* __re
             hv = __builtin_bit_cast(h8, dv[set][j / 4]);         // timing-only: no split arithmetic
             lv = __builtin_bit_cast(h8, dv[set][j / 4 + 1]);
 #else
+#if SIR_NT_SPLIT_MIX == 1
+            split8_mix(dv[set][j / 4], dv[set][j / 4 + 1], s, hv, lv);
+#elif SIR_NT_SPLIT_MIX == 2
+            split8_fma(dv[set][j / 4], dv[set][j / 4 + 1], s, hv, lv);
+#else
             split8(dv[set][j / 4], dv[set][j / 4 + 1], s, hv, lv);
+#endif
 #endif
             *reinterpret_cast<h8*>(st + (0 * 2 + ks) * BD * 32 + fimg(rho, pos >> 3)) = hv;
             *reinterpret_cast<h8*>(st + (1 * 2 + ks) * BD * 32 + fimg(rho, pos >> 3)) = lv;

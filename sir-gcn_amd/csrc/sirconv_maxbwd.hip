@@ -649,8 +649,185 @@ done:
         wpart[(int64_t)blockIdx.y * ldw + (int64_t)O * H + t] = 0.f;
 }
 
+// k_max_dw_qk with larger batches (round 6): up to MDW2_ROWS rows / MDW2_EDGES edges per batch (4 / 64
+// above), the batch's arg / dY staged in LDS with its activations (registers: one batch of K / Q columns and
+// arg / dY in flight), its row bounds in LDS (the rowptr window may move while it is summed).  k_max_dw_qk
+// spent ~5.7 us a batch at S1 against ~0.5 us of arithmetic: each 4-row batch waited for its gathers behind
+// two barriers.  Same per-lane order of terms (rows ascending, the arg edge's activation recomputed with the
+// same operations): bit-identical to k_max_dw_qk.
+constexpr int MDW2_ROWS = 16, MDW2_EDGES = 128, MDW2_WIN = 1024;
+
+template <int ACT1>
+__global__ void __launch_bounds__(512)
+k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ arg, int64_t lda,
+             const float* __restrict__ dY, int64_t ldy, const float* __restrict__ Q, int64_t ldq,
+             const float* __restrict__ K, int64_t ldk, int V, int O, int H, float slope, int rows_per,
+             float* __restrict__ wpart, int64_t ldw) {
+    constexpr int NR = MDW2_ROWS, NE = MDW2_EDGES, WIN = MDW2_WIN, PITCH = MDW_PITCH;
+    constexpr int EPT = NE * 16 / 512;                       // staged (edge, quad) float4s per thread
+    constexpr int APT = NR * 256 / 512;                      // staged (row, output) pairs per thread
+    static_assert(EPT * 512 == NE * 16 && APT * 512 == NR * 256, "staging map");
+    __shared__ float sA[NE * PITCH];
+    __shared__ int sArg[NR * 256];
+    __shared__ float sY[NR * 256];
+    __shared__ int sRp[WIN + 1];                             // rowptr[wb .. wb + WIN]
+    __shared__ int sB[NR + 1];                               // the staged batch's row bounds
+    const int t = threadIdx.x;
+    const int o = t & 255, hc = t >> 8;                      // output, half of the 64-column block
+    const bool ook = o < O;
+    const int c0 = 64 * blockIdx.x;
+    const int cl = 32 * hc;                                  // this lane's 32 accumulated columns
+    const int qq = t & 15;                                   // staging: this thread's quad of the 64 columns
+    const bool qok = c0 + 4 * qq < H;
+    const int r0 = blockIdx.y * rows_per;
+    const int r1 = (r0 + rows_per) < V ? (r0 + rows_per) : V;
+    const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = zero4;
+    float db = 0.f;
+    int wb = r0;
+    auto fill = [&]() {
+        for (int i = t; i <= WIN && wb + i <= V; i += 512) sRp[i] = rowptr[wb + i];
+        __syncthreads();
+    };
+    auto rp = [&](int r) { return sRp[r - wb]; };
+    auto form = [&](int br, int& be, bool& hub) {
+        const int base = rp(br);
+        be = br + 1;
+        hub = rp(br + 1) - base > NE;
+        if (!hub)
+            while (be < r1 && be - br < NR && rp(be + 1) - base <= NE) ++be;
+    };
+    // this thread's staging edges e_k = t / 16 + 32 k: column ids and rows (a merge walk over the bounds)
+    auto load_cols = [&](int br, int be, bool hub, int* cn, int* rn) {
+        const int base = rp(br), ne = rp(be) - base;
+        int j = br;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int e = (t >> 4) + 32 * k;
+            const bool ok = !hub && e < ne;
+            while (ok && j + 1 < be && base + e >= rp(j + 1)) ++j;
+            cn[k] = ok ? col[base + e] : -1;
+            rn[k] = j;
+        }
+    };
+    auto load_qk = [&](const int* cn, const int* rn, float4* kq, float4* qv) {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const bool ok = cn[k] >= 0 && qok;
+            kq[k] = ok ? ld4(K + (int64_t)cn[k] * ldk + c0 + 4 * qq) : zero4;
+            qv[k] = ok ? ld4(Q + (int64_t)rn[k] * ldq + c0 + 4 * qq) : zero4;
+        }
+    };
+    // staged pairs of this thread: (row br + hc + 2 k, output o)
+    auto load_args = [&](int br, int be, int* na, float* ny) {
+#pragma unroll
+        for (int k = 0; k < APT; ++k) {
+            const int r = br + hc + 2 * k;
+            na[k] = (ook && r < be) ? arg[(int64_t)r * lda + o] : -1;
+            ny[k] = (ook && r < be) ? dY[(int64_t)r * ldy + o] : 0.f;
+        }
+    };
+    if (r0 >= r1) goto done;
+    {
+        fill();
+        int br = r0, be, bn, ben;
+        bool hub, hubn;
+        int cn[EPT], rn[EPT], na[APT];
+        float ny[APT];
+        float4 kq[EPT], qv[EPT];
+        form(br, be, hub);
+        load_cols(br, be, hub, cn, rn);
+        load_qk(cn, rn, kq, qv);
+        load_args(br, be, na, ny);
+        bn = be;
+        if (bn < r1) {
+            if (bn + NR + 1 > wb + WIN) { __syncthreads(); wb = bn; fill(); }
+            form(bn, ben, hubn);
+            load_cols(bn, ben, hubn, cn, rn);
+        }
+        while (br < r1) {
+            // stage batch (br, be): a = act1(Q[v] + K[u]), arg / dY, row bounds
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
+                const int e = (t >> 4) + 32 * k;
+                float4 a;
+                a.x = sig<ACT1>(qv[k].x + kq[k].x, slope); a.y = sig<ACT1>(qv[k].y + kq[k].y, slope);
+                a.z = sig<ACT1>(qv[k].z + kq[k].z, slope); a.w = sig<ACT1>(qv[k].w + kq[k].w, slope);
+                *reinterpret_cast<float4*>(&sA[e * PITCH + 4 * qq]) = a;
+            }
+#pragma unroll
+            for (int k = 0; k < APT; ++k) {
+                sArg[(hc + 2 * k) * 256 + o] = na[k];
+                sY[(hc + 2 * k) * 256 + o] = ny[k];
+            }
+            if (t <= NR) sB[t] = (br + t <= be) ? rp(br + t) : 0;
+            const int cbr = br, cbe = be;
+            const bool chub = hub;
+            __syncthreads();
+            // next batch: its K / Q columns and arg / dY in flight; the one after: its column ids
+            br = bn; be = ben; hub = hubn;
+            if (br < r1) {
+                load_qk(cn, rn, kq, qv);
+                load_args(br, be, na, ny);
+                bn = be;
+                if (bn < r1) {
+                    if (bn + NR + 1 > wb + WIN) { __syncthreads(); wb = br; fill(); }
+                    form(bn, ben, hubn);
+                    load_cols(bn, ben, hubn, cn, rn);
+                }
+            }
+            const int base = sB[0];
+            for (int j = 0; j < cbe - cbr; ++j) {
+                const int a = sArg[j * 256 + o];
+                if (!ook || a < sB[j] || a >= sB[j + 1]) continue;    // no arg edge (empty row)
+                const float y = sY[j * 256 + o];
+                if (hc == 0) db += y;
+                if (chub) {                                           // hub row: the arg edge's K row
+                    const int u = col[a];
+                    const float* kp = K + (int64_t)u * ldk + c0 + cl;
+                    const float* qp = Q + (int64_t)(cbr + j) * ldq + c0 + cl;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        if (c0 + cl + 4 * q < H) {
+                            const float4 kv = ld4(kp + 4 * q), qv4 = ld4(qp + 4 * q);
+                            acc[q].x = fmaf(y, sig<ACT1>(qv4.x + kv.x, slope), acc[q].x);
+                            acc[q].y = fmaf(y, sig<ACT1>(qv4.y + kv.y, slope), acc[q].y);
+                            acc[q].z = fmaf(y, sig<ACT1>(qv4.z + kv.z, slope), acc[q].z);
+                            acc[q].w = fmaf(y, sig<ACT1>(qv4.w + kv.w, slope), acc[q].w);
+                        }
+                    }
+                } else {
+                    const float* ap = &sA[(a - base) * PITCH + cl];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
+                        acc[q].x = fmaf(y, v.x, acc[q].x); acc[q].y = fmaf(y, v.y, acc[q].y);
+                        acc[q].z = fmaf(y, v.z, acc[q].z); acc[q].w = fmaf(y, v.w, acc[q].w);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+done:
+    if (ook) {
+        float* wp = wpart + (int64_t)blockIdx.y * ldw;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (c0 + cl + 4 * q < H) *reinterpret_cast<float4*>(wp + (int64_t)o * H + c0 + cl + 4 * q) = acc[q];
+        if (blockIdx.x == 0 && hc == 0) wp[(int64_t)O * H + o] = db;
+    }
+    if (blockIdx.x == 0 && hc == 0 && t >= O && t < ((O + 3) & ~3))
+        wpart[(int64_t)blockIdx.y * ldw + (int64_t)O * H + t] = 0.f;
+}
+
 #ifndef SIR_MAXB_U
 #define SIR_MAXB_U 4
+#endif
+#ifndef SIR_MAXDW
+#define SIR_MAXDW 2             // sir_max_dw_qk: 1 = k_max_dw_qk (4-row / 64-edge batches), 2 = k_max_dw_qk2
 #endif
 
 template <typename Fn>
@@ -686,7 +863,8 @@ int64_t max_dw_rows_ranges(int64_t V, int H) {
 
 hipError_t run_max_dw_rows(const int* rowptr, int64_t V, const int* arg, int64_t lda, const float* dY, int64_t ldy,
                            const float* A, int64_t ldA, int O, int H, float* wpart, int64_t ldw, hipStream_t st) {
-    if (V == 0) return hipSuccess;
+    // no rows: the one partial (max_dw_rows_ranges(0, H) == 1) is written as zeros, never left unset
+    if (V == 0) return wpart != nullptr ? hipMemsetAsync(wpart, 0, (size_t)ldw * sizeof(float), st) : hipSuccess;
     const int64_t R = max_dw_rows_ranges(V, H);
     const int rows_per = (int)((V + R - 1) / R);
     hipLaunchKernelGGL(k_max_dw_rows, dim3((unsigned)((H + 63) / 64), (unsigned)R), dim3(512), 0, st, rowptr, arg,
@@ -697,13 +875,21 @@ hipError_t run_max_dw_rows(const int* rowptr, int64_t V, const int* arg, int64_t
 hipError_t run_max_dw_qk(const int* rowptr, const int* col, int64_t V, const int* arg, int64_t lda, const float* dY,
                          int64_t ldy, const float* Q, int64_t ldq, const float* K, int64_t ldk, int O, int H, int act1,
                          float slope, float* wpart, int64_t ldw, hipStream_t st) {
-    if (V == 0) return hipSuccess;
+    if (V == 0) return wpart != nullptr ? hipMemsetAsync(wpart, 0, (size_t)ldw * sizeof(float), st) : hipSuccess;
     const int64_t R = max_dw_rows_ranges(V, H);
     const int rows_per = (int)((V + R - 1) / R);
+    const char* e = getenv("SIR_MAXDW");
+    const int form = (e != nullptr && e[0] != 0) ? atoi(e) : SIR_MAXDW;
     return maxb_acts(act1, [&](auto A1) -> hipError_t {
         constexpr int X1 = decltype(A1)::value;
-        hipLaunchKernelGGL((k_max_dw_qk<X1>), dim3((unsigned)((H + 63) / 64), (unsigned)R), dim3(512), 0, st, rowptr,
-                           col, arg, lda, dY, ldy, Q, ldq, K, ldk, (int)V, O, H, slope, rows_per, wpart, ldw);
+        if (form == 1)
+            hipLaunchKernelGGL((k_max_dw_qk<X1>), dim3((unsigned)((H + 63) / 64), (unsigned)R), dim3(512), 0, st,
+                               rowptr, col, arg, lda, dY, ldy, Q, ldq, K, ldk, (int)V, O, H, slope, rows_per, wpart,
+                               ldw);
+        else
+            hipLaunchKernelGGL((k_max_dw_qk2<X1>), dim3((unsigned)((H + 63) / 64), (unsigned)R), dim3(512), 0, st,
+                               rowptr, col, arg, lda, dY, ldy, Q, ldq, K, ldk, (int)V, O, H, slope, rows_per, wpart,
+                               ldw);
         return hipGetLastError();
     });
 }
@@ -713,6 +899,14 @@ hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st) {
     const int opad = O <= 64 ? 64 : (O <= 128 ? 128 : 256);
     const int nk = opad / 64;
     hipError_t err = hipSuccess;
+    // nothing to route / no rows: the partials the caller sums are zeros, never left unset (one route
+    // block, one dW range: maxb_route_blocks(0) == maxb_dw_ranges(0) == 1)
+    if (a.n_items_d == 0 && a.dbpart != nullptr &&
+        (err = hipMemsetAsync(a.dbpart, 0, (size_t)((O + 3) / 4 * 4) * sizeof(float), st)) != hipSuccess)
+        return err;
+    if (a.V == 0 && a.wpart != nullptr &&
+        (err = hipMemsetAsync(a.wpart, 0, (size_t)O * H * sizeof(float), st)) != hipSuccess)
+        return err;
     // 1. routing table + db partials
     if (a.n_items_d > 0) {
         const int nb = (int)(a.route_blocks);

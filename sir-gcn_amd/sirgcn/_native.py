@@ -719,8 +719,10 @@ def max_dw_qk(dcsr, arg, dY, Q, K, O, act1, slope):
     R = max(int(lib.sir_max_dw_rows_parts(V, H)), 1)
     ldw = O * H + (O + 3) // 4 * 4
     wpart = torch.empty((R, ldw), device=Q.device, dtype=torch.float32)
+    # a graph without edges has no col storage; the kernel reads no column id then (every row is empty)
+    col = dcsr.col if dcsr.col.numel() else torch.zeros(1, dtype=torch.int32, device=Q.device)
     with _Timed("sir_max_dw_qk", Q.device):
-        rc = lib.sir_max_dw_qk(_ptr(dcsr.rowptr), _ptr(dcsr.col), V, _ptr(arg), arg.stride(0), _ptr(dY), dY.stride(0),
+        rc = lib.sir_max_dw_qk(_ptr(dcsr.rowptr), _ptr(col), V, _ptr(arg), arg.stride(0), _ptr(dY), dY.stride(0),
                                _ptr(Q), Q.stride(0), _ptr(K), K.stride(0), O, H, int(act1), float(slope), _ptr(wpart),
                                ldw, _stream(Q.device))
     _check(rc, lib)

@@ -40,7 +40,9 @@ backend ``nccl``):
   before the mask of its owner can apply.
 * **agg_type='max'** (``conv.py:46-47``): the halo K rows are gathered by the same chunked
   exchange (``HaloGather``, its backward the reverse exchange) and the fused max layer
-  (``edgemlp.EdgeMaxLinearQK``) runs on [own | halo] rows.
+  (``edgemlp.EdgeMaxLinearQK``) runs on [own | halo] rows.  Its Q / K dropout is the same hashed
+  mask (``HashedDropout``, seeds mixed with the rank's first global row), applied to the own rows
+  before the gather, so ranks seeded alike still draw independent masks.
 * **Autocast** (``DistSIRConvFunction16``): 16-bit K_ext rows, edge passes and both exchanges in
   the 16-bit type — half the wire bytes.
 * ``sym`` needs GLOBAL out-degrees: own-row out-degree histograms are completed by the same reverse
@@ -541,9 +543,11 @@ class _GradReducer:
         ts = [t for t in tensors if t is not None]
         if not ts:
             return
-        flat = torch.cat([t.reshape(-1) for t in ts])
         if hasattr(self.group, "all_to_all_rows"):
             raise NotImplementedError("reduce_in_backward needs a torch.distributed process group")
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return                  # one process: its partial sums are the gradients (as allreduce_grads)
+        flat = torch.cat([t.reshape(-1) for t in ts])
         if flat.is_cuda and not _host_staged(self.group, flat):
             work = dist.all_reduce(flat, group=self.group, async_op=True)     # RCCL, under the exchange
         else:
@@ -798,6 +802,21 @@ class DistEdgeAggregate(torch.autograd.Function):
         return dQ, dK, None, None, None, None, None, None, None, None
 
 
+class HashedDropout(torch.autograd.Function):
+    """Feature dropout (conv.py:60-61) with the hashed mask of ``drop`` = (seed, p) (``sir_dropout_apply``:
+    keep / scale decided per (local row, column) from the seed); the backward applies the same mask to
+    the gradient."""
+
+    @staticmethod
+    def forward(ctx, X, drop):
+        ctx.drop = drop
+        return _native.dropout_apply(X.contiguous().clone(), drop)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _native.dropout_apply(g.contiguous().clone(), ctx.drop), None
+
+
 class HaloGather(torch.autograd.Function):
     """K_ext = [K own rows | halo rows of the peers] (forward: the chunked alltoallv); backward: the
     halo rows' gradients go back to their owners (reverse alltoallv) and are added to the own rows per
@@ -869,8 +888,14 @@ class DistSIRConv(torch.nn.Module):
             from .edgemlp import EdgeMaxLinearQK, max_supported
             if not (feat.is_cuda and self.backend is _native and max_supported(H, c.linear_relation.out_features)):
                 raise NotImplementedError("DistSIRConv max: native GPU path only (H, O <= 512, H % 4 == 0)")
-            Q = c.dropout(c._linear(feat, c.linear_query.weight, c.linear_query.bias))
-            K = c.dropout(c._linear(feat, c.linear_key.weight, None))
+            Q = c._linear(feat, c.linear_query.weight, c.linear_query.bias)
+            K = c._linear(feat, c.linear_key.weight, None)
+            drop = self._drop(feat.device)
+            if drop is not None:
+                # the fused paths' hashed masks (seeds mixed with the rank's first global row): local
+                # row i of two ranks draws independent bits, as nn.Dropout over the whole [V, H] does
+                dq, dk = _drops(drop, dgraph.row_begin)
+                Q, K = HashedDropout.apply(Q, dq), HashedDropout.apply(K, dk)
             K_ext = HaloGather.apply(K, dgraph)
             return EdgeMaxLinearQK.apply(Q, K_ext, c.linear_relation.weight, c.linear_relation.bias, dgraph, act, slope)
         # training dropout inside the fused functions needs the native kernels on device tensors (the

@@ -284,8 +284,13 @@ def max_linear_backward(plan, Q, K, W, arg, dY, act1, slope, dQ, dK):
     if E * per_edge > budget and E > 0:
         # the [E, *] buffers exceed the budget: the same dataflow over destination-row ranges of
         # <= budget / per_edge edges each (the S2 shape: 123 GB of buffers -> 3 ranges of <= 48 GiB)
-        # range size quantised to 4 Mi edges (a stable cache key while the free memory moves)
-        e_max = max((budget // per_edge) >> 22 << 22, 1 << 20)
+        # range size quantised (a stable cache key while the free memory moves): to 4 Mi edges, below
+        # that to a power of two that still fits, at least 4 Ki edges (past the budget only then: warned)
+        e_fit = max(int(budget) // per_edge, 0)
+        e_max = e_fit >> 22 << 22 if e_fit >= 1 << 22 else 1 << max(e_fit.bit_length() - 1, 12)
+        if e_max > e_fit:
+            warnings.warn(f"max backward: {e_max} edges per row range need {e_max * per_edge / 2**30:.2f} GiB, "
+                          f"past the {budget / 2**30:.2f} GiB budget", RuntimeWarning)
         return _max_bwd_ranges(plan, Q, K, W, arg, dY, act1, slope, dQ, dK, e_max)
     return _max_bwd_materialised(plan.dst, plan.src, Q, K, W, arg, dY, act1, slope, dQ, dK)
 

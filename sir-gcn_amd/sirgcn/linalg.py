@@ -80,10 +80,31 @@ def mm_w(A, W, out=None):
     return torch.mm(A, W, out=out)
 
 
-def _pair_ok(A, W, W2):
-    return (USE_NATIVE and _ok(A) and A.shape[0] < DIRECT_ROWS
+def _lt_nt_env():
+    """``SIR_LT_NT`` as the library reads it (atoi; unset / empty: -1 = by shape)."""
+    e = os.environ.get("SIR_LT_NT", "")
+    if not e:
+        return -1
+    digits = e.strip()
+    n = len(digits) - len(digits.lstrip("+-"))
+    while n < len(digits) and digits[n].isdigit():
+        n += 1
+    try:
+        return int(digits[:n])
+    except ValueError:
+        return 0
+
+
+def _pair_ok(A, W, W2, trans):
+    """The two-part weight (``sir_gemm_nt_direct2``) runs only on the LDS-tiled kernel: the same
+    conditions as run_gemm_nt_direct's route to it (SIR_LT_NT != 0, every byte offset of a tile's
+    resource in 29 bits), else the caller takes the cat + pad route."""
+    K = A.shape[1]
+    return (USE_NATIVE and _ok(A) and A.shape[0] < DIRECT_ROWS and _lt_nt_env() != 0
+            and 128 * A.stride(0) < (1 << 29)
             and all(w.is_cuda and w.dtype == torch.float32 and w.dim() == 2 and w.stride(1) == 1
-                    and w.stride(0) % 4 == 0 and w.stride(0) <= MAX_LD and w.data_ptr() % 16 == 0 for w in (W, W2)))
+                    and w.stride(0) % 4 == 0 and w.stride(0) <= MAX_LD and w.data_ptr() % 16 == 0
+                    and (K * w.stride(0) if trans else 128 * w.stride(0)) < (1 << 29) for w in (W, W2)))
 
 
 def mm_wt_pair(A, W, W2, bias=None, drop=None):
@@ -92,7 +113,7 @@ def mm_wt_pair(A, W, W2, bias=None, drop=None):
     W.shape[0] outputs only (``sir_gemm_nt_direct2``) — no concatenated weight, no padded bias per
     step; elsewhere the cat + pad + :func:`mm_wt`."""
     n1 = W.shape[0]
-    if (_pair_ok(A, W, W2) and n1 % 4 == 0 and W2.shape[0] % 4 == 0
+    if (_pair_ok(A, W, W2, False) and n1 % 4 == 0 and W2.shape[0] % 4 == 0
             and (bias is None or (bias.is_cuda and bias.dtype == torch.float32 and bias.is_contiguous()
                                   and bias.data_ptr() % 16 == 0))):
         return _native.gemm_nt_direct2(A, W, W2, False, bias, n1 if bias is not None else 0, drop=drop)
@@ -103,7 +124,7 @@ def mm_wt_pair(A, W, W2, bias=None, drop=None):
 def mm_w_pair(A, W, W2):
     """A [W; W2] (the layer's dX = [dQ dK] [W_Q; W_K]): in place on the small-batch route, else the
     cat + :func:`mm_w`."""
-    if _pair_ok(A, W, W2) and W.shape[1] % 4 == 0:
+    if _pair_ok(A, W, W2, True) and W.shape[1] % 4 == 0:
         return _native.gemm_nt_direct2(A, W, W2, True)
     return mm_w(A, torch.cat([W, W2], 0))
 

@@ -276,3 +276,37 @@ def test_dropout_seeds_differ_across_ranks():
     assert int(q1[0]) != int(q0[0]) and int(k1[0]) != int(k0[0])
     a, b = _drops((42, 0.2), 0), _drops((42, 0.2), 77)
     assert a[0][0] == 42 and a[0][0] != b[0][0] and a[1][0] != b[1][0]
+
+
+@pytest.mark.parametrize("agg", ["sum", "sym"])
+def test_single_process_reduce_in_backward_without_process_group(agg):
+    """``DistSIRConv(reduce_in_backward=True)`` on one process with no process group (world 1, no halo
+    chunks): the in-backward reducer has nothing to reduce, as ``allreduce_grads`` (advisor r05 finding);
+    layer output and every gradient match the CPU oracle."""
+    import torch.distributed as dist
+    import oracle
+    from torch import nn
+    import cpu_edge_backend
+    from sirgcn import SIRConv
+    from sirgcn.dist import DistGraph, DistSIRConv
+    from sirgcn.synth import powerlaw_edges
+    assert not dist.is_initialized()
+    V, E, d, H, O = 300, 3000, 16, 40, 12
+    src, dst = powerlaw_edges(V, E, 0.8, seed=7)
+    X = torch.randn(V, d, generator=torch.Generator().manual_seed(1))
+    dY = torch.randn(V, O, generator=torch.Generator().manual_seed(2))
+    torch.manual_seed(3)
+    conv = SIRConv(d, H, O, nn.LeakyReLU(0.2), 0, agg_type=agg)
+    dg = DistGraph.from_global(src, dst, V, 0, 1, "cpu", chunk=64)
+    dconv = DistSIRConv(conv, backend=cpu_edge_backend, reduce_in_backward=True)
+    Xl = X.clone().requires_grad_(True)
+    Y = dconv(dg, Xl)
+    Y.backward(dY)
+    dconv.allreduce_grads()
+    w = [conv.linear_query.weight, conv.linear_query.bias, conv.linear_key.weight,
+         conv.linear_relation.weight, conv.linear_relation.bias]
+    ref = oracle.reference_cpu_step(src, dst, V, X, *[t.detach() for t in w], dY, agg, "leaky", 0.2)
+    assert_close(Y.detach(), ref["Y"], 1e-5, "Y")
+    assert_close(Xl.grad, ref["dX"], 1e-5, "dX")
+    for p, k in zip(w, ("dW_Q", "db_Q", "dW_K", "dW_R", "db_R")):
+        assert_close(p.grad, ref[k], 1e-5, k)

@@ -279,3 +279,45 @@ def test_edge_cut_max_vs_single_gpu(world):
     for k, v in got.items():
         e = float((v.double() - ref[k].double()).norm() / ref[k].double().norm().clamp_min(1e-30))
         assert e < (1e-6 if k == "Y" else 1e-5), (k, e)
+
+
+def test_edge_cut_max_training_dropout_hashed_per_rank():
+    """agg_type='max' on the edge-cut in training mode: Q / K dropout is the hashed mask of the
+    layer's two device seeds mixed with the rank's first global row (advisor r05: the module's
+    nn.Dropout gave ranks seeded alike identical masks for their local rows).  World 1: the layer
+    equals the explicit chain with those masks, forward and every gradient, bit for bit; a rank
+    starting at another row draws different bits."""
+    from sirgcn.dist import HaloGather, HashedDropout
+    from sirgcn.edgemlp import EdgeMaxLinearQK
+    V, E, H, O, p = 2000, 30000, 128, 64, 0.2
+    src, dst = powerlaw_edges(V, E, 0.8, seed=23)
+    X = torch.randn(V, 48, generator=torch.Generator().manual_seed(1)).to(DEV)
+    dY = torch.randn(V, O, generator=torch.Generator().manual_seed(2)).to(DEV)
+    torch.manual_seed(4)
+    conv = SIRConv(48, H, O, nn.LeakyReLU(0.2), p, agg_type="max").to(DEV).train()
+    dg = DistGraph.from_global(src, dst, V, 0, 1, DEV)
+    layer = DistSIRConv(conv)
+    xr = X.clone().requires_grad_(True)
+    torch.cuda.manual_seed(77)
+    Y = layer(dg, xr)
+    Y.backward(dY)
+    got = [Y.detach(), xr.grad] + [q.grad.clone() for q in conv.parameters()]
+    torch.cuda.manual_seed(77)
+    seeds = torch.randint(0, 2 ** 62, (2,), device=DEV, dtype=torch.int64)
+    dq, dk = _drops((seeds, p), dg.row_begin)
+    mq = _native.dropout_apply(torch.ones(V, H, device=DEV), dq)
+    assert 0.15 < float((mq == 0).float().mean()) < 0.25
+    other = _native.dropout_apply(torch.ones(V, H, device=DEV), _drops((seeds, p), 1000)[0])
+    assert not torch.equal(mq, other)
+    for q in conv.parameters():
+        q.grad = None
+    xe = X.clone().requires_grad_(True)
+    Q = HashedDropout.apply(conv._linear(xe, conv.linear_query.weight, conv.linear_query.bias), dq)
+    K = HashedDropout.apply(conv._linear(xe, conv.linear_key.weight, None), dk)
+    assert torch.equal(Q.detach() == 0, (mq == 0) | (Q.detach() == 0))
+    Ye = EdgeMaxLinearQK.apply(Q, HaloGather.apply(K, dg), conv.linear_relation.weight, conv.linear_relation.bias,
+                               dg, _native.ACT_LEAKY, 0.2)
+    Ye.backward(dY)
+    want = [Ye.detach(), xe.grad] + [q.grad for q in conv.parameters()]
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)

@@ -503,3 +503,25 @@ def test_max_hybrid_backward_matches_materialised(act, chunk, dw_qk, monkeypatch
         assert torch.equal(a[k], a2[k]), k
         e = float((a[k].double() - b[k].double()).norm() / b[k].double().norm().clamp_min(1e-30))
         assert e < 2e-6, (k, e)
+
+
+@pytest.mark.parametrize("V", [0, 37])
+def test_max_default_backward_empty_graph_zero_weight_grads(V):
+    """A graph without edges (an empty batch, an edge-cut rank with no rows) through the DEFAULT max
+    backward (the hybrid route, dW_R with Q / K recomputed): every partial the weight gradients are
+    summed from is written as zeros (advisor r05: the V == 0 partial was left unset), so dW_R / db_R and
+    every other gradient are exactly 0 — checked on a caching allocator primed with NaN blocks."""
+    from sirgcn.edgemlp import EdgeMaxLinear
+    assert EdgeMaxLinear.fused_bwd is None and EdgeMaxLinear.hybrid_bwd and EdgeMaxLinear.dw_qk
+    junk = [torch.full((1 << 16,) if i % 2 else (1 << 18,), float("nan"), device=DEV) for i in range(64)]
+    del junk
+    src = dst = torch.zeros(0, dtype=torch.int64)
+    torch.manual_seed(3)
+    m = SIRConv(32, 256, 256, nn.LeakyReLU(0.2), 0, agg_type="max").to(DEV)
+    X = torch.randn(V, 32, device=DEV).requires_grad_(True)
+    Y = m(Graph(src, dst, V), X)
+    Y.backward(torch.randn(V, 256, device=DEV))
+    assert Y.shape == (V, 256) and torch.equal(Y, torch.zeros_like(Y))
+    assert torch.equal(X.grad, torch.zeros_like(X))
+    for n, p in m.named_parameters():
+        assert p.grad is not None and torch.equal(p.grad, torch.zeros_like(p)), n

@@ -524,6 +524,26 @@ def test_gemm_nt_direct2_two_part_weight_bit_identical(M, n1, n2, K, trans):
         _native.gemm_nt_direct2(A, W[:0], W2, False)
 
 
+@pytest.mark.parametrize("lt", ["0", "-1"])
+def test_pair_projections_fall_back_off_the_lds_kernel(lt, monkeypatch):
+    """linalg.mm_wt_pair / mm_w_pair (the layer's QK and dX on small batches) take the two-part
+    weight only where the LDS-tiled kernel runs; with it switched off (SIR_LT_NT=0) they take the
+    cat + pad route instead of raising (advisor r05 finding) and return the same product."""
+    from sirgcn import linalg
+    monkeypatch.setenv("SIR_LT_NT", lt)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    M, d, H = 1582, 300, 300
+    X = torch.randn(M, d, device=DEV, generator=g)
+    WQ, WK = torch.randn(H, d, device=DEV, generator=g), torch.randn(H, d, device=DEV, generator=g)
+    bQ = torch.randn(H, device=DEV, generator=g)
+    qk = linalg.mm_wt_pair(X, WQ, WK, bQ)
+    ref = torch.cat([X.double() @ WQ.double().t() + bQ.double(), X.double() @ WK.double().t()], 1)
+    assert _rel(qk.double(), ref) < 1e-6
+    dQK = torch.randn(M, 2 * H, device=DEV, generator=g)
+    dX = linalg.mm_w_pair(dQK, WQ, WK)
+    assert _rel(dX.double(), dQK.double() @ torch.cat([WQ, WK], 0).double()) < 1e-6
+
+
 def test_gemm_nt_direct_dropout_epilogue_and_errors():
     """The QK dropout in the direct kernel's epilogue: the kept entries are exactly the undropped
     result times 1/(1-p), the same hashed mask as the packed-weight kernels, ~p dropped."""
