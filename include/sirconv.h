@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 14
+#define SIR_ABI_VERSION 15
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57).  SIR_AGG_ACCUMULATE,
  * OR'd into the forward's `agg` (SUM / SYM): S[v] = S[v] + the sum over the given items' edges, rows
@@ -295,6 +295,25 @@ int sir_edge_mlp_fwd_stream(const int32_t* rowptr, const int32_t* col, const int
                             int64_t ldk, const float* norm_row, const float* norm_col, int agg, int act1, float slope,
                             int act2, const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg,
                             int64_t lda, void* work, void* stream);
+
+/* agg='max' under autocast (heterophilous-datasets/train.py:75, ABI 15): Q / K rows stored in bf16 or fp16
+ * (dtype SIR_DTYPE_BF16 / F16, rows 8-B aligned, ld % 4 == 0).  z = Q[v] + K[u] and act1 in fp32, a
+ * rounded once to dtype, h = a W^T + b as ONE dtype MFMA per 16 k with fp32 accumulation on W and b
+ * rounded to dtype (autocast's half-precision Linear), the max and the first arg-max edge over the fp32
+ * h.  W packed by sir_edge_mlp_pack_st with the same dtype (sir_edge_mlp_pack_bytes bytes).  agg must be
+ * SIR_AGG_MAX, act2 IDENTITY; otherwise the arguments, outputs (fp32 out) and limits of sir_edge_mlp_fwd /
+ * sir_edge_mlp_fwd_stream. */
+int sir_edge_mlp_pack_st(const float* W, int64_t H, int64_t F, int dtype, void* packed, void* stream);
+int sir_edge_mlp_fwd_st(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                        const int32_t* splits, int64_t n_splits, int64_t H, int64_t F, const void* Q, int64_t ldq,
+                        const void* K, int64_t ldk, int dtype, int agg, int act1, float slope, int act2,
+                        const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda,
+                        float* pval, int32_t* parg, void* stream);
+int sir_edge_mlp_fwd_stream_st(const int32_t* rowptr, const int32_t* col, const int32_t* erow, int64_t n_rows,
+                               int64_t n_edges, int64_t H, int64_t F, const void* Q, int64_t ldq, const void* K,
+                               int64_t ldk, int dtype, int agg, int act1, float slope, int act2, const void* packed,
+                               const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda, void* work,
+                               void* stream);
 
 /* Backward of the SUM / MEAN / SYM form (H, F <= 256): the destination pass writes dQ [rows, H] and one
  * partial [dW (FP x HP) | db (FP)] row per block into wpart (FP = F rounded up to 32, HP = H rounded up

@@ -366,7 +366,7 @@ static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) 
 static int check_mlp(const char* fn, const int32_t* rowptr, const int32_t* items, int64_t n_items,
                      const int32_t* splits, int64_t n_splits, int64_t H, int64_t F, const float* Q, int64_t ldq,
                      const float* K, int64_t ldk, int agg, int act1, int act2, const void* packed,
-                     const float* norm_row, const float* norm_col, bool bwd) {
+                     const float* norm_row, const float* norm_col, bool bwd, bool rows16 = false) {
     if (agg < SIR_AGG_SUM || agg > SIR_AGG_MAX || (bwd && agg == SIR_AGG_MAX))
         return fail(SIR_EINVAL, fn, bwd ? "agg must be SUM, MEAN or SYM" : "agg must be SUM, MEAN, SYM or MAX");
     if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "unknown act1");
@@ -376,8 +376,13 @@ static int check_mlp(const char* fn, const int32_t* rowptr, const int32_t* items
     if (n_items < 0 || n_splits < 0 || n_items > INT32_MAX) return fail(SIR_EINVAL, fn, "bad item count");
     if (n_items > 0 && (rowptr == nullptr || items == nullptr || packed == nullptr || Q == nullptr || K == nullptr))
         return fail(SIR_EINVAL, fn, "NULL buffer");
-    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || !al16(Q) || !al16(K))
+    if (rows16) {      // 16-bit rows: 8-B aligned
+        if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || (reinterpret_cast<uintptr_t>(Q) & 7u) ||
+            (reinterpret_cast<uintptr_t>(K) & 7u))
+            return fail(SIR_EUNSUPPORTED, fn, "Q/K rows must be 8-B aligned (ld % 4 == 0, ld >= H)");
+    } else if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || !al16(Q) || !al16(K)) {
         return fail(SIR_EUNSUPPORTED, fn, "Q/K rows must be 16-B aligned (ld % 4 == 0, ld >= H)");
+    }
     if (n_splits > 0 && splits == nullptr) return fail(SIR_EINVAL, fn, "NULL splits");
     if (agg == SIR_AGG_SYM && n_items > 0 && (norm_row == nullptr || norm_col == nullptr))
         return fail(SIR_EINVAL, fn, "SYM needs norm_row and norm_col");
@@ -449,6 +454,70 @@ int sir_edge_mlp_fwd_stream(const int32_t* rowptr, const int32_t* col, const int
     a.Q = Q; a.ldq = ldq; a.K = K; a.ldk = ldk; a.norm_row = norm_row; a.norm_col = norm_col; a.slope = slope;
     a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.bias = bias;
     a.out = out; a.ldo = ldo; a.arg = arg; a.lda = lda; a.work = work;
+    return finish(fn, sir::run_mlp_fwd_stream(a, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_edge_mlp_pack_st(const float* W, int64_t H, int64_t F, int dtype, void* packed, void* stream) {
+    const char* fn = "sir_edge_mlp_pack_st";
+    if (H <= 0 || F <= 0 || H > 512 || F > 512) return fail(SIR_EINVAL, fn, "H <= 512, F <= 512");
+    if (dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "dtype must be BF16 or F16");
+    if (W == nullptr || packed == nullptr || !al16(packed)) return fail(SIR_EINVAL, fn, "NULL / unaligned buffer");
+    return finish(fn, sir::run_mlp_pack_st(W, (int)H, (int)F, dtype, packed, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+static int check_st(const char* fn, int dtype, int agg, int act2, const void* Q, int64_t ldq, const void* K, int64_t ldk,
+                    int64_t H) {
+    if (dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "dtype must be BF16 or F16");
+    if (agg != SIR_AGG_MAX || act2 != SIR_ACT_IDENTITY)
+        return fail(SIR_EUNSUPPORTED, fn, "16-bit storage: agg MAX and act2 IDENTITY only");
+    if (ldq < H || ldk < H || ldq % 4 || ldk % 4 || (reinterpret_cast<uintptr_t>(Q) & 7u) ||
+        (reinterpret_cast<uintptr_t>(K) & 7u))
+        return fail(SIR_EUNSUPPORTED, fn, "Q/K rows must be 8-B aligned (ld % 4 == 0, ld >= H)");
+    return SIR_OK;
+}
+
+int sir_edge_mlp_fwd_st(const int32_t* rowptr, const int32_t* col, const int32_t* items, int64_t n_items,
+                        const int32_t* splits, int64_t n_splits, int64_t H, int64_t F, const void* Q, int64_t ldq,
+                        const void* K, int64_t ldk, int dtype, int agg, int act1, float slope, int act2,
+                        const void* packed, const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda,
+                        float* pval, int32_t* parg, void* stream) {
+    const char* fn = "sir_edge_mlp_fwd_st";
+    int rc = check_st(fn, dtype, agg, act2, Q, ldq, K, ldk, H);
+    if (rc) return rc;
+    rc = check_mlp(fn, rowptr, items, n_items, splits, n_splits, H, F, static_cast<const float*>(Q), ldq,
+                   static_cast<const float*>(K), ldk, agg, act1, act2, packed, nullptr, nullptr, false, true);
+    if (rc) return rc;
+    if (n_items > 0 && (out == nullptr || ldo < F || arg == nullptr || lda < F)) return fail(SIR_EINVAL, fn, "out / arg");
+    if (n_splits > 0 && (pval == nullptr || parg == nullptr)) return fail(SIR_EINVAL, fn, "split rows need pval and parg");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr; a.col = col; a.items = items; a.n_items = n_items; a.splits = splits; a.n_splits = n_splits;
+    a.Q = static_cast<const float*>(Q); a.ldq = ldq; a.K = static_cast<const float*>(K); a.ldk = ldk;
+    a.slope = slope; a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.bias = bias;
+    a.out = out; a.ldo = ldo; a.arg = arg; a.lda = lda; a.pval = pval; a.parg = parg; a.st = dtype;
+    return finish(fn, sir::run_mlp_fwd(a, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
+}
+
+int sir_edge_mlp_fwd_stream_st(const int32_t* rowptr, const int32_t* col, const int32_t* erow, int64_t n_rows,
+                               int64_t n_edges, int64_t H, int64_t F, const void* Q, int64_t ldq, const void* K,
+                               int64_t ldk, int dtype, int agg, int act1, float slope, int act2, const void* packed,
+                               const float* bias, float* out, int64_t ldo, int32_t* arg, int64_t lda, void* work,
+                               void* stream) {
+    const char* fn = "sir_edge_mlp_fwd_stream_st";
+    int rc = check_st(fn, dtype, agg, act2, Q, ldq, K, ldk, H);
+    if (rc) return rc;
+    if (H != 256 || F <= 0 || F > 256) return fail(SIR_EUNSUPPORTED, fn, "H = 256, F <= 256");
+    if (n_rows < 0 || n_edges < 0 || n_edges >= INT32_MAX) return fail(SIR_EINVAL, fn, "bad sizes");
+    if (act1 < SIR_ACT_IDENTITY || act1 > SIR_ACT_GELU_TANH) return fail(SIR_EINVAL, fn, "act");
+    if (n_rows > 0 && (rowptr == nullptr || out == nullptr || ldo < F || packed == nullptr || work == nullptr ||
+                       arg == nullptr || lda < F))
+        return fail(SIR_EINVAL, fn, "NULL buffer / ldo / lda");
+    if (n_edges > 0 && (col == nullptr || erow == nullptr || Q == nullptr || K == nullptr))
+        return fail(SIR_EINVAL, fn, "NULL col / erow / Q / K");
+    sir::EdgeMlpArgs a{};
+    a.rowptr = rowptr; a.col = col; a.erow = erow; a.n_rows = n_rows; a.n_edges = n_edges;
+    a.Q = static_cast<const float*>(Q); a.ldq = ldq; a.K = static_cast<const float*>(K); a.ldk = ldk;
+    a.slope = slope; a.H = (int)H; a.HP = (int)((H + 7) / 8 * 8); a.F = (int)F; a.Wp = packed; a.bias = bias;
+    a.out = out; a.ldo = ldo; a.arg = arg; a.lda = lda; a.work = work; a.st = dtype;
     return finish(fn, sir::run_mlp_fwd_stream(a, agg, act1, act2, static_cast<hipStream_t>(stream)), nullptr);
 }
 

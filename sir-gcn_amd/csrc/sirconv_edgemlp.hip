@@ -108,16 +108,53 @@ k_mlp_pack16(const float* __restrict__ W, int H, int F, int NG, _Float16* __rest
     if (l == 0) inv[n] = (n < F) ? mlp_pow2(-se) : 0.f;
 }
 
+// 16-bit storage (autocast, SIR_DTYPE_BF16 / F16): Q / K rows are read in the storage type (half the gather
+// bytes of fp32 rows), z and act1 are evaluated in fp32, a is rounded once to the storage type (autocast's
+// half-precision message) and h = a W^T runs as ONE 16-bit MFMA per 16 k on W rounded to it (autocast's
+// W.to(dtype); k_mlp_pack_st) with fp32 accumulation — the half-precision Linear of the reference's AMP
+// path, no operand split.
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+template <int ST>
+__device__ __forceinline__ mf16 mfma16_st(h8v a, h8v b, mf16 c) {
+    if constexpr (ST == ST_BF16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, a), __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// four fp32 values rounded to the storage type, as 8 B (the a image of the 16-bit forms)
+template <int ST>
+__device__ __forceinline__ uint2 pack4_st(float4 a) {
+    return make_uint2(f2h<ST>(a.x) | (f2h<ST>(a.y) << 16), f2h<ST>(a.z) | (f2h<ST>(a.w) << 16));
+}
+// the weight of the 16-bit forms in k_mlp_pack16's layout: plane 0 = W rounded to the storage type,
+// plane 1 = 0, inverse scales 1 (0 past F)
+template <int ST>
+__global__ void __launch_bounds__(64)
+k_mlp_pack_st(const float* __restrict__ W, int H, int F, int NG, uint16_t* __restrict__ out16, float* __restrict__ inv) {
+    const int n = blockIdx.x, l = threadIdx.x;
+    const int t = n >> 5, r = n & 31;
+    for (int k = l; k < NG * 16; k += 64) {
+        const float x = (n < F && k < H) ? W[(int64_t)n * H + k] : 0.f;
+        const int g = k >> 4, h = (k >> 3) & 1, j = k & 7;
+        const int lane = h * 32 + r;
+        out16[(((int64_t)t * NG + g) * 2 + 0) * 512 + lane * 8 + j] = (uint16_t)f2h<ST>(x);
+        out16[(((int64_t)t * NG + g) * 2 + 1) * 512 + lane * 8 + j] = 0;
+    }
+    if (l == 0) inv[n] = (n < F) ? 1.f : 0.f;
+}
+
 // RPW = rows of the 32-edge tile per wave (32 / NW), C4 = float4 chunks of 256 features per row (HP16 / 256)
-template <int ACT1, int ACT2, int RED, int NW, int TPW, int C4>
+template <int ACT1, int ACT2, int RED, int NW, int TPW, int C4, int ST = ST_F32>
 __global__ void __launch_bounds__(64 * NW)
 k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const int4* __restrict__ items,
-            const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
+            const typename Stor<ST>::T* __restrict__ Q, int64_t ldq, const typename Stor<ST>::T* __restrict__ K,
+            int64_t ldk,
             const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope,
             int H, int NG, int F, const h8v* __restrict__ Wp16, const float* __restrict__ winv,
             const float* __restrict__ bias, float* __restrict__ out, int64_t ldo, int* __restrict__ arg, int64_t lda,
             float* __restrict__ pval, int* __restrict__ parg) {
     constexpr int RPW = 32 / NW;
+    constexpr bool X16 = ST != ST_F32;                 // 16-bit storage: one image, one MFMA per 16 k
     extern __shared__ float smem[];
     char* const img = reinterpret_cast<char*>(smem);                // [NG][2][32 rows fimg] halves
     float* const sInv = reinterpret_cast<float*>(img + NG * 2048);  // [32] 2^-se of the edge rows
@@ -127,7 +164,7 @@ k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     const int4 it = uniform_item(items, blockIdx.x);
     const int row = it.x, e0 = it.y, e1 = it.z, slot = it.w;
     const float nr = (RED == AGG_SYM) ? norm_row[row] : 1.f;
-    const float* qp = Q + (int64_t)row * ldq;
+    const auto* qp = Q + (int64_t)row * ldq;
     const int ntile = (F + 31) / 32;
 
     float racc[TPW], best[TPW], bb[TPW], iw[TPW];
@@ -136,14 +173,20 @@ k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const i
     for (int j = 0; j < TPW; ++j) {
         racc[j] = 0.f; best[j] = -INFINITY; bidx[j] = INT_MAX;
         const int n = 32 * (w + NW * j) + (l & 31);
-        bb[j] = (bias != nullptr && n < F) ? bias[n] : 0.f;
+        bb[j] = (bias != nullptr && n < F) ? round_st<ST>(bias[n]) : 0.f;
         iw[j] = (n < F) ? winv[n] : 0.f;
     }
     float4 q4[C4];
 #pragma unroll
     for (int c = 0; c < C4; ++c) {
         const int k = 256 * c + 4 * l;
-        q4[c] = (k < H) ? *reinterpret_cast<const float4*>(qp + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (X16) {
+            float t4[4] = {0.f, 0.f, 0.f, 0.f};
+            if (k < H) tload_p<ST, 4, false>(t4, qp + k);
+            q4[c] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+        } else {
+            q4[c] = (k < H) ? *reinterpret_cast<const float4*>(qp + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
 
     for (int t0 = e0; t0 < e1; t0 += 32) {
@@ -157,8 +200,14 @@ k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const i
 #pragma unroll
             for (int c = 0; c < C4; ++c) {
                 const int k = 256 * c + 4 * l;
-                kv[ii][c] = (k < H) ? *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k)
-                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (X16) {
+                    float t4[4] = {0.f, 0.f, 0.f, 0.f};
+                    if (k < H) tload_p<ST, 4, false>(t4, K + (int64_t)u * ldk + k);
+                    kv[ii][c] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+                } else {
+                    kv[ii][c] = (k < H) ? *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
             }
         }
 #pragma unroll
@@ -175,6 +224,18 @@ k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const i
                 a4[c].z = ok ? act_f<ACT1>(q4[c].z + kv[ii][c].z, slope) : 0.f;
                 a4[c].w = ok ? act_f<ACT1>(q4[c].w + kv[ii][c].w, slope) : 0.f;
                 m = fmaxf(m, fmaxf(fmaxf(fabsf(a4[c].x), fabsf(a4[c].y)), fmaxf(fabsf(a4[c].z), fabsf(a4[c].w))));
+            }
+            if constexpr (X16) {
+#pragma unroll
+                for (int c = 0; c < C4; ++c) {
+                    const int k = 256 * c + 4 * l;
+                    if (k < NG * 16) {
+                        const int g = k >> 4, h = (k >> 3) & 1, j8 = k & 7;
+                        *reinterpret_cast<uint2*>(img + g * 2048 + mlp_fimg(i, h) + j8 * 2) = pack4_st<ST>(a4[c]);
+                    }
+                }
+                if (l == 0) sInv[i] = 1.f;
+                continue;
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
@@ -211,16 +272,20 @@ k_mlp_fwd16(const int* __restrict__ rowptr, const int* __restrict__ col, const i
         const int fo = mlp_fimg(l & 31, l >> 5);
         for (int g = 0; g < NG; ++g) {
             const h8v ahi = *reinterpret_cast<const h8v*>(img + g * 2048 + fo);
-            const h8v alo = *reinterpret_cast<const h8v*>(img + g * 2048 + 1024 + fo);
+            const h8v alo = X16 ? h8v{} : *reinterpret_cast<const h8v*>(img + g * 2048 + 1024 + fo);
 #pragma unroll
             for (int j = 0; j < TPW; ++j) {
                 const int t = w + NW * j;
                 if (t >= ntile) continue;            // wave-uniform: tiles past F have no packed W
                 const h8v whi = Wp16[(((int64_t)t * NG + g) * 2 + 0) * 64 + l];
-                const h8v wlo = Wp16[(((int64_t)t * NG + g) * 2 + 1) * 64 + l];
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo, acc[j], 0, 0, 0);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi, acc[j], 0, 0, 0);
+                if constexpr (X16) {
+                    acc[j] = mfma16_st<ST>(ahi, whi, acc[j]);
+                } else {
+                    const h8v wlo = Wp16[(((int64_t)t * NG + g) * 2 + 1) * 64 + l];
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo, acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi, acc[j], 0, 0, 0);
+                }
             }
         }
         // ---- m = act2(h + b), reduced in edge order within the lane
@@ -690,15 +755,17 @@ k_mlp_fwd16q(const int* __restrict__ col, const int4* __restrict__ items, int64_
 // k_mlp_stream_combine merges the slots of each row in block (= edge) order; rows with no edge are
 // written by k_mlp_empty_rows.  H = 256 (the S1 / S2 shape), F <= 256; the rest is k_mlp_fwd16q's
 // pipeline (weights in registers, two images, next tile's gathers in flight).
-template <int ACT1, int ACT2, int RED>
+template <int ACT1, int ACT2, int RED, int ST = ST_F32>
 __global__ void __launch_bounds__(512)
 k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const int* __restrict__ rowptr, int64_t E,
-             const float* __restrict__ Q, int64_t ldq, const float* __restrict__ K, int64_t ldk,
+             const typename Stor<ST>::T* __restrict__ Q, int64_t ldq, const typename Stor<ST>::T* __restrict__ K,
+             int64_t ldk,
              const float* __restrict__ norm_row, const float* __restrict__ norm_col, float slope, int F,
              const h8v* __restrict__ Wp16, const float* __restrict__ winv, const float* __restrict__ bias,
              float* __restrict__ out, int64_t ldo, int* __restrict__ arg, int64_t lda, float* __restrict__ pval,
              int* __restrict__ parg, int* __restrict__ prow) {
     constexpr int NW = 8, RPW = 4, NG = 16, MP = 36;   // MP: pitch of the m tile (floats), bank-rotating
+    constexpr bool X16 = ST != ST_F32;                 // 16-bit storage: one image, one MFMA per 16 k
     __shared__ __attribute__((aligned(16))) char img[2][NG * 2048];
     __shared__ __attribute__((aligned(16))) float sInv[2][32];
     __shared__ __attribute__((aligned(16))) float sC[2][32];
@@ -713,7 +780,8 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
     const int row_after = ee < E ? erow[ee] : -1;            // ... into the next block
     const int n = 32 * w + (l & 31);
     const bool fo_ok = (l < 32) && n < F;                    // the lane that owns feature n's walk / stores
-    const float bbv = (bias != nullptr && n < F) ? bias[n] : 0.f;
+    // 16-bit forms: the bias rounded to the storage type (autocast's bias.to(dtype))
+    const float bbv = (bias != nullptr && n < F) ? round_st<ST>(bias[n]) : 0.f;
     const float iwv = (n < F) ? winv[n] : 0.f;
     h8v whi[NG], wlo[NG];
     const bool has_t = w < (F + 31) / 32;
@@ -721,7 +789,7 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
     for (int g = 0; g < NG; ++g) {
         if (has_t) {
             whi[g] = Wp16[(((int64_t)w * NG + g) * 2 + 0) * 64 + l];
-            wlo[g] = Wp16[(((int64_t)w * NG + g) * 2 + 1) * 64 + l];
+            wlo[g] = X16 ? h8v{} : Wp16[(((int64_t)w * NG + g) * 2 + 1) * 64 + l];
         } else {
             whi[g] = h8v{};
             wlo[g] = h8v{};
@@ -746,8 +814,16 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
         for (int ii = 0; ii < RPW; ++ii) {
             const int u = __builtin_amdgcn_readlane(colv, w + NW * ii);
             const int r = __builtin_amdgcn_readlane(rowv, w + NW * ii);
-            kv[ii] = *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k4);
-            qv[ii] = *reinterpret_cast<const float4*>(Q + (int64_t)r * ldq + k4);
+            if constexpr (X16) {
+                float t4[4];
+                tload_p<ST, 4, false>(t4, K + (int64_t)u * ldk + k4);
+                kv[ii] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+                tload_p<ST, 4, false>(t4, Q + (int64_t)r * ldq + k4);
+                qv[ii] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+            } else {
+                kv[ii] = *reinterpret_cast<const float4*>(K + (int64_t)u * ldk + k4);
+                qv[ii] = *reinterpret_cast<const float4*>(Q + (int64_t)r * ldq + k4);
+            }
         }
         if constexpr (RED == AGG_SYM) cn = norm_col[colv] * norm_row[rowv];   // conv.py:45 operand order
     };
@@ -761,6 +837,12 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
             a4.y = ok ? act_f<ACT1>(qv[ii].y + kv[ii].y, slope) : 0.f;
             a4.z = ok ? act_f<ACT1>(qv[ii].z + kv[ii].z, slope) : 0.f;
             a4.w = ok ? act_f<ACT1>(qv[ii].w + kv[ii].w, slope) : 0.f;
+            if constexpr (X16) {
+                const int g = k4 >> 4, h = (k4 >> 3) & 1, j8 = k4 & 7;
+                *reinterpret_cast<uint2*>(img[bf] + g * 2048 + mlp_fimg(i, h) + j8 * 2) = pack4_st<ST>(a4);
+                if (l == 0) sInv[bf][i] = 1.f;
+                continue;
+            }
             const float m = wave_max64(fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w))));
             const int se = mlp_scale_exp(m);
             const float sc = mlp_pow2(se);
@@ -798,10 +880,14 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             const h8v ahi = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + fo);
-            const h8v alo = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + 1024 + fo);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
+            if constexpr (X16) {
+                acc = mfma16_st<ST>(ahi, whi[g], acc);
+            } else {
+                const h8v alo = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + 1024 + fo);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);
+            }
         }
         stage(bf ^ 1, tile_nv(j + 1));
         const int colv3 = col[edge_of(j + 3)], rowv3 = erow[edge_of(j + 3)];
@@ -1209,6 +1295,31 @@ int64_t mlp_pack16_bytes(int H, int F) {
 #define SIR_MLP_PIPE 1          // 1: 128 < H <= 256, F <= 256 on k_mlp_fwd16q (S1 max forward 13.69 -> 10.02 ms,
                                 // profiles/r04_ab_mlp_fwd.txt; at H <= 128 k_mlp_fwd16p stays faster)
 #endif
+// the 16-bit storage forms (max, act2 = identity) on k_mlp_fwd16
+template <int ACT1, int ST>
+hipError_t mlp_fwd16_st(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
+    const int NG = mlp_ng(a.H), FP = (a.F + 31) / 32 * 32;
+    const h8v* w16 = static_cast<const h8v*>(p16);
+    const float* winv = reinterpret_cast<const float*>(static_cast<const char*>(p16) + (int64_t)FP * NG * 64);
+    const auto* Q = reinterpret_cast<const typename Stor<ST>::T*>(a.Q);
+    const auto* K = reinterpret_cast<const typename Stor<ST>::T*>(a.K);
+    const size_t lds = (size_t)NG * 2048 + 64 * sizeof(float);
+#define SIR_MLP_FWD16S(NWV, TPWV, C4V)                                                                           \
+    hipLaunchKernelGGL((k_mlp_fwd16<ACT1, ACT_IDENTITY, 3, NWV, TPWV, C4V, ST>), grid, dim3(64 * NWV), lds, st,    \
+                       a.rowptr, a.col, reinterpret_cast<const int4*>(a.items), Q, a.ldq, K, a.ldk, a.norm_row,    \
+                       a.norm_col, a.slope, a.H, NG, a.F, w16, winv, a.bias, a.out, a.ldo, a.arg, a.lda, a.pval,   \
+                       a.parg)
+    if (NG * 16 <= 256) {
+        if (nt <= 4) SIR_MLP_FWD16S(4, 1, 1);
+        else SIR_MLP_FWD16S(8, 2, 1);
+    } else {
+        if (nt <= 8) SIR_MLP_FWD16S(4, 2, 2);
+        else SIR_MLP_FWD16S(8, 2, 2);
+    }
+#undef SIR_MLP_FWD16S
+    return hipGetLastError();
+}
+
 template <int ACT1, int ACT2, int RED>
 hipError_t mlp_fwd16_nt(int nt, dim3 grid, hipStream_t st, const EdgeMlpArgs& a, const void* p16) {
     const int NG = mlp_ng(a.H), FP = (a.F + 31) / 32 * 32;
@@ -1352,14 +1463,37 @@ hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t 
     return hipGetLastError();
 }
 
+hipError_t run_mlp_pack_st(const float* W, int H, int F, int dtype, void* packed, hipStream_t st) {
+    if (dtype != ST_BF16 && dtype != ST_F16) return hipErrorInvalidValue;
+    const int FP = (F + 31) / 32 * 32, NG = mlp_ng(H);
+    char* p16 = static_cast<char*>(packed) + mlp_pack32_floats(H, F) * 4;
+    uint16_t* o16 = reinterpret_cast<uint16_t*>(p16);
+    float* inv = reinterpret_cast<float*>(p16 + (int64_t)FP * NG * 64);
+    if (dtype == ST_BF16)
+        hipLaunchKernelGGL(k_mlp_pack_st<ST_BF16>, dim3((unsigned)FP), dim3(64), 0, st, W, H, F, NG, o16, inv);
+    else
+        hipLaunchKernelGGL(k_mlp_pack_st<ST_F16>, dim3((unsigned)FP), dim3(64), 0, st, W, H, F, NG, o16, inv);
+    return hipGetLastError();
+}
+
 hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st) {
+    if (a.st != ST_F32 && (red != 3 || act2 != ACT_IDENTITY)) return hipErrorInvalidValue;
     if (a.n_items > 0) {
         if (a.H > 512) return hipErrorInvalidValue;           // the ABI's limit (sirconv.h)
         const int nt = (a.F + 31) / 32;
         const dim3 grid((unsigned)a.n_items);
-        hipError_t err = by_acts(act1, act2, [&](auto A1, auto A2) {
-            return mlp_fwd16_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, st, a, mlp_p16(a.Wp, a.H, a.F));
-        });
+        hipError_t err;
+        if (a.st != ST_F32)
+            err = by_acts(act1, ACT_IDENTITY, [&](auto A1, auto) {
+                constexpr int X1 = decltype(A1)::value;
+                return a.st == ST_BF16 ? mlp_fwd16_st<X1, ST_BF16>(nt, grid, st, a, mlp_p16(a.Wp, a.H, a.F))
+                                       : mlp_fwd16_st<X1, ST_F16>(nt, grid, st, a, mlp_p16(a.Wp, a.H, a.F));
+            });
+        else
+            err = by_acts(act1, act2, [&](auto A1, auto A2) {
+                return mlp_fwd16_red<decltype(A1)::value, decltype(A2)::value>(red, nt, grid, st, a,
+                                                                               mlp_p16(a.Wp, a.H, a.F));
+            });
         if (err != hipSuccess) return err;
     }
     if (a.n_splits > 0) {
@@ -1402,6 +1536,25 @@ hipError_t run_mlp_fwd_stream(const EdgeMlpArgs& a, int red, int act1, int act2,
                        a.F, a.out, a.ldo, red == 3 ? a.arg : nullptr, a.lda);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess || a.n_edges == 0) return err;
+    if (a.st != ST_F32) {
+        if (red != 3 || act2 != ACT_IDENTITY) return hipErrorInvalidValue;
+        return by_acts(act1, ACT_IDENTITY, [&](auto A1, auto) {
+            constexpr int X1 = decltype(A1)::value;
+            auto launch = [&](auto S) {
+                constexpr int SV = decltype(S)::value;
+                using T = typename Stor<SV>::T;
+                hipLaunchKernelGGL((k_mlp_fwd16r<X1, ACT_IDENTITY, 3, SV>), dim3((unsigned)nb), dim3(512), 0, st, a.col,
+                                   a.erow, a.rowptr, a.n_edges, reinterpret_cast<const T*>(a.Q), a.ldq,
+                                   reinterpret_cast<const T*>(a.K), a.ldk, a.norm_row, a.norm_col, a.slope, a.F, w16,
+                                   winv, a.bias, a.out, a.ldo, a.arg, a.lda, pval, parg, prow);
+                hipLaunchKernelGGL((k_mlp_stream_combine<3>), dim3(1), dim3(256), 0, st, pval, parg, prow, slots, a.F,
+                                   a.rowptr, a.out, a.ldo, a.arg, a.lda);
+                return hipGetLastError();
+            };
+            return a.st == ST_BF16 ? launch(std::integral_constant<int, ST_BF16>())
+                                   : launch(std::integral_constant<int, ST_F16>());
+        });
+    }
     err = by_acts(act1, act2, [&](auto A1, auto A2) {
         constexpr int X1 = decltype(A1)::value, X2 = decltype(A2)::value;
         auto launch = [&](auto R) {

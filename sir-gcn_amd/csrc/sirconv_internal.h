@@ -147,11 +147,15 @@ struct EdgeMlpArgs {
     const int* erow;
     int64_t n_rows, n_edges;
     void* work;
+    // forward: storage type of Q / K (ST_F32, or ST_BF16 / ST_F16 with the 16-bit weight of run_mlp_pack_st:
+    // max reduce, act2 = identity only; Q / K then point at 16-bit rows)
+    int st = 0;
 };
 int64_t mlp_stream_work_bytes(int F);
 hipError_t run_mlp_fwd_stream(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st);
 int64_t mlp_pack_floats(int H, int F);
 hipError_t run_mlp_pack(const float* W, int H, int F, void* packed, hipStream_t st);
+hipError_t run_mlp_pack_st(const float* W, int H, int F, int dtype, void* packed, hipStream_t st);
 hipError_t run_mlp_fwd(const EdgeMlpArgs& a, int red, int act1, int act2, hipStream_t st);
 int mlp_bwd_blocks(int64_t n_items, int H, int F);
 hipError_t run_mlp_bwd(const EdgeMlpArgs& a, bool dst, int red, int act1, int act2, hipStream_t st);

@@ -656,9 +656,15 @@ done:
 // two barriers.  Same per-lane order of terms (rows ascending, the arg edge's activation recomputed with the
 // same operations): bit-identical to k_max_dw_qk.
 constexpr int MDW2_ROWS = 16, MDW2_EDGES = 128, MDW2_WIN = 1024;
+#ifndef SIR_MAXDW2_OCC
+#define SIR_MAXDW2_OCC 2        // blocks per CU the register budget is held to (2: <= 128 VGPRs; LDS fits two)
+#endif
 
+// waves per SIMD the register budget is held to: two blocks a CU (<= 128 VGPRs) but for the GELU forms,
+// whose erf code would spill there (one block, <= 256)
+constexpr int mdw2_wpe(int act) { return (act == ACT_GELU || act == ACT_GELU_TANH) ? 2 : 2 * SIR_MAXDW2_OCC; }
 template <int ACT1>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(mdw2_wpe(ACT1))))
 k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ arg, int64_t lda,
              const float* __restrict__ dY, int64_t ldy, const float* __restrict__ Q, int64_t ldq,
              const float* __restrict__ K, int64_t ldk, int V, int O, int H, float slope, int rows_per,
@@ -672,6 +678,8 @@ k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const 
     __shared__ float sY[NR * 256];
     __shared__ int sRp[WIN + 1];                             // rowptr[wb .. wb + WIN]
     __shared__ int sB[NR + 1];                               // the staged batch's row bounds
+    __shared__ float sZ[64];                                 // a zero row: lanes without a term read it
+    __shared__ float4 sQ[2][NR * 16];                        // Q quads of the staged batch's rows (by parity)
     const int t = threadIdx.x;
     const int o = t & 255, hc = t >> 8;                      // output, half of the 64-column block
     const bool ook = o < O;
@@ -699,9 +707,12 @@ k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const 
         if (!hub)
             while (be < r1 && be - br < NR && rp(be + 1) - base <= NE) ++be;
     };
-    // this thread's staging edges e_k = t / 16 + 32 k: column ids and rows (a merge walk over the bounds)
-    auto load_cols = [&](int br, int be, bool hub, int* cn, int* rn) {
+    // this thread's staging edges e_k = t / 16 + 32 k: column ids and rows (a merge walk over the bounds);
+    // threads t < 16 NR also fetch quad t % 16 of the batch's row t / 16 of Q (staged in LDS one batch later)
+    auto load_cols = [&](int br, int be, bool hub, int* cn, int* rn, float4& qn) {
         const int base = rp(br), ne = rp(be) - base;
+        const int qr = br + (t >> 4);
+        qn = (t < 16 * NR && !hub && qr < be && qok) ? ld4(Q + (int64_t)qr * ldq + c0 + 4 * qq) : zero4;
         int j = br;
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
@@ -712,12 +723,11 @@ k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const 
             rn[k] = j;
         }
     };
-    auto load_qk = [&](const int* cn, const int* rn, float4* kq, float4* qv) {
+    auto load_k = [&](const int* cn, float4* kq) {
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             const bool ok = cn[k] >= 0 && qok;
             kq[k] = ok ? ld4(K + (int64_t)cn[k] * ldk + c0 + 4 * qq) : zero4;
-            qv[k] = ok ? ld4(Q + (int64_t)rn[k] * ldq + c0 + 4 * qq) : zero4;
         }
     };
     // staged pairs of this thread: (row br + hc + 2 k, output o)
@@ -730,33 +740,43 @@ k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const 
         }
     };
     if (r0 >= r1) goto done;
+    if (t < 64) sZ[t] = 0.f;                                 // visible after fill()'s barrier
     {
         fill();
         int br = r0, be, bn, ben;
         bool hub, hubn;
-        int cn[EPT], rn[EPT], na[APT];
+        int cn[EPT], rn[EPT], rc[EPT], na[APT];
         float ny[APT];
-        float4 kq[EPT], qv[EPT];
+        float4 kq[EPT], qn;
+        int par = 0;                                         // parity of the batch being staged
         form(br, be, hub);
-        load_cols(br, be, hub, cn, rn);
-        load_qk(cn, rn, kq, qv);
+        load_cols(br, be, hub, cn, rn, qn);
+        if (t < 16 * NR) sQ[0][t] = qn;
+        __syncthreads();
+        load_k(cn, kq);
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) rc[k] = rn[k] - br;
         load_args(br, be, na, ny);
         bn = be;
+        qn = zero4;
         if (bn < r1) {
             if (bn + NR + 1 > wb + WIN) { __syncthreads(); wb = bn; fill(); }
             form(bn, ben, hubn);
-            load_cols(bn, ben, hubn, cn, rn);
+            load_cols(bn, ben, hubn, cn, rn, qn);
         }
         while (br < r1) {
             // stage batch (br, be): a = act1(Q[v] + K[u]), arg / dY, row bounds
 #pragma unroll
             for (int k = 0; k < EPT; ++k) {
                 const int e = (t >> 4) + 32 * k;
+                const float4 qv = sQ[par][rc[k] * 16 + qq];
                 float4 a;
-                a.x = sig<ACT1>(qv[k].x + kq[k].x, slope); a.y = sig<ACT1>(qv[k].y + kq[k].y, slope);
-                a.z = sig<ACT1>(qv[k].z + kq[k].z, slope); a.w = sig<ACT1>(qv[k].w + kq[k].w, slope);
+                a.x = sig<ACT1>(qv.x + kq[k].x, slope); a.y = sig<ACT1>(qv.y + kq[k].y, slope);
+                a.z = sig<ACT1>(qv.z + kq[k].z, slope); a.w = sig<ACT1>(qv.w + kq[k].w, slope);
                 *reinterpret_cast<float4*>(&sA[e * PITCH + 4 * qq]) = a;
             }
+            if (t < 16 * NR) sQ[par ^ 1][t] = qn;                // the next batch's Q rows
+            par ^= 1;
 #pragma unroll
             for (int k = 0; k < APT; ++k) {
                 sArg[(hc + 2 * k) * 256 + o] = na[k];
@@ -769,22 +789,41 @@ k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const 
             // next batch: its K / Q columns and arg / dY in flight; the one after: its column ids
             br = bn; be = ben; hub = hubn;
             if (br < r1) {
-                load_qk(cn, rn, kq, qv);
+                load_k(cn, kq);
+#pragma unroll
+                for (int k = 0; k < EPT; ++k) rc[k] = rn[k] - br;
                 load_args(br, be, na, ny);
                 bn = be;
                 if (bn < r1) {
                     if (bn + NR + 1 > wb + WIN) { __syncthreads(); wb = br; fill(); }
                     form(bn, ben, hubn);
-                    load_cols(bn, ben, hubn, cn, rn);
+                    load_cols(bn, ben, hubn, cn, rn, qn);
                 }
             }
             const int base = sB[0];
-            for (int j = 0; j < cbe - cbr; ++j) {
+            if (!chub) {
+                // branch-free over the lanes: a lane without a term (empty row, o >= O) multiplies the
+                // zero row by 0 (adds +0: the same values as skipping it, -0 sums aside)
+                for (int j = 0; j < cbe - cbr; ++j) {
+                    const int a = sArg[j * 256 + o];
+                    const bool ok = ook && a >= sB[j] && a < sB[j + 1];
+                    const float y = ok ? sY[j * 256 + o] : 0.f;
+                    if (hc == 0) db += y;
+                    const float* ap = ok ? &sA[(a - base) * PITCH + cl] : &sZ[cl];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
+                        acc[q].x = fmaf(y, v.x, acc[q].x); acc[q].y = fmaf(y, v.y, acc[q].y);
+                        acc[q].z = fmaf(y, v.z, acc[q].z); acc[q].w = fmaf(y, v.w, acc[q].w);
+                    }
+                }
+            }
+            for (int j = 0; chub && j < cbe - cbr; ++j) {
                 const int a = sArg[j * 256 + o];
                 if (!ook || a < sB[j] || a >= sB[j + 1]) continue;    // no arg edge (empty row)
                 const float y = sY[j * 256 + o];
                 if (hc == 0) db += y;
-                if (chub) {                                           // hub row: the arg edge's K row
+                {                                                     // hub row: the arg edge's K row
                     const int u = col[a];
                     const float* kp = K + (int64_t)u * ldk + c0 + cl;
                     const float* qp = Q + (int64_t)(cbr + j) * ldq + c0 + cl;
@@ -797,14 +836,6 @@ k_max_dw_qk2(const int* __restrict__ rowptr, const int* __restrict__ col, const 
                             acc[q].z = fmaf(y, sig<ACT1>(qv4.z + kv.z, slope), acc[q].z);
                             acc[q].w = fmaf(y, sig<ACT1>(qv4.w + kv.w, slope), acc[q].w);
                         }
-                    }
-                } else {
-                    const float* ap = &sA[(a - base) * PITCH + cl];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
-                        acc[q].x = fmaf(y, v.x, acc[q].x); acc[q].y = fmaf(y, v.y, acc[q].y);
-                        acc[q].z = fmaf(y, v.z, acc[q].z); acc[q].w = fmaf(y, v.w, acc[q].w);
                     }
                 }
             }

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("SIRGCN_LIB") or os.path.join(os.path.dirname(os.path.
 AGG = {"sum": 0, "mean": 1, "sym": 2}
 ACT_IDENTITY, ACT_RELU, ACT_LEAKY, ACT_GELU, ACT_GELU_TANH = range(5)
 DTYPE_F32, DTYPE_BF16, DTYPE_F16 = 0, 1, 2
-ABI_VERSION = 14
+ABI_VERSION = 15
 STORAGE = {torch.float32: DTYPE_F32, torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}
 
 # exported symbol -> (restype, argtypes); mirrors include/sirconv.h
@@ -77,6 +77,11 @@ SIGNATURES = {
     "sir_edge_mlp_stream_work_bytes": (ctypes.c_int64, [_I64]),
     "sir_edge_mlp_fwd_stream": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _I, _I,
                                                _F, _I, _P, _P, _P, _I64, _P, _I64, _P, _P]),
+    "sir_edge_mlp_pack_st": (ctypes.c_int, [_P, _I64, _I64, _I, _P, _P]),
+    "sir_edge_mlp_fwd_st": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _I, _I, _F,
+                                           _I, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
+    "sir_edge_mlp_fwd_stream_st": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _I, _I, _I,
+                                                  _F, _I, _P, _P, _P, _I64, _P, _I64, _P, _P]),
     "sir_edge_max_bwd_dst": (ctypes.c_int, [_P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64,
                                             _P, _I64, _I, _F, _P, _P, _I64, _P, _P, _P]),
     "sir_edge_max_bwd_src": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P,

@@ -14,9 +14,14 @@ whose message runs a Linear on every edge, without any [E, *] tensor in the forw
   a_{arg} per (v, o) — V O H multiply-adds per product instead of E O H, no [E, *] tensor); the dense
   fused one (fp32 MFMA, opt-in ``fused_bwd``).
 
-Everything is fp32, under autocast too: there the reference runs the per-edge Linear (and sigma)
-in 16 bits, these kernels take Q, K widened to fp32 and return the result cast back to QK's dtype —
-a stated deviation (more accurate, not bit-level AMP parity; ``tests/test_amp_gpu.py::
+Under autocast (the reference trains its max configs with AMP, ``heterophilous-datasets/train.py:75``)
+the max forward reads Q, K in their 16-bit storage and runs the per-edge Linear as the reference's
+half-precision nn.Linear does: a = act1(Q[v] + K[u]) evaluated in fp32 and rounded once to the 16-bit type,
+h = a W^T + b as one 16-bit MFMA per 16 k on W, b rounded to it, fp32 accumulation
+(``sir_edge_mlp_fwd*_st``, round 6); the max and its arg edge are taken over the fp32 h (the reference
+rounds h to 16 bits first: its ties among equal rounded values may pick another edge).  The max backward
+and the Sequential-sigma form widen Q, K to fp32 (a V-sized copy) and run the fp32 kernels — more accurate
+than the reference's 16-bit backward, not bit-level AMP parity (``tests/test_amp_gpu.py::
 test_fused_edge_mlp_forms_under_autocast``).  A CPU tensor or a shape outside the kernels' limits is
 never silently served by another path — :func:`seq_sigma` / :func:`max_supported` say up front which
 form applies.
@@ -90,6 +95,48 @@ def _edge_rows(csr):
         er = torch.repeat_interleave(torch.arange(csr.n_rows, device=deg.device, dtype=torch.int32), deg)
         csr._erow = er
     return er
+
+
+# 16-bit Q / K (autocast) on the max forward's 16-bit kernels; False: widened to fp32 (the fp32 kernels)
+NATIVE_16 = True
+
+
+def _st_ok(QK, H):
+    return (NATIVE_16 and QK.dtype in (torch.bfloat16, torch.float16) and QK.dim() == 2 and QK.stride(1) == 1
+            and QK.stride(0) % 4 == 0 and H % 4 == 0 and QK.data_ptr() % 8 == 0)
+
+
+def _fwd_st(plan, Q, K, W, b, act1, slope, out, arg):
+    """The max forward on 16-bit Q, K rows (``sir_edge_mlp_pack_st`` + ``sir_edge_mlp_fwd_stream_st`` /
+    ``sir_edge_mlp_fwd_st``): one 16-bit MFMA per product, fp32 accumulation, fp32 ``out``."""
+    lib = _native.load()
+    csr = plan.dst
+    Fo, H = W.shape
+    dt = _native.STORAGE[Q.dtype]
+    P = _native._ptr
+    st = _native._stream(Q.device)
+    packed = torch.empty((lib.sir_edge_mlp_pack_bytes(H, Fo),), dtype=torch.uint8, device=Q.device)
+    _native._check(lib.sir_edge_mlp_pack_st(P(W), H, Fo, dt, P(packed), st), lib)
+    if STREAM and H == 256 and Fo <= 256:
+        E = csr.col.numel()
+        work = torch.empty((lib.sir_edge_mlp_stream_work_bytes(Fo),), dtype=torch.uint8, device=Q.device)
+        with _native._Timed("sir_edge_mlp_fwd", Q.device, 2 * E * H * Fo):
+            rc = lib.sir_edge_mlp_fwd_stream_st(P(csr.rowptr), P(csr.col) if E else None,
+                                                P(_edge_rows(csr)) if E else None, csr.n_rows, E, H, Fo, P(Q),
+                                                Q.stride(0), P(K), K.stride(0), dt, AGG_MAX, act1, float(slope),
+                                                _native.ACT_IDENTITY, P(packed), P(b), P(out), out.stride(0), P(arg),
+                                                arg.stride(0), P(work), st)
+        _native._check(rc, lib)
+        return
+    n = csr.n_slots
+    pval = torch.empty((max(n, 1) * Fo,), device=Q.device, dtype=torch.float32) if n else None
+    parg = torch.empty((max(n, 1) * Fo,), device=Q.device, dtype=torch.int32) if n else None
+    with _native._Timed("sir_edge_mlp_fwd", Q.device, 2 * csr.col.numel() * H * Fo):
+        rc = lib.sir_edge_mlp_fwd_st(P(csr.rowptr), P(csr.col), P(csr.items), csr.n_items, P(csr.splits),
+                                     csr.n_splits, H, Fo, P(Q), Q.stride(0), P(K), K.stride(0), dt, AGG_MAX, act1,
+                                     float(slope), _native.ACT_IDENTITY, P(packed), P(b), P(out), out.stride(0),
+                                     P(arg), arg.stride(0), P(pval), P(parg), st)
+    _native._check(rc, lib)
 
 
 def _fwd(plan, Q, K, W, b, agg, act1, slope, act2, out, arg=None):
@@ -207,14 +254,17 @@ class EdgeMaxLinear(torch.autograd.Function):
     def forward(ctx, QK, W, b, plan, H, act1, slope):
         if QK.device.type != "cuda":
             raise RuntimeError("sirgcn fused max path needs a ROCm GPU tensor (no CPU fallback)")
-        QK = QK.contiguous().float()
         W = W.contiguous().float()
         b = b.contiguous().float() if b is not None else None
         O = W.shape[0]
         V = plan.dst.n_rows
         Y = torch.empty((V, O), device=QK.device, dtype=torch.float32)
         arg = torch.empty((V, O), device=QK.device, dtype=torch.int32)
-        _fwd(plan, QK[:, :H], QK[:, H:], W, b, "max", act1, slope, _native.ACT_IDENTITY, Y, arg)
+        if _st_ok(QK, H):             # autocast: 16-bit rows, 16-bit per-edge Linear (module docstring)
+            _fwd_st(plan, QK[:, :H], QK[:, H:], W, b, act1, slope, Y, arg)
+        else:
+            QK = QK.contiguous().float()
+            _fwd(plan, QK[:, :H], QK[:, H:], W, b, "max", act1, slope, _native.ACT_IDENTITY, Y, arg)
         ctx.save_for_backward(QK, W, arg)
         ctx.plan, ctx.H, ctx.act1, ctx.slope, ctx.has_b = plan, H, act1, slope, b is not None
         return Y
@@ -223,6 +273,7 @@ class EdgeMaxLinear(torch.autograd.Function):
     def backward(ctx, dY):
         QK, W, arg = ctx.saved_tensors
         H = ctx.H
+        QK = QK.float()               # 16-bit rows of the autocast forward: the fp32 backward on widened rows
         dQK = torch.empty_like(QK)
         dW, db = max_linear_backward(ctx.plan, QK[:, :H], QK[:, H:], W, arg, dY, ctx.act1, ctx.slope,
                                      dQK[:, :H], dQK[:, H:])

@@ -233,12 +233,118 @@ def test_autocast_layer_native_nt16_large(dt, monkeypatch):
         assert e <= max(tol, AMP_SLACK * e_amp), f"{k}: relL2 {e:.3e} vs fp32 (reference AMP {e_amp:.3e})"
 
 
+def _max16_graph(seed, V=400, E=5000):
+    gen = torch.Generator().manual_seed(seed)
+    src = torch.randint(0, V, (E,), generator=gen)
+    dst = torch.randint(0, V - 20, (E,), generator=gen)      # 20 isolated destinations
+    dst[:600] = 5                                            # a hub row (split items / several stream blocks)
+    return src, dst, V, gen
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("H,O,act", [(256, 256, "leaky"), (256, 40, "relu"), (512, 512, "leaky"), (64, 48, "relu"),
+                                     (128, 200, "leaky")])
+def test_max_forward_16bit_kernel_semantics(dt, H, O, act):
+    """The 16-bit max forward (sir_edge_mlp_fwd_stream_st at H = 256, sir_edge_mlp_fwd_st per item otherwise)
+    against its stated semantics in fp64 on the host: a = round_dt(act1(Q[v] + K[u]) in fp32) from the 16-bit
+    rows, h = a round_dt(W)^T + round_dt(b), Y[v] = max_e h, arg = the first arg-max edge, empty rows 0 / -1.
+    ReLU / LeakyReLU: a is bit-identical on both sides, so Y may differ only by the fp32 accumulation
+    (<= 1e-5 of sum |a| |w| + |b|) and arg only where the row's two best h are closer than that."""
+    from sirgcn import edgemlp
+    from sirgcn.graph import get_plan
+    src, dst, V, gen = _max16_graph(H + O)
+    QK = (torch.randn(V, 2 * H, generator=gen) * 2).to(DT[dt]).to(DEV)
+    W = (torch.randn(O, H, generator=gen) / H ** 0.5).to(DEV)
+    b = torch.randn(O, generator=gen).to(DEV)
+    code, slope = activation_code(ACTS[act])
+    plan = get_plan(Graph(src, dst, V), torch.device(DEV))
+    Y = torch.empty(V, O, device=DEV)
+    arg = torch.empty(V, O, device=DEV, dtype=torch.int32)
+    edgemlp._fwd_st(plan, QK[:, :H], QK[:, H:], W, b, code, slope, Y, arg)
+    torch.cuda.synchronize()
+    # host reference, edges in dst-CSR order (ascending edge id inside a row)
+    order = torch.argsort(dst, stable=True)
+    s_, d_ = src[order], dst[order]
+    q, k = QK[:, :H].float().cpu(), QK[:, H:].float().cpu()
+    z = q[d_] + k[s_]                                        # fp32, as the kernel
+    a32 = torch.relu(z) if act == "relu" else torch.nn.functional.leaky_relu(z, slope)
+    a = a32.to(DT[dt]).double()
+    Wr, br = W.cpu().to(DT[dt]).double(), b.cpu().to(DT[dt]).double()
+    h = a @ Wr.t() + br                                      # [E, O] fp64
+    bound = 1e-5 * (a.abs() @ Wr.abs().t() + br.abs())
+    Yr = torch.zeros(V, O, dtype=torch.float64)
+    Ar = torch.full((V, O), -1, dtype=torch.int64)
+    gap = torch.full((V, O), float("inf"), dtype=torch.float64)
+    rp = torch.zeros(V + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(torch.bincount(d_, minlength=V), 0)
+    for v in range(V):
+        e0, e1 = int(rp[v]), int(rp[v + 1])
+        if e0 == e1:
+            continue
+        hv = h[e0:e1]
+        best, idx = hv.max(0)                                # torch.max returns the first maximal index
+        Yr[v], Ar[v] = best, idx + e0
+        if e1 - e0 > 1:
+            top2 = hv.topk(2, dim=0).values
+            gap[v] = top2[0] - top2[1]
+    tol = torch.zeros(V, O, dtype=torch.float64)
+    for v in range(V):
+        e0, e1 = int(rp[v]), int(rp[v + 1])
+        if e1 > e0:
+            tol[v] = bound[e0:e1].max(0).values
+    Yg, Ag = Y.double().cpu(), arg.long().cpu()
+    assert ((Yg - Yr).abs() <= tol).all(), f"Y off by {(Yg - Yr).abs().max():.3e}"
+    clear = gap > 2 * tol
+    assert torch.equal(Ag[clear], Ar[clear]), int((Ag[clear] != Ar[clear]).sum())
+    assert (Ag[rp[1:] == rp[:-1]] == -1).all()
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("H,O,act", [(256, 256, "gelu"), (512, 512, "gelu")])
+def test_max_layer_under_autocast_runs_16bit_forward(dt, H, O, act, monkeypatch):
+    """The reference's AMP max configs (heterophilous-datasets/README.md:8: roman-empire H = O = 512, GELU;
+    amazon-ratings H = 256): SIRConv(agg_type='max') under autocast takes the 16-bit forward (16-bit Q / K
+    rows, one 16-bit MFMA per product) — Y and every gradient within the AMP bar of the fp32 layer, or no
+    worse than 1.25x the reference's own AMP dataflow."""
+    from sirgcn import edgemlp
+    calls = []
+    orig = edgemlp._fwd_st
+    monkeypatch.setattr(edgemlp, "_fwd_st", lambda *a: calls.append(a[0]) or orig(*a))
+    src, dst, V, gen = _max16_graph(7 + H)
+    d = 64
+    X = torch.randn(V, d, generator=gen).to(DEV)
+    dY = torch.randn(V, O, generator=gen).to(DEV)
+    torch.manual_seed(9)
+    m = SIRConv(d, H, O, ACTS[act], 0, agg_type="max").to(DEV)
+    ref = oracle.SIRConvRef(d, H, O, ACTS[act], 0, agg_type="max").to(DEV)
+    ref.load_state_dict(m.state_dict())
+    g = Graph(src, dst, V)
+
+    def run(mod, amp):
+        for p in mod.parameters():
+            p.grad = None
+        x = X.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=DT[dt], enabled=amp):
+            y = mod(g, x)
+        y.float().backward(dY)
+        out = {"Y": y.detach().float(), "dX": x.grad}
+        out.update({n: p.grad for n, p in mod.named_parameters()})
+        return {k: v.detach().float().cpu() for k, v in out.items()}
+
+    got = run(m, True)
+    assert len(calls) == 1, "the 16-bit max forward did not run"
+    truth, amp = run(ref, False), run(ref, True)
+    tol = 2e-2 if dt == "bf16" else 1e-2
+    for k in truth:
+        e, e_amp = rel_err(got[k], truth[k]), rel_err(amp[k], truth[k])
+        assert e <= max(tol, AMP_SLACK * e_amp), f"max16 {k}: relL2 {e:.3e} (reference AMP {e_amp:.3e})"
+
+
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("form", ["max", "seq"])
 def test_fused_edge_mlp_forms_under_autocast(form, dt):
-    """agg='max' (conv.py:46-47, roman-empire trains it under AMP) and the DictionaryLookup
-    Sequential sigma run their per-edge Linear inside the fused kernels in fp32 even under autocast
-    (sirgcn/edgemlp.py: stated deviation, more accurate than the reference's 16-bit per-edge Linear):
+    """agg='max' (conv.py:46-47, roman-empire trains it under AMP: the 16-bit forward) and the DictionaryLookup
+    Sequential sigma (its per-edge Linear in fp32 even under autocast: sirgcn/edgemlp.py, a stated deviation):
     outputs and gradients within the AMP bar of the fp32 layer, or no worse than 1.25x the
     reference's own AMP dataflow (oracle.SIRConvRef under the same autocast)."""
     gen = torch.Generator().manual_seed(31 + len(dt))

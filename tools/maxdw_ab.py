@@ -3,6 +3,7 @@
 batches; 2 k_max_dw_qk2, 16-row / 128-edge batches) on an S1-shaped max layer (V=500k, E=10M, H=O=256,
 LeakyReLU 0.2), interleaved in one process; the outputs must be bit-identical."""
 import argparse
+import ctypes
 import os
 import statistics
 import sys
@@ -22,7 +23,8 @@ def main():
     ap.add_argument("--V", type=int, default=500_000)
     ap.add_argument("--E", type=int, default=10_000_000)
     ap.add_argument("--H", type=int, default=256)
-    ap.add_argument("--forms", default="1,2")
+    ap.add_argument("--forms", default="1,2", help="SIR_MAXDW values, each optionally @<lib name>")
+    ap.add_argument("--libs", nargs="*", default=[], help="name=path of A/B library builds (same ABI)")
     a = ap.parse_args()
     _native.load()
     dev = torch.device("cuda")
@@ -40,10 +42,21 @@ def main():
     edgemlp._fwd(plan, Q, K, W, b, "max", _native.ACT_LEAKY, 0.2, _native.ACT_IDENTITY, Y, arg)
     dY = torch.randn(a.V, a.H, device=dev)
     forms = a.forms.split(",")
+    libs = {"main": _native.load()}
+    for kv in a.libs:
+        name, path = kv.split("=", 1)
+        h = ctypes.CDLL(path)
+        for fn, (res, args) in _native.SIGNATURES.items():
+            f = getattr(h, fn, None)
+            if f is not None:
+                f.restype, f.argtypes = res, args
+        libs[name] = h
     outs, times = {}, {f: [] for f in forms}
     for r in range(a.rounds):
         for f in forms:
-            os.environ["SIR_MAXDW"] = f
+            form, _, lib = f.partition("@")
+            os.environ["SIR_MAXDW"] = form
+            _native._lib = libs[lib or "main"]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             dW, db = _native.max_dw_qk(plan.dst, arg, dY, Q, K, a.H, _native.ACT_LEAKY, 0.2)
