@@ -206,10 +206,53 @@ class _Linear(torch.autograd.Function):
         return dx, dW, db
 
 
+class _Linear16(torch.autograd.Function):
+    """Autocast's nn.Linear (``F.linear(x.to(dt), W.to(dt), b.to(dt))``) on the native 16-bit
+    kernels: y = mm16_wt (x.to(dt) fused into the loads, the rounded x written for dW only when W
+    needs a gradient), dx = mm16_w(dy, W) in x's dtype straight from the fp32 accumulator, and
+    (dW, db) = mm_tn16(dy, x) in fp32 like the parameters (exact 16-bit products, fp32 sums)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, dt):
+        xh = x
+        if x.dtype != dt and ctx.needs_input_grad[1]:
+            xh = torch.empty(x.shape, dtype=dt, device=x.device)
+            y = mm16_wt(x, W, b, dt, acopy=xh)
+        else:
+            y = mm16_wt(x, W, b, dt)
+        ctx.save_for_backward(xh if ctx.needs_input_grad[1] else None, W)
+        ctx.has_b, ctx.x_dtype, ctx.dt = b is not None, x.dtype, dt
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xh, W = ctx.saved_tensors
+        dt = ctx.dt
+        dy = dy.contiguous().to(dt)
+        dx = mm16_w(dy, W, dt, out_dtype=ctx.x_dtype) if ctx.needs_input_grad[0] else None
+        dW = db = None
+        need_b = ctx.has_b and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1]:
+            dW, db = mm_tn16(dy, xh, colsum=True) if need_b else (mm_tn16(dy, xh), None)
+        elif need_b:
+            db = dy.float().sum(0)
+        return dx, dW, db, None
+
+
 def linear(x, W, b=None):
     """``F.linear(x, W, b)`` (the reference's ``nn.Linear`` calls, conv.py:60-61,65) on the native
-    split-fp16 GEMMs for fp32 GPU operands the kernels take; anything else (autocast, fp64, other
-    layouts, CPU tensors) is torch's own ``F.linear`` — the same dataflow autocast would run."""
+    split-fp16 GEMMs for fp32 GPU operands the kernels take; under a bf16 / fp16 autocast (the
+    reference's AMP path, heterophilous-datasets/train.py:75) on the native 16-bit GEMMs
+    (:class:`_Linear16`) for shapes those take; anything else (fp64, other layouts, CPU tensors,
+    small or odd-shaped autocast operands) is torch's own ``F.linear``."""
+    if (USE_NATIVE and torch.is_autocast_enabled() and x.dim() == 2 and W.dim() == 2 and x.is_cuda
+            and W.dtype == torch.float32 and W.is_cuda and (b is None or (b.dtype == torch.float32 and b.is_cuda))):
+        dt = torch.get_autocast_dtype("cuda")
+        xc = x if x.stride(1) == 1 else x.contiguous()
+        if dt in (torch.bfloat16, torch.float16) and _nt16_ok(xc, W.shape[1], W.shape[0], dt):
+            with torch.autocast("cuda", enabled=False):
+                return _Linear16.apply(xc, W, b, dt)
+        return torch.nn.functional.linear(x, W, b)
     if (USE_NATIVE and not torch.is_autocast_enabled() and x.dim() == 2 and W.dim() == 2
             and x.dtype == torch.float32 and W.dtype == torch.float32 and (b is None or b.dtype == torch.float32)):
         xc = x if x.stride(1) == 1 else x.contiguous()

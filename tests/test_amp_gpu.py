@@ -9,6 +9,7 @@ relative L2 within 2e-2 (bf16) / 1e-2 (fp16), or no worse than the 
 dataflow (``oracle.SIRConvRef`` under the same autocast; ratio <= 1.25 — both are dominated by the
 same half-precision GEMMs, the edge part here is fp32 inside).
 """
+import copy
 import numpy as np
 import pytest
 import torch
@@ -17,7 +18,7 @@ from torch import nn
 import oracle
 from conftest import golden_manifest, load_case, rel_err
 
-from sirgcn import _native
+from sirgcn import _native, linalg
 from sirgcn.conv import EdgeAggregate, SIRConv, activation_code
 from sirgcn.graph import Graph, GraphPlan
 
@@ -338,6 +339,57 @@ def test_max_layer_under_autocast_runs_16bit_forward(dt, H, O, act, monkeypatch)
     for k in truth:
         e, e_amp = rel_err(got[k], truth[k]), rel_err(amp[k], truth[k])
         assert e <= max(tol, AMP_SLACK * e_amp), f"max16 {k}: relL2 {e:.3e} (reference AMP {e_amp:.3e})"
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("agg,act,H,O", [("max", "gelu", 256, 256), ("max", "leaky", 128, 40),
+                                         ("seq", "relu", 256, 128)])
+def test_autocast_projections_native_nt16(dt, agg, act, H, O, monkeypatch):
+    """The max / Sequential-sigma layers under autocast run their projections (QK = X [W_Q; W_K]^T + b,
+    and linear_relation for the Sequential form) through linalg.linear's 16-bit route (_Linear16:
+    sir_gemm_nt16 forward and dX, sir_gemm_tn16 weight gradients) instead of torch's bf16 GEMM plus
+    casts — outputs and every gradient within the AMP bar of the fp32 layer, or no worse than 1.25x the
+    reference's own AMP dataflow."""
+    monkeypatch.setattr(linalg, "MIN_ROWS_16", 0)
+    calls = {"nt": 0, "tn": 0}
+    nt, tn = _native.gemm_nt16, _native.gemm_tn16
+    monkeypatch.setattr(_native, "gemm_nt16", lambda *a, **k: calls.__setitem__("nt", calls["nt"] + 1) or nt(*a, **k))
+    monkeypatch.setattr(_native, "gemm_tn16", lambda *a, **k: calls.__setitem__("tn", calls["tn"] + 1) or tn(*a, **k))
+    src, dst, V, gen = _max16_graph(11 + H + O)
+    d = 128
+    X = torch.randn(V, d, generator=gen).to(DEV)
+    dY = torch.randn(V, O, generator=gen).to(DEV)
+    torch.manual_seed(5)
+    if agg == "max":
+        sig, kind = ACTS[act], "max"
+    else:
+        sig, kind = nn.Sequential(ACTS[act], nn.Linear(H, H), nn.ReLU()), "sum"
+    m = SIRConv(d, H, O, sig, 0, agg_type=kind).to(DEV)
+    ref = oracle.SIRConvRef(d, H, O, copy.deepcopy(sig), 0, agg_type=kind).to(DEV)
+    ref.load_state_dict(m.state_dict())
+    g = Graph(src, dst, V)
+
+    def run(mod, amp):
+        for p in mod.parameters():
+            p.grad = None
+        x = X.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=DT[dt], enabled=amp):
+            y = mod(g, x)
+        y.float().backward(dY)
+        out = {"Y": y.detach().float(), "dX": x.grad}
+        out.update({n: p.grad for n, p in mod.named_parameters()})
+        return {k: v.detach().float().cpu() for k, v in out.items()}
+
+    got = run(m, True)
+    n_lin = 1 if agg == "max" else 2
+    assert calls["nt"] == 2 * n_lin and calls["tn"] == n_lin, calls
+    for n, p in m.named_parameters():
+        assert p.grad.dtype == torch.float32, n
+    truth, amp = run(ref, False), run(ref, True)
+    tol = 2e-2 if dt == "bf16" else 1e-2
+    for k in truth:
+        e, e_amp = rel_err(got[k], truth[k]), rel_err(amp[k], truth[k])
+        assert e <= max(tol, AMP_SLACK * e_amp), f"{agg} {k}: relL2 {e:.3e} (reference AMP {e_amp:.3e})"
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
