@@ -56,9 +56,10 @@ def parse():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--agg", default="sum", choices=["sum", "mean", "sym", "max"],
                     help="max: the fused per-edge W_R + running max (sirgcn.edgemlp), an MFMA-bound kernel")
-    ap.add_argument("--max-bwd", default="materialised", choices=["materialised", "routed"],
-                    help="agg max: the edge-materialised backward (default) or the routed one (no [E, *] buffer, "
-                         "sirgcn.edgemlp.EdgeMaxLinear.sparse_bwd)")
+    ap.add_argument("--max-bwd", default="hybrid", choices=["hybrid", "materialised", "routed"],
+                    help="agg max: the default hybrid backward (routed dQ / dK passes, dW_R with the activations "
+                         "recomputed: no [E, *] buffer), the edge-materialised one (EdgeMaxLinear.hybrid_bwd = "
+                         "False) or the fully routed one (sirgcn.edgemlp.EdgeMaxLinear.sparse_bwd)")
     ap.add_argument("--dtype", default=None, choices=["f32", "bf16", "f16"],
                     help="feature dtype (16-bit = the autocast path); default f32 (cfg2: bf16)")
     ap.add_argument("--chunk", type=int, default=None)
@@ -346,9 +347,12 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
     torch.manual_seed(4)
     p_drop = args.dropout or 0.0
     conv = SIRConv(H, H, H, nn.LeakyReLU(0.2, inplace=True), p_drop, agg_type=args.agg).to(dev)
-    if args.agg == "max" and args.max_bwd == "routed":
+    if args.agg == "max" and args.max_bwd != "hybrid":
         from sirgcn.edgemlp import EdgeMaxLinear
-        EdgeMaxLinear.sparse_bwd = True
+        if args.max_bwd == "routed":
+            EdgeMaxLinear.sparse_bwd = True
+        else:
+            EdgeMaxLinear.hybrid_bwd = False
     if args.chunk:
         conv.chunk = args.chunk
     X_full = torch.randn(V, H, generator=torch.Generator().manual_seed(3))
