@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define SIR_ABI_VERSION 15
+#define SIR_ABI_VERSION 16
 
 /* aggregation: conv.py:41 (`sym` -> fn.sum with deg^-1/2 norms conv.py:54-57).  SIR_AGG_ACCUMULATE,
  * OR'd into the forward's `agg` (SUM / SYM): S[v] = S[v] + the sum over the given items' edges, rows
@@ -361,7 +361,8 @@ int sir_edge_max_bwd_src(const int32_t* rowptr_s, const int32_t* col_s, const in
  *   dQ[v] = sum_e dz_e (dst CSR),  dK[u] = sum_e dz_e (src CSR),
  *   dW[o, :] = sum_v dY[v][o] act1(Q[v] + K[col[arg[v][o]]]),  db[o] = sum_v dY[v][o]
  * with V * O * H multiply-adds per product (not E * O * H) and no [E, H] / [E, O] buffer.  Workspace:
- * ent = 8 * V * O bytes (V * O < 2^31), ecnt_d / ecnt_s = 8 * E bytes each, partial = max(n_slots) * H
+ * ent = 8 * V * O + 64 bytes (V * O < 2^31; ABI 16: the last 64 bytes hold the dQ / dK passes' work-queue
+ * counters, zeroed by the call), ecnt_d / ecnt_s = 8 * E bytes each, partial = max(n_slots) * H
  * floats, dbpart = route_blocks * O4 floats (O4 = O rounded up to 4) and wpart = dw_ranges * O * H floats (the sizes from
  * sir_edge_max_bwd_sparse_parts; sum each over its rows in row order for db / dW, e.g. sir_col_sum;
  * wpart NULL skips the dW pass, for a caller that has A and uses sir_max_dw_rows).  With no work items

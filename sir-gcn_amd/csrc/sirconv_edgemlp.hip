@@ -82,6 +82,17 @@ __device__ __forceinline__ float mlp_pow2(int e) {
 __device__ __forceinline__ int mlp_scale_exp(float m) { const int s = 15 - mlp_bexp(m); return s > 126 ? 126 : s; }
 // fragment image of one 16-k step plane: piece (row, h) of 16 B at (row / 32) * 1024 + h * 512 + (row % 32) * 16
 __device__ __forceinline__ int mlp_fimg(int row, int h) { return ((row >> 5) << 10) + (h << 9) + ((row & 31) << 4); }
+// The stream forward's image (32 rows): mlp_fimg with the row's 16-B slot XORed by f = 2 (g & 3) + h.  A
+// staging store (ds_write_b64, one edge row a wave, lane l: k-group g = l / 4, half h = (l / 2) & 1) then
+// puts the 16 lanes of each store group on 16 distinct 8-B positions of the 128-B bank period (unswizzled:
+// all on the row's one slot, 8-way), and the MFMA fragment read (lane l: row l & 31, half l / 32, one g a
+// read) still takes 32 distinct slots of its 512-B half (the XOR is a bijection on the slot).
+#ifndef SIR_MLP_SWZ
+#define SIR_MLP_SWZ 1
+#endif
+__device__ __forceinline__ int mlp_fimg_sw(int row, int h, int g) {
+    return (h << 9) + (((row & 31) << 4) ^ (SIR_MLP_SWZ ? ((h << 4) | ((g & 3) << 5)) : 0));
+}
 
 // pack: out16[((t * NG + g) * 2 + p) * 64 + l] = 8 halves of part p (hi / lo) of W[32t + l%32][16g + 8(l/32) + j]
 // scaled by 2^se(n); inv[n] = 2^-se(n) (0 past F).  One 64-thread block per padded feature.
@@ -795,8 +806,11 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
             wlo[g] = h8v{};
         }
     }
-    const int fo = mlp_fimg(l & 31, l >> 5);
+    int fos[4];                                             // the lane's fragment slot for g & 3 = 0..3
+#pragma unroll
+    for (int q = 0; q < 4; ++q) fos[q] = mlp_fimg_sw(l & 31, l >> 5, q);
     const int k4 = 4 * l;
+    const int sg = k4 >> 4, sh = (k4 >> 3) & 1, sj8 = k4 & 7;  // the lane's staging k-group / half / offset
     const int T = (int)((ee - eb + 31) / 32);
     // lane l (mod 32) of tile j's column / row vectors (clamped: any index is a valid edge)
     auto tile_t0 = [&](int j) { return eb + 32 * (int64_t)j; };
@@ -837,9 +851,9 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
             a4.y = ok ? act_f<ACT1>(qv[ii].y + kv[ii].y, slope) : 0.f;
             a4.z = ok ? act_f<ACT1>(qv[ii].z + kv[ii].z, slope) : 0.f;
             a4.w = ok ? act_f<ACT1>(qv[ii].w + kv[ii].w, slope) : 0.f;
+            char* const d = img[bf] + sg * 2048 + mlp_fimg_sw(i, sh, sg) + sj8 * 2;
             if constexpr (X16) {
-                const int g = k4 >> 4, h = (k4 >> 3) & 1, j8 = k4 & 7;
-                *reinterpret_cast<uint2*>(img[bf] + g * 2048 + mlp_fimg(i, h) + j8 * 2) = pack4_st<ST>(a4);
+                *reinterpret_cast<uint2*>(d) = pack4_st<ST>(a4);
                 if (l == 0) sInv[bf][i] = 1.f;
                 continue;
             }
@@ -850,8 +864,6 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
             _Float16 hv[4], lv[4];
 #pragma unroll
             for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
-            const int g = k4 >> 4, h = (k4 >> 3) & 1, j8 = k4 & 7;
-            char* d = img[bf] + g * 2048 + mlp_fimg(i, h) + j8 * 2;
             *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
             *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
             if (l == 0) sInv[bf][i] = mlp_pow2(-se);
@@ -879,11 +891,11 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
-            const h8v ahi = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + fo);
+            const h8v ahi = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + fos[g & 3]);
             if constexpr (X16) {
                 acc = mfma16_st<ST>(ahi, whi[g], acc);
             } else {
-                const h8v alo = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + 1024 + fo);
+                const h8v alo = *reinterpret_cast<const h8v*>(img[bf] + g * 2048 + 1024 + fos[g & 3]);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi[g], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo[g], acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi[g], acc, 0, 0, 0);

@@ -22,6 +22,10 @@
 //                 dY[v][o] a; per-range partials summed in range order afterwards.
 #include "sirconv_edge_impl.h"
 
+#ifndef SIR_MAXB_QC
+#define SIR_MAXB_QC 4           // items a work-queue claim of the dz passes
+#endif
+
 namespace sir {
 namespace {
 
@@ -119,13 +123,19 @@ k_maxb_route(const int* __restrict__ rowptr, const int4* __restrict__ items, int
 // batch.  The next batch's {start, count} and neighbour index (at an item's last batch: the next item's
 // descriptor, own row and first batch) are in flight while the current batch's entries run; the entry
 // loop is wave-uniform (both groups' counts, 4 entries a step: staged slots past a count hold {0, 0.f}).
+// Items are handed out by a work queue (one counter per column slice, zeroed before the launch), QC at a
+// time: an item's cost is its entry count, which on the source CSR ranges over 1-5,600 entries (S1), so a
+// static item -> wave assignment left the pass waiting on its slowest waves (max / mean wave work 1.48 on
+// S1, 1.22 on the destination CSR).  The next chunk is claimed one chunk ahead (its atomic's latency hidden
+// under the current chunk); a wave stops at its first claim past the last item.
 template <bool DST, int ACT1, int OPAD, int U>
 __global__ void __launch_bounds__(1024)
 k_maxb_dz(const int* __restrict__ col, const int4* __restrict__ items, int64_t n_items,
           const int2* __restrict__ ecnt, const int2* __restrict__ ent,
           const float* __restrict__ own, int64_t ldown, const float* __restrict__ oth, int64_t ldoth,
           const float* __restrict__ W, int H, int O, float slope, int nsl,
-          float* __restrict__ out, int64_t ldo, float* __restrict__ partial) {
+          float* __restrict__ out, int64_t ldo, float* __restrict__ partial, int* __restrict__ qctr) {
+    constexpr int QC = SIR_MAXB_QC;
     __shared__ float4 sW[OPAD * 32];
     __shared__ int2 sE[16][2][32];
     const int t = threadIdx.x, l = t & 63, g = l >> 5, c = l & 31;
@@ -140,9 +150,12 @@ k_maxb_dz(const int* __restrict__ col, const int4* __restrict__ items, int64_t n
     const int cc = c0 + 4 * c;
     const bool colok = cc < H;
     const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int64_t wstride = (int64_t)(gridDim.x / nsl) * 16;
-    int64_t wi = (int64_t)(blockIdx.x / nsl) * 16 + w;
+    int* const ctr = qctr + s;
+    int pend = (l == 0) ? atomicAdd(ctr, QC) : 0;
+    int64_t wi = __builtin_amdgcn_readfirstlane(pend);
     if (wi >= n_items) return;               // whole wave; no block barrier past this point
+    pend = (l == 0) ? atomicAdd(ctr, QC) : 0;  // the next chunk, read when this one is done
+    int qi = 0;                              // position of wi in its chunk
     int4 it = uniform_item(items, wi);
     float4 ov = colok ? ld4(own + (int64_t)it.x * ldown + cc) : zero4;
     int2 ec[U];
@@ -155,7 +168,13 @@ k_maxb_dz(const int* __restrict__ col, const int4* __restrict__ items, int64_t n
     }
     while (true) {
         const int row = it.x, e1 = it.z, slot = it.w;
-        const int64_t wn = wi + wstride;
+        int64_t wn;
+        if (qi + 1 < QC) {
+            wn = wi + 1;
+        } else {                             // into the claimed chunk; claim the one after it
+            wn = __builtin_amdgcn_readfirstlane(pend);
+            if (wn < n_items) pend = (l == 0) ? atomicAdd(ctr, QC) : 0;
+        }
         const bool more = wn < n_items;
         const int4 itn = more ? uniform_item(items, wn) : make_int4(0, 0, 0, 0);
         float4 ovn = zero4;
@@ -249,6 +268,7 @@ k_maxb_dz(const int* __restrict__ col, const int4* __restrict__ items, int64_t n
         }
         if (!more) break;
         wi = wn;
+        qi = (qi + 1 < QC) ? qi + 1 : 0;
         it = itn;
         ov = ovn;
     }
@@ -938,6 +958,11 @@ hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st) {
     if (a.V == 0 && a.wpart != nullptr &&
         (err = hipMemsetAsync(a.wpart, 0, (size_t)O * H * sizeof(float), st)) != hipSuccess)
         return err;
+    // the dz passes' work-queue counters: 16 ints after the entries (the dQ pass [0, nsl), the dK pass [8, 8 + nsl))
+    int* const qctr = reinterpret_cast<int*>(static_cast<int2*>(a.ent) + a.V * O);
+    if (a.ent != nullptr && (a.n_items_d > 0 || a.n_items_s > 0) &&
+        (err = hipMemsetAsync(qctr, 0, 16 * sizeof(int), st)) != hipSuccess)
+        return err;
     // 1. routing table + db partials
     if (a.n_items_d > 0) {
         const int nb = (int)(a.route_blocks);
@@ -968,7 +993,7 @@ hipError_t run_max_bwd_sparse(const MaxBwdArgs& a, hipStream_t st) {
                                reinterpret_cast<const int2*>(DV ? a.ecnt_d : a.ecnt_s),
                                reinterpret_cast<const int2*>(a.ent), DV ? a.Q : a.K, DV ? a.ldq : a.ldk,
                                DV ? a.K : a.Q, DV ? a.ldk : a.ldq, a.W, H, O, a.slope, nsl,
-                               DV ? a.dQ : a.dK, DV ? a.lddq : a.lddk, a.partial);
+                               DV ? a.dQ : a.dK, DV ? a.lddq : a.lddk, a.partial, qctr + (DV ? 0 : 8));
             hipError_t e2 = hipGetLastError();
             if (e2 != hipSuccess) return e2;
             const int64_t ns = DV ? a.n_splits_d : a.n_splits_s;

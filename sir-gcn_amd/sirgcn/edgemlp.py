@@ -491,7 +491,7 @@ def _max_bwd_sparse(plan, Q, K, W, arg, dY, act1, slope, dQ, dK, with_dw=True):
     W = W.contiguous()
     rb, nr = ctypes.c_int64(0), ctypes.c_int64(0)
     _native._check(lib.sir_edge_max_bwd_sparse_parts(d.n_items, V, ctypes.byref(rb), ctypes.byref(nr)), lib)
-    ent = torch.empty((max(V * O, 1),), device=dev, dtype=torch.int64)
+    ent = torch.empty((V * O + 8,), device=dev, dtype=torch.int64)     # + the dz passes' queue counters
     ecnt_d = torch.empty((max(E, 1),), device=dev, dtype=torch.int64)
     ecnt_s = torch.empty((max(E, 1),), device=dev, dtype=torch.int64)
     part = torch.empty((max(d.n_slots, s.n_slots, 1) * H,), device=dev, dtype=torch.float32)

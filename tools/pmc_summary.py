@@ -32,6 +32,7 @@ def main():
                 names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
             for (d, c), v in per.items():
                 k = names[d]
+                k = k.replace("(anonymous namespace)::", "")
                 short = k.split("sir::", 1)[-1] if "sir::" in k else k
                 short = re.sub(r"\(.*", "", short)[:80]
                 if a.match and a.match not in short:
