@@ -423,13 +423,15 @@ int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X,
  * _LEAKY_RELU (slope).  The same ops, types and order as torch's add, relu / leaky_relu and their
  * autograd (a 16-bit activation rounds to its type, a 16-bit gradient is rounded once from fp32):
  * bit-identical to the separate torch kernels.  Backward: D = dout (fp32); dY in `dtype`; order 0
- * also writes dR = act'(Y + R) D (order 1: dR is D itself, DR ignored).  N % 4 == 0; rows 16-B
+ * also writes dR = act'(Y + R) D (order 1: dR is D itself, DR ignored).  D2 (order 0, optional; ABI 16):
+ * a second fp32 gradient of out, added to D as it is read — the residual gradient of the next layer,
+ * whose input out is (the sum autograd would otherwise form in its own pass).  N % 4 == 0; rows 16-B
  * aligned (leading dimensions multiples of 4 elements).  ABI 13. */
 int sir_resid_act_fwd(const void* Y, int64_t ldy, int dtype, const float* R, int64_t ldr, float* out, int64_t ldo,
                       int64_t M, int64_t N, int act, float slope, int order, void* stream);
-int sir_resid_act_bwd(const float* D, int64_t ldd, const void* Y, int64_t ldy, int dtype, const float* R, int64_t ldr,
-                      void* dY, int64_t lddy, float* dR, int64_t lddr, int64_t M, int64_t N, int act, float slope,
-                      int order, void* stream);
+int sir_resid_act_bwd(const float* D, int64_t ldd, const float* D2, int64_t ldd2, const void* Y, int64_t ldy, int dtype,
+                      const float* R, int64_t ldr, void* dY, int64_t lddy, float* dR, int64_t lddr, int64_t M, int64_t N,
+                      int act, float slope, int order, void* stream);
 
 /* GraphNorm with the stack's activation and residual after it, one kernel per direction — the
  * layer loop of ogbn-arxiv/model.py:65-73 / ogbg-molhiv/model.py:76-84 (h = act(norm(h)) + resid)

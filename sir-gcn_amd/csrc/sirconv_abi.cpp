@@ -742,15 +742,17 @@ int sir_resid_act_fwd(const void* Y, int64_t ldy, int dtype, const float* R, int
                                              static_cast<hipStream_t>(stream)), nullptr);
 }
 
-int sir_resid_act_bwd(const float* D, int64_t ldd, const void* Y, int64_t ldy, int dtype, const float* R, int64_t ldr,
-                      void* dY, int64_t lddy, float* dR, int64_t lddr, int64_t M, int64_t N, int act, float slope,
-                      int order, void* stream) {
+int sir_resid_act_bwd(const float* D, int64_t ldd, const float* D2, int64_t ldd2, const void* Y, int64_t ldy, int dtype,
+                      const float* R, int64_t ldr, void* dY, int64_t lddy, float* dR, int64_t lddr, int64_t M, int64_t N,
+                      int act, float slope, int order, void* stream) {
     const char* fn = "sir_resid_act_bwd";
     if (M < 0 || N <= 0 || N % 4 != 0 || N > (1 << 30)) return fail(SIR_EINVAL, fn, "bad shape (N % 4 == 0)");
     if (dtype != SIR_DTYPE_F32 && dtype != SIR_DTYPE_BF16 && dtype != SIR_DTYPE_F16) return fail(SIR_EINVAL, fn, "bad dtype");
     if (act != SIR_ACT_IDENTITY && act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU)
         return fail(SIR_EINVAL, fn, "act must be identity, relu or leaky_relu");
     if (order != 0 && order != 1) return fail(SIR_EINVAL, fn, "order must be 0 (zinc) or 1 (arxiv)");
+    if (D2 != nullptr && (order != 0 || ldd2 < N || ldd2 % 4 || !al16(D2)))
+        return fail(SIR_EINVAL, fn, "D2 (order 0 only): rows 16-B aligned, ldd2 >= N, ldd2 % 4 == 0");
     if (ldd < N || ldy < N || lddy < N || ldd % 4 || ldy % 4 || lddy % 4 ||
         (order == 0 && (ldr < N || ldr % 4 || (dR != nullptr && (lddr < N || lddr % 4)))))
         return fail(SIR_EINVAL, fn, "leading dimensions must be >= N and multiples of 4");
@@ -760,7 +762,7 @@ int sir_resid_act_bwd(const float* D, int64_t ldd, const void* Y, int64_t ldy, i
     if (!al16(D) || (y16 ? (reinterpret_cast<uintptr_t>(Y) & 7u) || (reinterpret_cast<uintptr_t>(dY) & 7u)
                          : !al16(Y) || !al16(dY)) || (order == 0 && (!al16(R) || !al16(dR))))
         return fail(SIR_EINVAL, fn, "rows must be 16-B aligned (8-B for 16-bit Y, dY)");
-    return finish(fn, sir::run_resid_act_bwd(D, ldd, Y, ldy, dtype, R, ldr, dY, lddy, order == 0 ? dR : nullptr, lddr, M,
+    return finish(fn, sir::run_resid_act_bwd(D, ldd, D2, ldd2, Y, ldy, dtype, R, ldr, dY, lddy, order == 0 ? dR : nullptr, lddr, M,
                                              (int)N, act, slope, order, static_cast<hipStream_t>(stream)), nullptr);
 }
 

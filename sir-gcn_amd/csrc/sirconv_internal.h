@@ -88,9 +88,9 @@ hipError_t run_seg_max_bwd(const GenericArgs& a, hipStream_t st);
 
 hipError_t run_resid_act_fwd(const void* Y, int64_t ldy, int dtype, const float* R, int64_t ldr, float* O, int64_t ldo,
                              int64_t M, int N, int act, float slope, int order, hipStream_t st);
-hipError_t run_resid_act_bwd(const float* D, int64_t ldd, const void* Y, int64_t ldy, int dtype, const float* R,
-                             int64_t ldr, void* DY, int64_t lddy, float* DR, int64_t lddr, int64_t M, int N, int act,
-                             float slope, int order, hipStream_t st);
+hipError_t run_resid_act_bwd(const float* D, int64_t ldd, const float* D2, int64_t ldd2, const void* Y, int64_t ldy,
+                             int dtype, const float* R, int64_t ldr, void* DY, int64_t lddy, float* DR, int64_t lddr,
+                             int64_t M, int N, int act, float slope, int order, hipStream_t st);
 hipError_t run_graph_norm_fwd(const int64_t* off, int64_t B, int F, const float* X, int64_t ldx,
                               const float* w, const float* bias, const float* ms, float eps, int act, float slope,
                               const float* R, int64_t ldr, float* Y, int64_t ldy, float* mean, float* sd,

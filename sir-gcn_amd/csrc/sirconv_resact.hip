@@ -88,7 +88,8 @@ k_resact_fwd(const void* __restrict__ Y, int64_t ldy, const float* __restrict__ 
 
 template <int DT, int ACT, int ORDER>
 __global__ void __launch_bounds__(256)
-k_resact_bwd(const float* __restrict__ D, int64_t ldd, const void* __restrict__ Y, int64_t ldy,
+k_resact_bwd(const float* __restrict__ D, int64_t ldd, const float* __restrict__ D2, int64_t ldd2,
+             const void* __restrict__ Y, int64_t ldy,
              const float* __restrict__ R, int64_t ldr, void* __restrict__ DY, int64_t lddy, float* __restrict__ DR,
              int64_t lddr, int64_t M, int N, float slope) {
     using E = Elt<DT>;
@@ -98,7 +99,11 @@ k_resact_bwd(const float* __restrict__ D, int64_t ldd, const void* __restrict__ 
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
         const int64_t m = q / nq;
         const int n = (int)(q - m * nq) * 4;
-        const float4 d = *reinterpret_cast<const float4*>(D + m * ldd + n);
+        float4 d = *reinterpret_cast<const float4*>(D + m * ldd + n);
+        if (D2 != nullptr) {           // a second gradient of the output (order 0): the sum autograd would form
+            const float4 d2 = *reinterpret_cast<const float4*>(D2 + m * ldd2 + n);
+            d.x += d2.x; d.y += d2.y; d.z += d2.z; d.w += d2.w;
+        }
         const T* y = static_cast<const T*>(Y) + m * ldy + n;
         float yv[4];
         if constexpr (DT == SIR_DTYPE_F32) {
@@ -163,20 +168,21 @@ hipError_t resact_fwd_t(int act, const void* Y, int64_t ldy, const float* R, int
 }
 
 template <int DT, int ORDER>
-hipError_t resact_bwd_t(int act, const float* D, int64_t ldd, const void* Y, int64_t ldy, const float* R, int64_t ldr,
+hipError_t resact_bwd_t(int act, const float* D, int64_t ldd, const float* D2, int64_t ldd2, const void* Y, int64_t ldy,
+                        const float* R, int64_t ldr,
                         void* DY, int64_t lddy, float* DR, int64_t lddr, int64_t M, int N, float slope, hipStream_t st) {
     const dim3 grid(resact_grid(M, N));
     switch (act) {
     case SIR_ACT_IDENTITY:
-        hipLaunchKernelGGL((k_resact_bwd<DT, SIR_ACT_IDENTITY, ORDER>), grid, dim3(256), 0, st, D, ldd, Y, ldy, R, ldr, DY,
+        hipLaunchKernelGGL((k_resact_bwd<DT, SIR_ACT_IDENTITY, ORDER>), grid, dim3(256), 0, st, D, ldd, D2, ldd2, Y, ldy, R, ldr, DY,
                            lddy, DR, lddr, M, N, slope);
         break;
     case SIR_ACT_RELU:
-        hipLaunchKernelGGL((k_resact_bwd<DT, SIR_ACT_RELU, ORDER>), grid, dim3(256), 0, st, D, ldd, Y, ldy, R, ldr, DY, lddy,
+        hipLaunchKernelGGL((k_resact_bwd<DT, SIR_ACT_RELU, ORDER>), grid, dim3(256), 0, st, D, ldd, D2, ldd2, Y, ldy, R, ldr, DY, lddy,
                            DR, lddr, M, N, slope);
         break;
     case SIR_ACT_LEAKY_RELU:
-        hipLaunchKernelGGL((k_resact_bwd<DT, SIR_ACT_LEAKY_RELU, ORDER>), grid, dim3(256), 0, st, D, ldd, Y, ldy, R, ldr, DY,
+        hipLaunchKernelGGL((k_resact_bwd<DT, SIR_ACT_LEAKY_RELU, ORDER>), grid, dim3(256), 0, st, D, ldd, D2, ldd2, Y, ldy, R, ldr, DY,
                            lddy, DR, lddr, M, N, slope);
         break;
     default: return hipErrorInvalidValue;
@@ -199,18 +205,15 @@ hipError_t run_resid_act_fwd(const void* Y, int64_t ldy, int dtype, const float*
                  : resact_fwd_t<SIR_DTYPE_F16, 0>(act, Y, ldy, R, ldr, O, ldo, M, N, slope, st);
 }
 
-hipError_t run_resid_act_bwd(const float* D, int64_t ldd, const void* Y, int64_t ldy, int dtype, const float* R,
-                             int64_t ldr, void* DY, int64_t lddy, float* DR, int64_t lddr, int64_t M, int N, int act,
-                             float slope, int order, hipStream_t st) {
+hipError_t run_resid_act_bwd(const float* D, int64_t ldd, const float* D2, int64_t ldd2, const void* Y, int64_t ldy,
+                             int dtype, const float* R, int64_t ldr, void* DY, int64_t lddy, float* DR, int64_t lddr,
+                             int64_t M, int N, int act, float slope, int order, hipStream_t st) {
     if (M == 0 || N == 0) return hipSuccess;
-    if (dtype == SIR_DTYPE_F32)
-        return order ? resact_bwd_t<SIR_DTYPE_F32, 1>(act, D, ldd, Y, ldy, R, ldr, DY, lddy, DR, lddr, M, N, slope, st)
-                     : resact_bwd_t<SIR_DTYPE_F32, 0>(act, D, ldd, Y, ldy, R, ldr, DY, lddy, DR, lddr, M, N, slope, st);
-    if (dtype == SIR_DTYPE_BF16)
-        return order ? resact_bwd_t<SIR_DTYPE_BF16, 1>(act, D, ldd, Y, ldy, R, ldr, DY, lddy, DR, lddr, M, N, slope, st)
-                     : resact_bwd_t<SIR_DTYPE_BF16, 0>(act, D, ldd, Y, ldy, R, ldr, DY, lddy, DR, lddr, M, N, slope, st);
-    return order ? resact_bwd_t<SIR_DTYPE_F16, 1>(act, D, ldd, Y, ldy, R, ldr, DY, lddy, DR, lddr, M, N, slope, st)
-                 : resact_bwd_t<SIR_DTYPE_F16, 0>(act, D, ldd, Y, ldy, R, ldr, DY, lddy, DR, lddr, M, N, slope, st);
+#define SIR_RESACT_BWD(DTV, ORD) resact_bwd_t<DTV, ORD>(act, D, ldd, D2, ldd2, Y, ldy, R, ldr, DY, lddy, DR, lddr, M, N, slope, st)
+    if (dtype == SIR_DTYPE_F32) return order ? SIR_RESACT_BWD(SIR_DTYPE_F32, 1) : SIR_RESACT_BWD(SIR_DTYPE_F32, 0);
+    if (dtype == SIR_DTYPE_BF16) return order ? SIR_RESACT_BWD(SIR_DTYPE_BF16, 1) : SIR_RESACT_BWD(SIR_DTYPE_BF16, 0);
+    return order ? SIR_RESACT_BWD(SIR_DTYPE_F16, 1) : SIR_RESACT_BWD(SIR_DTYPE_F16, 0);
+#undef SIR_RESACT_BWD
 }
 
 }  // namespace sir

@@ -33,8 +33,8 @@ SIGNATURES = {
     "sir_graph_norm_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I64,
                                           _P, _P, _P, _P]),
     "sir_resid_act_fwd": (ctypes.c_int, [_P, _I64, _I, _P, _I64, _P, _I64, _I64, _I64, _I, _F, _I, _P]),
-    "sir_resid_act_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _F, _I,
-                                         _P]),
+    "sir_resid_act_bwd": (ctypes.c_int, [_P, _I64, _P, _I64, _P, _I64, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I,
+                                         _F, _I, _P]),
     "sir_graph_norm_act_fwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P, _F, _I, _F, _P, _I64, _P, _I64,
                                               _P, _P, _P]),
     "sir_graph_norm_act_bwd": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P, _I, _F, _P,
@@ -463,12 +463,14 @@ def resid_act_fwd(Y, R, act, slope, order, out):
     _check(rc, lib)
 
 
-def resid_act_bwd(D, Y, R, act, slope, order, dY, dR=None):
-    """Backward of :func:`resid_act_fwd` (``sir_resid_act_bwd``): dY in Y's type; order 0 also dR."""
+def resid_act_bwd(D, Y, R, act, slope, order, dY, dR=None, D2=None):
+    """Backward of :func:`resid_act_fwd` (``sir_resid_act_bwd``): dY in Y's type; order 0 also dR.  D2
+    (order 0): a second fp32 gradient of the output, added to D as it is read."""
     lib = load()
     M, N = Y.shape
     with _Timed("sir_resid_act_bwd", dY.device):
-        rc = lib.sir_resid_act_bwd(_ptr(D), D.stride(0), _ptr(Y), Y.stride(0), _DT_CODE[Y.dtype], _ptr(R),
+        rc = lib.sir_resid_act_bwd(_ptr(D), D.stride(0), _ptr(D2), D2.stride(0) if D2 is not None else 0,
+                                   _ptr(Y), Y.stride(0), _DT_CODE[Y.dtype], _ptr(R),
                                    R.stride(0) if R is not None else 0, _ptr(dY), dY.stride(0), _ptr(dR),
                                    dR.stride(0) if dR is not None else 0, M, N, int(act), float(slope), int(order),
                                    _stream(dY.device))

@@ -6,12 +6,14 @@ whose message runs a Linear on every edge, without any [E, *] tensor in the forw
   H, F <= 256 (the config-1 shape is H = F = 64; the DictionaryLookup sweep reaches H = F = 200,
   ``dictionary-lookup/README.md:8``).
 * ``agg_type='max'`` (``conv.py:46-47``: ``linear_relation`` per edge, DGL ``fn.max``):
-  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge) and three
-  backwards: the edge-materialised one by default (edge activations recomputed once into [E, H]
-  buffers, native gather / split-fp16 GEMM / segment kernels, over destination-row ranges past a memory
-  budget); the routed one (``sir_edge_max_bwd_sparse``, H <= 512, O <= 256, opt-in ``sparse_bwd``: the
-  (v, o) pairs grouped by their arg edge, dA_e from the W_R rows of e's routed outputs only, dW_R from
-  a_{arg} per (v, o) — V O H multiply-adds per product instead of E O H, no [E, *] tensor); the dense
+  :class:`EdgeMaxLinear` — fused forward (running max with the first arg-max edge) and four
+  backwards: the hybrid one by default where its routing table fits the memory budget (H <= 512,
+  O <= 256: dQ / dK from the routed passes of ``sir_edge_max_bwd_sparse`` — the (v, o) pairs grouped by
+  their arg edge, dA_e from the W_R rows of e's routed outputs only, V O H multiply-adds per product
+  instead of E O H — and dW_R / db_R from ``sir_max_dw_qk`` with the activations recomputed per row
+  batch: no [E, *] tensor); the edge-materialised one otherwise (edge activations recomputed once into
+  [E, H] buffers, native gather / split-fp16 GEMM / segment kernels, over destination-row ranges past
+  the budget); the fully routed one (opt-in ``sparse_bwd``: dW_R from a_{arg} per (v, o)); the dense
   fused one (fp32 MFMA, opt-in ``fused_bwd``).
 
 Under autocast (the reference trains its max configs with AMP, ``heterophilous-datasets/train.py:75``)
@@ -21,7 +23,9 @@ h = a W^T + b as one 16-bit MFMA per 16 k on W, b rounded to it, fp32 accumulati
 (``sir_edge_mlp_fwd*_st``, round 6); the max and its arg edge are taken over the fp32 h (the reference
 rounds h to 16 bits first: its ties among equal rounded values may pick another edge).  The max backward
 and the Sequential-sigma form widen Q, K to fp32 (a V-sized copy) and run the fp32 kernels — more accurate
-than the reference's 16-bit backward, not bit-level AMP parity (``tests/test_amp_gpu.py::
+than the reference's 16-bit backward, not bit-level AMP parity (the reference trains only its max and
+sym configs under AMP, ``heterophilous-datasets/train.py:191-223``; the Sequential sigma's
+DictionaryLookup runs in fp32) (``tests/test_amp_gpu.py::
 test_fused_edge_mlp_forms_under_autocast``).  A CPU tensor or a shape outside the kernels' limits is
 never silently served by another path — :func:`seq_sigma` / :func:`max_supported` say up front which
 form applies.

@@ -19,16 +19,27 @@ MI355X modules (tests, ``bench.py --workload``):
 from torch import nn
 
 
-def _resid_act(y, resid, activation, order):
+def _resid_act(y, resid, activation, order, r_link=None, out_link=None):
     """sirgcn.resact.resid_act for GPU tensors (imported lazily: the stack also runs the reference's
     own modules on the CPU, where it returns None)."""
     if not (getattr(y, "is_cuda", False) and getattr(resid, "is_cuda", False)):
         return None
     from .resact import resid_act
-    return resid_act(y, resid, activation, order)
+    return resid_act(y, resid, activation, order, r_link, out_link)
+
+
+def _new_link():
+    from .resact import GradLink
+    return GradLink()
 
 
 class SIRStack(nn.Module):
+    # zinc order on the fused residual pass: each layer's residual gradient handed to the previous
+    # layer's backward (sirgcn.resact.GradLink) instead of an autograd add.  The parameters' and the
+    # stack input's gradients are the same bits either way; a hook on (or torch.autograd.grad of) an
+    # intermediate layer output sees only its conv-input part — set False for that.
+    link_residual_grads = True
+
     def __init__(self, conv_cls, hidden, num_layers, activation, agg_type="sum", order="arxiv",
                  norm_cls=None, conv_activation=None, feat_dropout=0):
         super().__init__()
@@ -53,6 +64,7 @@ class SIRStack(nn.Module):
                 seeds = torch.randint(0, 2 ** 62, (len(drawing),), device=feats.device, dtype=torch.int64)
                 for j, c in enumerate(drawing):
                     c.step_seed = seeds[j:j + 1]
+        link = None          # the GradLink of feats when a fused zinc-order pass produced it
         for i, conv in enumerate(self.convs):
             if self.order == "plain":
                 feats = conv(graph, feats)
@@ -60,11 +72,17 @@ class SIRStack(nn.Module):
             resid = feats
             feats = conv(graph, feats)
             if self.norms is None:
-                # + resid and the activation in one pass when the operands allow (sirgcn.resact)
-                fused = _resid_act(feats, resid, self.activation, self.order)
+                # + resid and the activation in one pass when the operands allow (sirgcn.resact);
+                # zinc order: the residual gradient of each layer's input handed to the layer that
+                # produced it (resact.GradLink) instead of an autograd add
+                out_link = (_new_link() if self.link_residual_grads and self.order == "zinc"
+                            and getattr(feats, "is_cuda", False) else None)
+                fused = _resid_act(feats, resid, self.activation, self.order, link, out_link)
                 if fused is not None:
                     feats = fused
+                    link = out_link
                     continue
+            link = None
             if self.order == "zinc":
                 feats = feats + resid
             if self.norms is not None:
