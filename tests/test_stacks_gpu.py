@@ -295,6 +295,29 @@ def test_fused_norm_activation_residual_bit_identical(name, autocast, monkeypatc
         assert torch.equal(fused[2][k], plain[2][k]), k
 
 
+@pytest.mark.parametrize("autocast", [None, torch.bfloat16])
+def test_zinc_residual_grad_link(autocast, monkeypatch):
+    """cfg2's zinc-order stack hands each layer's residual gradient to the previous layer's fused residual
+    backward (sirgcn.resact.GradLink, D2 of sir_resid_act_bwd) instead of an autograd add: the link is used
+    by every layer but the first, and the output and every gradient are the same bits as with the
+    autograd add (SIRStack.link_residual_grads = False)."""
+    from sirgcn.stacks import SIRStack
+    g = make_graph("cfg2", small=True)
+    X, dY = make_inputs("cfg2", g.num_nodes(), DEV)
+    ours, _ = _stacks("cfg2")
+    used = []
+    orig = _native.resid_act_bwd
+    monkeypatch.setattr(_native, "resid_act_bwd",
+                        lambda *a, **k: used.append(k.get("D2") is not None) or orig(*a, **k))
+    linked = _run(ours, g, X, dY, autocast=autocast)
+    assert sorted(used) == [False] + [True] * (len(ours.convs) - 1), used
+    monkeypatch.setattr(SIRStack, "link_residual_grads", False)
+    plain = _run(ours, g, X, dY, autocast=autocast)
+    assert torch.equal(linked[0], plain[0]) and torch.equal(linked[1], plain[1])
+    for k in plain[2]:
+        assert torch.equal(linked[2][k], plain[2][k]), k
+
+
 @pytest.mark.parametrize("name", ["cfg1", "cfg5"])
 def test_small_batches_on_the_product_gemm_route(name, monkeypatch):
     """The product's own GEMM routing (linalg.MIN_ROWS / MIN_ROWS_16 at their defaults — the suite
