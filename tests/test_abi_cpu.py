@@ -77,6 +77,22 @@ def test_argument_checks_are_synchronous_and_reported():
     assert rc == 1 and b"perm" in lib.sir_last_error()
 
 
+def test_resid_act_argument_checks():
+    """sir_resid_act_bwd (ABI 16): the second gradient D2 is defined for order 0 only and needs 16-B rows."""
+    lib = _native.load()
+    n = _null()
+    buf = ctypes.create_string_buffer(256)
+    p = ctypes.c_void_p((ctypes.addressof(buf) + 15) & ~15)
+    # order 1 with D2
+    rc = lib.sir_resid_act_bwd(p, 4, p, 4, p, 4, 0, n, 0, p, 4, n, 0, 1, 4, 1, 0.0, 1, n)
+    assert rc == 1 and b"D2" in lib.sir_last_error()
+    # order 0 with a D2 leading dimension below N
+    rc = lib.sir_resid_act_bwd(p, 4, p, 2, p, 4, 0, p, 4, p, 4, p, 4, 1, 4, 1, 0.0, 0, n)
+    assert rc == 1 and b"D2" in lib.sir_last_error()
+    # empty work with D2 is a no-op
+    assert lib.sir_resid_act_bwd(p, 4, p, 4, p, 4, 0, p, 4, p, 4, p, 4, 0, 4, 1, 0.0, 0, n) == 0
+
+
 def test_gemm16_argument_checks():
     """sir_gemm_pack16 / sir_gemm_nt16 (the autocast projections): bad dtypes, shapes and
     alignments are rejected synchronously with a message; sizing returns 0 for bad shapes."""
