@@ -593,9 +593,12 @@ int sir_edge_max_bwd_dst(const int32_t* rowptr, const int32_t* col, const int32_
                   nullptr);
 }
 
+#ifndef SIR_MAXB_ROUTE_CAP
+#define SIR_MAXB_ROUTE_CAP 4096   // routing-table blocks (4 waves, ~12 KB of LDS each): 16 a CU in one round
+#endif
 static int64_t maxb_route_blocks(int64_t n_items) {
     const int64_t b = (n_items + 3) / 4;
-    return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+    return b < 1 ? 1 : (b > SIR_MAXB_ROUTE_CAP ? SIR_MAXB_ROUTE_CAP : b);
 }
 
 int sir_edge_max_bwd_sparse_parts(int64_t n_items_d, int64_t V, int64_t* route_blocks, int64_t* dw_ranges) {
