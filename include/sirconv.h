@@ -423,9 +423,10 @@ int sir_graph_norm_bwd(const int64_t* off, int64_t B, int64_t F, const float* X,
  * _LEAKY_RELU (slope).  The same ops, types and order as torch's add, relu / leaky_relu and their
  * autograd (a 16-bit activation rounds to its type, a 16-bit gradient is rounded once from fp32):
  * bit-identical to the separate torch kernels.  Backward: D = dout (fp32); dY in `dtype`; order 0
- * also writes dR = act'(Y + R) D (order 1: dR is D itself, DR ignored).  D2 (order 0, optional; ABI 16):
- * a second fp32 gradient of out, added to D as it is read — the residual gradient of the next layer,
- * whose input out is (the sum autograd would otherwise form in its own pass).  N % 4 == 0; rows 16-B
+ * also writes dR = act'(Y + R) D (order 1: dR is D itself, DR ignored).  D2 (optional; ABI 16): a
+ * second fp32 gradient of out, added to D as it is read — the residual gradient of the next layer,
+ * whose input out is (the sum autograd would otherwise form in its own pass); order 1 then writes that
+ * sum D + D2 to dR (required).  N % 4 == 0; rows 16-B
  * aligned (leading dimensions multiples of 4 elements).  ABI 13. */
 int sir_resid_act_fwd(const void* Y, int64_t ldy, int dtype, const float* R, int64_t ldr, float* out, int64_t ldo,
                       int64_t M, int64_t N, int act, float slope, int order, void* stream);

@@ -754,18 +754,19 @@ int sir_resid_act_bwd(const float* D, int64_t ldd, const float* D2, int64_t ldd2
     if (act != SIR_ACT_IDENTITY && act != SIR_ACT_RELU && act != SIR_ACT_LEAKY_RELU)
         return fail(SIR_EINVAL, fn, "act must be identity, relu or leaky_relu");
     if (order != 0 && order != 1) return fail(SIR_EINVAL, fn, "order must be 0 (zinc) or 1 (arxiv)");
-    if (D2 != nullptr && (order != 0 || ldd2 < N || ldd2 % 4 || !al16(D2)))
-        return fail(SIR_EINVAL, fn, "D2 (order 0 only): rows 16-B aligned, ldd2 >= N, ldd2 % 4 == 0");
-    if (ldd < N || ldy < N || lddy < N || ldd % 4 || ldy % 4 || lddy % 4 ||
-        (order == 0 && (ldr < N || ldr % 4 || (dR != nullptr && (lddr < N || lddr % 4)))))
+    if (D2 != nullptr && (ldd2 < N || ldd2 % 4 || !al16(D2) || (order == 1 && dR == nullptr)))
+        return fail(SIR_EINVAL, fn, "D2: rows 16-B aligned, ldd2 >= N, ldd2 % 4 == 0 (order 1: with dR for the sum)");
+    const bool want_dr = order == 0 || D2 != nullptr;        // order 1 writes dR only as the sum D + D2
+    if (ldd < N || ldy < N || lddy < N || ldd % 4 || ldy % 4 || lddy % 4 || (order == 0 && (ldr < N || ldr % 4)) ||
+        (want_dr && dR != nullptr && (lddr < N || lddr % 4)))
         return fail(SIR_EINVAL, fn, "leading dimensions must be >= N and multiples of 4");
     if (M > 0 && (D == nullptr || Y == nullptr || dY == nullptr || (order == 0 && R == nullptr)))
         return fail(SIR_EINVAL, fn, "NULL buffer");
     const bool y16 = dtype != SIR_DTYPE_F32;
     if (!al16(D) || (y16 ? (reinterpret_cast<uintptr_t>(Y) & 7u) || (reinterpret_cast<uintptr_t>(dY) & 7u)
-                         : !al16(Y) || !al16(dY)) || (order == 0 && (!al16(R) || !al16(dR))))
+                         : !al16(Y) || !al16(dY)) || (order == 0 && !al16(R)) || (want_dr && !al16(dR)))
         return fail(SIR_EINVAL, fn, "rows must be 16-B aligned (8-B for 16-bit Y, dY)");
-    return finish(fn, sir::run_resid_act_bwd(D, ldd, D2, ldd2, Y, ldy, dtype, R, ldr, dY, lddy, order == 0 ? dR : nullptr, lddr, M,
+    return finish(fn, sir::run_resid_act_bwd(D, ldd, D2, ldd2, Y, ldy, dtype, R, ldr, dY, lddy, want_dr ? dR : nullptr, lddr, M,
                                              (int)N, act, slope, order, static_cast<hipStream_t>(stream)), nullptr);
 }
 

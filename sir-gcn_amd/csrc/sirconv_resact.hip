@@ -100,7 +100,7 @@ k_resact_bwd(const float* __restrict__ D, int64_t ldd, const float* __restrict__
         const int64_t m = q / nq;
         const int n = (int)(q - m * nq) * 4;
         float4 d = *reinterpret_cast<const float4*>(D + m * ldd + n);
-        if (D2 != nullptr) {           // a second gradient of the output (order 0): the sum autograd would form
+        if (D2 != nullptr) {           // a second gradient of the output: the sum autograd would form
             const float4 d2 = *reinterpret_cast<const float4*>(D2 + m * ldd2 + n);
             d.x += d2.x; d.y += d2.y; d.z += d2.z; d.w += d2.w;
         }
@@ -127,6 +127,8 @@ k_resact_bwd(const float* __restrict__ D, int64_t ldd, const float* __restrict__
             // casts the add's fp32 gradient for the 16-bit operand), in opmath, rounded once more
 #pragma unroll
             for (int i = 0; i < 4; ++i) g[i] = act_b<ACT>(yv[i], E::up(E::down(dv[i])), slope);
+            // R's gradient is dout itself: written only when it is a sum formed here (D2)
+            if (D2 != nullptr && DR != nullptr) *reinterpret_cast<float4*>(DR + m * lddr + n) = d;
         }
         if constexpr (DT == SIR_DTYPE_F32) {
             *reinterpret_cast<float4*>(static_cast<float*>(DY) + m * lddy + n) = make_float4(g[0], g[1], g[2], g[3]);

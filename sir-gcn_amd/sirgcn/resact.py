@@ -8,11 +8,12 @@ Bit-identical to torch's separate add / activation kernels and their autograd (i
 autocast dtypes: a 16-bit conv output, an fp32 residual); replaces two kernels forward and two or
 three backward (the 16-bit gradient cast included).
 
-Chained zinc-order layers (:class:`GradLink`): layer i's output h is both the next layer's conv input
-and its residual, so autograd would add the two gradients of h in a pass of its own before layer i's
-backward reads them.  With a link the next layer's pass hands its residual gradient over instead of
-returning it, and layer i's backward adds it while reading the conv input's gradient (``D2`` of
-``sir_resid_act_bwd``): the same sum (a + b == b + a), one [V, H] pass and one launch fewer per layer.
+Chained layers (:class:`GradLink`): layer i's output h is both the next layer's conv input and its
+residual, so autograd would add the two gradients of h in a pass of its own before layer i's backward
+reads them.  With a link the next layer's pass hands its residual gradient over instead of returning
+it, and layer i's backward adds it while reading the conv input's gradient (``D2`` of
+``sir_resid_act_bwd``; arxiv order: the sum is also written once, as layer i's own residual gradient):
+the same sum (a + b == b + a), one launch and one or two [V, H] passes fewer per layer.
 """
 import torch
 from torch import nn
@@ -77,15 +78,24 @@ class ResidActFunction(torch.autograd.Function):
                 ctx.r_link.put(dR)
                 dR = None
             return dY, dR, None, None, None, None, None
-        _native.resid_act_bwd(D, Y, None, ctx.act, ctx.slope, 1, dY)
-        return dY, D, None, None, None, None, None
+        D2 = ctx.out_link.take() if ctx.out_link is not None else None
+        if D2 is not None:              # R's gradient is dout: the sum D + D2, formed by the pass
+            dR = torch.empty(Y.shape, device=Y.device, dtype=torch.float32)
+            _native.resid_act_bwd(D, Y, None, ctx.act, ctx.slope, 1, dY, dR, D2=D2)
+        else:
+            _native.resid_act_bwd(D, Y, None, ctx.act, ctx.slope, 1, dY)
+            dR = D
+        if ctx.r_link is not None and ctx.needs_input_grad[1]:
+            ctx.r_link.put(dR)
+            dR = None
+        return dY, dR, None, None, None, None, None
 
 
 def resid_act(y, resid, activation, order, r_link=None, out_link=None):
     """``activation(y + resid)`` (order "zinc") or ``activation(y) + resid`` ("arxiv") in one pass,
     or None when the activation / operands are not the native pass's (or a hook waits on the
     activation's call): the caller then runs the torch ops itself.  ``r_link`` / ``out_link``
-    (zinc order; :class:`GradLink`): ``resid`` is the output of the layer that holds ``r_link`` as
+    (:class:`GradLink`): ``resid`` is the output of the layer that holds ``r_link`` as
     its ``out_link`` — the residual gradient goes there instead of through autograd; ``out_link``
     receives the next layer's."""
     code = act_code(activation)
@@ -95,6 +105,4 @@ def resid_act(y, resid, activation, order, r_link=None, out_link=None):
             or y.shape[1] % 4 != 0 or not _ok(y, (torch.float32, torch.bfloat16, torch.float16))
             or not _ok(resid, (torch.float32,))):
         return None
-    if order != "zinc":
-        r_link = out_link = None
     return ResidActFunction.apply(y, resid, code[0], code[1], 0 if order == "zinc" else 1, r_link, out_link)

@@ -34,8 +34,8 @@ def _new_link():
 
 
 class SIRStack(nn.Module):
-    # zinc order on the fused residual pass: each layer's residual gradient handed to the previous
-    # layer's backward (sirgcn.resact.GradLink) instead of an autograd add.  The parameters' and the
+    # the fused residual pass (no norm): each layer's residual gradient handed to the previous layer's
+    # backward (sirgcn.resact.GradLink) instead of an autograd add.  The parameters' and the
     # stack input's gradients are the same bits either way; a hook on (or torch.autograd.grad of) an
     # intermediate layer output sees only its conv-input part — set False for that.
     link_residual_grads = True
@@ -64,7 +64,7 @@ class SIRStack(nn.Module):
                 seeds = torch.randint(0, 2 ** 62, (len(drawing),), device=feats.device, dtype=torch.int64)
                 for j, c in enumerate(drawing):
                     c.step_seed = seeds[j:j + 1]
-        link = None          # the GradLink of feats when a fused zinc-order pass produced it
+        link = None          # the GradLink of feats when a fused residual pass produced it
         for i, conv in enumerate(self.convs):
             if self.order == "plain":
                 feats = conv(graph, feats)
@@ -73,10 +73,9 @@ class SIRStack(nn.Module):
             feats = conv(graph, feats)
             if self.norms is None:
                 # + resid and the activation in one pass when the operands allow (sirgcn.resact);
-                # zinc order: the residual gradient of each layer's input handed to the layer that
-                # produced it (resact.GradLink) instead of an autograd add
-                out_link = (_new_link() if self.link_residual_grads and self.order == "zinc"
-                            and getattr(feats, "is_cuda", False) else None)
+                # the residual gradient of each layer's input handed to the layer that produced it
+                # (resact.GradLink) instead of an autograd add
+                out_link = _new_link() if self.link_residual_grads and getattr(feats, "is_cuda", False) else None
                 fused = _resid_act(feats, resid, self.activation, self.order, link, out_link)
                 if fused is not None:
                     feats = fused

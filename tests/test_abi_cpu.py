@@ -78,12 +78,13 @@ def test_argument_checks_are_synchronous_and_reported():
 
 
 def test_resid_act_argument_checks():
-    """sir_resid_act_bwd (ABI 16): the second gradient D2 is defined for order 0 only and needs 16-B rows."""
+    """sir_resid_act_bwd (ABI 16): the second gradient D2 needs 16-B rows, and in order 1 the dR buffer that
+    receives the sum D + D2."""
     lib = _native.load()
     n = _null()
     buf = ctypes.create_string_buffer(256)
     p = ctypes.c_void_p((ctypes.addressof(buf) + 15) & ~15)
-    # order 1 with D2
+    # order 1 with D2 but no dR
     rc = lib.sir_resid_act_bwd(p, 4, p, 4, p, 4, 0, n, 0, p, 4, n, 0, 1, 4, 1, 0.0, 1, n)
     assert rc == 1 and b"D2" in lib.sir_last_error()
     # order 0 with a D2 leading dimension below N

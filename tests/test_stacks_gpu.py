@@ -295,16 +295,21 @@ def test_fused_norm_activation_residual_bit_identical(name, autocast, monkeypatc
         assert torch.equal(fused[2][k], plain[2][k]), k
 
 
-@pytest.mark.parametrize("autocast", [None, torch.bfloat16])
-def test_zinc_residual_grad_link(autocast, monkeypatch):
-    """cfg2's zinc-order stack hands each layer's residual gradient to the previous layer's fused residual
-    backward (sirgcn.resact.GradLink, D2 of sir_resid_act_bwd) instead of an autograd add: the link is used
-    by every layer but the first, and the output and every gradient are the same bits as with the
-    autograd add (SIRStack.link_residual_grads = False)."""
+@pytest.mark.parametrize("name,autocast", [("cfg2", None), ("cfg2", torch.bfloat16), ("cfg3", None),
+                                           ("cfg3", torch.bfloat16)])
+def test_residual_grad_link(name, autocast, monkeypatch):
+    """The stacks without a norm (cfg2's zinc order act(conv(h) + h), cfg3's arxiv order act(conv(h)) + h)
+    hand each layer's residual gradient to the previous layer's fused residual backward
+    (sirgcn.resact.GradLink, D2 of sir_resid_act_bwd) instead of an autograd add: the link is used by every
+    layer but the first, and the output and every gradient are the same bits as with the autograd add
+    (SIRStack.link_residual_grads = False)."""
     from sirgcn.stacks import SIRStack
-    g = make_graph("cfg2", small=True)
-    X, dY = make_inputs("cfg2", g.num_nodes(), DEV)
-    ours, _ = _stacks("cfg2")
+    g = make_graph(name, small=True)
+    X, dY = make_inputs(name, g.num_nodes(), DEV)
+    ours, _ = _stacks(name)
+    for m in ours.modules():          # dropout off: the two runs must draw nothing
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
     used = []
     orig = _native.resid_act_bwd
     monkeypatch.setattr(_native, "resid_act_bwd",
