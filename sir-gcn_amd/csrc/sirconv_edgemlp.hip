@@ -90,6 +90,26 @@ __device__ __forceinline__ int mlp_fimg(int row, int h) { return ((row >> 5) << 
 #ifndef SIR_MLP_SWZ
 #define SIR_MLP_SWZ 1
 #endif
+#ifndef SIR_MLP_SPLIT_MIX
+#define SIR_MLP_SPLIT_MIX 1     // stream forward staging: hi / lo split by v_fma_mix (2 VALU per element)
+#endif
+// hi = fp16(x s), lo = fp16(x s - hi) of 4 floats (s an exact power of two), one v_fma_mix each into the
+// halves of the packed registers: x s is exact and x s - hi exact inside the fused op, so the bits are
+// those of rounding y = x s and y - hi separately.  s_nop 1: VALU-write wait states the hazard recognizer
+// does not see inside inline asm.
+__device__ inline void split4_mix(float4 a, float s, uint2& hi, uint2& lo) {
+    uint32_t h0, h1, l0, l1;
+    asm volatile(
+        "v_fma_mixlo_f16 %0, %4, %8, 0\n\tv_fma_mixhi_f16 %0, %5, %8, 0\n\t"
+        "v_fma_mixlo_f16 %1, %6, %8, 0\n\tv_fma_mixhi_f16 %1, %7, %8, 0\n\t"
+        "v_fma_mixlo_f16 %2, %4, %8, -%0 op_sel_hi:[0,0,1]\n\tv_fma_mixhi_f16 %2, %5, %8, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixlo_f16 %3, %6, %8, -%1 op_sel_hi:[0,0,1]\n\tv_fma_mixhi_f16 %3, %7, %8, -%1 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "s_nop 1"
+        : "=&v"(h0), "=&v"(h1), "=&v"(l0), "=&v"(l1)
+        : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(s));
+    hi = make_uint2(h0, h1);
+    lo = make_uint2(l0, l1);
+}
 __device__ __forceinline__ int mlp_fimg_sw(int row, int h, int g) {
     return (h << 9) + (((row & 31) << 4) ^ (SIR_MLP_SWZ ? ((h << 4) | ((g & 3) << 5)) : 0));
 }
@@ -860,12 +880,19 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
             const float m = wave_max64(fmaxf(fmaxf(fabsf(a4.x), fabsf(a4.y)), fmaxf(fabsf(a4.z), fabsf(a4.w))));
             const int se = mlp_scale_exp(m);
             const float sc = mlp_pow2(se);
-            const float y[4] = {a4.x * sc, a4.y * sc, a4.z * sc, a4.w * sc};
-            _Float16 hv[4], lv[4];
+            if constexpr (SIR_MLP_SPLIT_MIX) {
+                uint2 hv, lv;
+                split4_mix(a4, sc, hv, lv);
+                *reinterpret_cast<uint2*>(d) = hv;
+                *reinterpret_cast<uint2*>(d + 1024) = lv;
+            } else {
+                const float y[4] = {a4.x * sc, a4.y * sc, a4.z * sc, a4.w * sc};
+                _Float16 hv[4], lv[4];
 #pragma unroll
-            for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
-            *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
-            *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
+                for (int x = 0; x < 4; ++x) { hv[x] = (_Float16)y[x]; lv[x] = (_Float16)(y[x] - (float)hv[x]); }
+                *reinterpret_cast<uint2*>(d) = __builtin_bit_cast(uint2, hv);
+                *reinterpret_cast<uint2*>(d + 1024) = __builtin_bit_cast(uint2, lv);
+            }
             if (l == 0) sInv[bf][i] = mlp_pow2(-se);
         }
         if (w == 0 && l < 32) sC[bf][l] = (l < nv) ? ((RED == AGG_SYM) ? cn : 1.f) : 0.f;
