@@ -432,14 +432,19 @@ def run_edge_cut(args, world, rank, dev, rehearsal, torch, dist, nn):
                                  edges_local, H, args.agg, masked, s)
     if "sir_edge_mlp_fwd" in kernels:      # max: the per-edge W_R GEMM bounds the dominant kernel
         k = kernels["sir_edge_mlp_fwd"]
-        # split-fp16 MFMA (k_mlp_fwd16: 3 fp16 MFMAs per fp32-accurate product): the peak in
-        # fp32-equivalent flops is the dense fp16 peak / 3; the fp32-MFMA peak is given beside it
-        peak = FP16_PEAK_FLOPS / 3 / 1e12
-        out["roofline"] = {"bound": "mfma", "kernel": "sir_edge_mlp_fwd (gather -> sigma -> split-fp16 MFMA W_R -> running max)",
+        # fp32: split-fp16 MFMA (3 fp16 MFMAs per fp32-accurate product): the peak in fp32-equivalent
+        # flops is the dense fp16 peak / 3.  Under autocast the 16-bit forward (sir_edge_mlp_fwd*_st)
+        # runs ONE 16-bit MFMA per product: its peak is the dense 16-bit peak itself.
+        from sirgcn import edgemlp
+        per = 1 if (dtn in ("bf16", "f16") and edgemlp.NATIVE_16) else 3
+        peak = FP16_PEAK_FLOPS / per / 1e12
+        form = "one 16-bit MFMA per product" if per == 1 else "split-fp16 MFMA, 3 per product"
+        out["roofline"] = {"bound": "mfma", "kernel": f"sir_edge_mlp_fwd (gather -> sigma -> {form} W_R -> running max)",
                            "achieved": k["TFLOPs"], "peak": round(peak, 1), "unit": "TFLOP/s",
                            "frac": round(k["TFLOPs"] / peak, 4), "traffic": None,
-                           "flops_formula": "2 * E * H * O per launch (fp32-equivalent; 3 v_mfma_f32_32x32x16_f16 per product)",
-                           "fp16_mfma_util": round(3 * k["TFLOPs"] * 1e12 / FP16_PEAK_FLOPS, 4),
+                           "flops_formula": f"2 * E * H * O per launch ({'16-bit' if per == 1 else 'fp32-equivalent'}; "
+                                            f"{per} v_mfma_f32_32x32x16 per product)",
+                           "fp16_mfma_util": round(per * k["TFLOPs"] * 1e12 / FP16_PEAK_FLOPS, 4),
                            "vs_fp32_mfma_peak": round(k["TFLOPs"] / FP32_PEAK_TFLOPS, 4),
                            "ms_per_launch": k["ms"]}
     else:
