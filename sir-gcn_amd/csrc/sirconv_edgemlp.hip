@@ -90,6 +90,9 @@ __device__ __forceinline__ int mlp_fimg(int row, int h) { return ((row >> 5) << 
 #ifndef SIR_MLP_SWZ
 #define SIR_MLP_SWZ 1
 #endif
+#ifndef SIR_MLP_SPLIT_WALK
+#define SIR_MLP_SPLIT_WALK 1    // stream max forward: interior tiles walked by both half-waves (16 edges each)
+#endif
 #ifndef SIR_MLP_SPLIT_MIX
 #define SIR_MLP_SPLIT_MIX 1     // stream forward staging: hi / lo split by v_fma_mix (2 VALU per element)
 #endif
@@ -951,12 +954,6 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): this wave's tile writes done
         __builtin_amdgcn_wave_barrier();
-        float mv[32];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const float4 v = *reinterpret_cast<const float4*>(mw + (l & 31) * MP + 4 * q);
-            mv[4 * q + 0] = v.x; mv[4 * q + 1] = v.y; mv[4 * q + 2] = v.z; mv[4 * q + 3] = v.w;
-        }
         const int next_first = (j + 1 < T) ? __builtin_amdgcn_readlane(rowv1, 0) : row_after;
         // run ends of the tile as one ballot (bit e: edge e is the last of its row's run here): the row
         // changes after it, or the block ends there
@@ -964,6 +961,83 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
         const int r_next = __shfl(rowv0, (li + 1) & 31);
         const bool end_l = li < nv && ((li + 1 < nv ? r_next : next_first) != rowv0 || (li + 1 == nv && t0 + nv == ee));
         const uint32_t bnd = (uint32_t)__builtin_amdgcn_ballot_w64(l < 32 && end_l);
+        if constexpr (RED == 3 && SIR_MLP_SPLIT_WALK) {
+            if (!first_run && t0 + 32 < ee) {
+                // max over a full interior tile (no block-boundary slot can end here): the two half-waves
+                // walk edges 0-15 and 16-31 of the same features.  Half 1's first run may have begun in
+                // half 0 (or earlier), so its result waits for half 0's trailing state; max with the
+                // first arg-max edge merges exactly (strict >: ties keep the earlier half), so the
+                // values and arg edges are those of the one-lane walk.
+                const int h = l >> 5;
+                float mh[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = *reinterpret_cast<const float4*>(mw + li * MP + 16 * h + 4 * q);
+                    mh[4 * q + 0] = v.x; mh[4 * q + 1] = v.y; mh[4 * q + 2] = v.z; mh[4 * q + 3] = v.w;
+                }
+                const uint32_t bh = bnd >> (16 * h);
+                const int eb = (int)t0 + 16 * h;
+                float hb_ = h ? -INFINITY : best;
+                int hi_ = h ? INT_MAX : bidx;
+                float pb = -INFINITY;                 // half 1: its first run, held back
+                int pi = INT_MAX, pr = 0;
+                bool seen = false;
+                const bool fo_n = n < F;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float v = mh[i];
+                    const bool take = v > hb_;
+                    hb_ = take ? v : hb_;
+                    hi_ = take ? eb + i : hi_;
+                    // the rows of edges i and 16 + i by readlane (read whatever the EXEC mask: a cross-lane
+                    // read inside the divergent branch would see the other half's lanes disabled)
+                    const int re0 = __builtin_amdgcn_readlane(rowv0, i);
+                    const int re1 = __builtin_amdgcn_readlane(rowv0, 16 + i);
+                    if ((bh >> i) & 1u) {
+                        const int re = h ? re1 : re0;
+                        if (h == 1 && !seen) {
+                            pb = hb_; pi = hi_; pr = re;
+                        } else if (fo_n) {
+                            const bool any = hi_ != INT_MAX;
+                            out[(int64_t)re * ldo + n] = any ? hb_ : 0.f;
+                            arg[(int64_t)re * lda + n] = any ? hi_ : -1;
+                        }
+                        seen = true;
+                        hb_ = -INFINITY;
+                        hi_ = INT_MAX;
+                    }
+                }
+                // half 0's trailing state <-> half 1's
+                const float ob = __shfl_xor(hb_, 32);
+                const int oi = __shfl_xor(hi_, 32);
+                if (h == 1 && (bh & 0xffffu) != 0u) {                 // half 1 had a run end: its first
+                    const bool t1 = pb > ob;                         // run continues half 0's trailing one
+                    const float mb = t1 ? pb : ob;
+                    const int mi = t1 ? pi : oi;
+                    if (fo_n) {
+                        const bool any = mi != INT_MAX;
+                        out[(int64_t)pr * ldo + n] = any ? mb : 0.f;
+                        arg[(int64_t)pr * lda + n] = any ? mi : -1;
+                    }
+                }
+                // the carry into the next tile (both halves): half 1's trailing run, or, without a run end
+                // in half 1, half 0's trailing run continued through half 1
+                const float b0 = h ? ob : hb_, b1 = h ? hb_ : ob;
+                const int i0 = h ? oi : hi_, i1 = h ? hi_ : oi;
+                const bool end1 = (bnd >> 16) != 0u;
+                const bool t1 = end1 || b1 > b0;
+                best = t1 ? b1 : b0;
+                bidx = t1 ? i1 : i0;
+                goto tile_done;
+            }
+        }
+        {
+        float mv[32];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(mw + (l & 31) * MP + 4 * q);
+            mv[4 * q + 0] = v.x; mv[4 * q + 1] = v.y; mv[4 * q + 2] = v.z; mv[4 * q + 3] = v.w;
+        }
         // ---- walk the tile's edges in order; a run of equal rows ends where the row changes
 #pragma unroll
         for (int e = 0; e < 32; ++e) {
@@ -1009,6 +1083,8 @@ k_mlp_fwd16r(const int* __restrict__ col, const int* __restrict__ erow, const in
                 }
             }
         }
+        }
+    tile_done:
         __syncthreads();
         colv0 = colv1; rowv0 = rowv1;
         colv1 = colv2; rowv1 = rowv2;
