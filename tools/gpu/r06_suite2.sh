@@ -2,7 +2,7 @@
 # round-6: smoke + the whole -m gpu suite on the final build
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/final6b
+O=${O:-gpurun_out/final6b}
 mkdir -p $O
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
